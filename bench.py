@@ -1,0 +1,164 @@
+#!/usr/bin/env python3
+"""Headline benchmark: smart-reply serving throughput on MI355X.
+
+Metric (BASELINE.json): "smart-reply tokens/sec (whole node) + p50 suggestion
+latency, Llama-3-8B TP=1".
+
+Workload per GPU (one engine replica per GPU, DP over the node = weak
+scaling): each timed *step* serves ``--batch`` smart-reply requests end to
+end through the continuous-batching engine - tokenization of the reference's
+smart-reply prompt over a synthetic 5-message channel history, one packed
+varlen prefill, then hipGraph-replayed decode steps until every request has
+produced ``--max-new-tokens`` tokens (EOS ignored: random-init weights never
+stop on their own; the reference's contract is 3 lines of < 10 words).
+Sampling uses the hosted backend's defaults (temperature 1.0, top-k 64,
+top-p 0.95) through the fused HIP sampler.
+
+``value`` = generated tokens / s over all ranks (max wall time over ranks);
+``p50_latency_ms`` = median request latency (arrival -> last token).
+
+Launch: ``python bench.py`` (1 GPU) or torchrun with --gpus N.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+from drtc_amd.engine import ChatTokenizer, LLMEngine, Request, SamplingParams  # noqa: E402
+from drtc_amd.llm.prompts import smart_reply_prompt  # noqa: E402
+from drtc_amd.models import TransformerLM, get_config  # noqa: E402
+from drtc_amd.parallel import init_distributed  # noqa: E402
+from drtc_amd.utils.synthetic import smart_reply_workload  # noqa: E402
+
+METRIC = "smart-reply tokens/sec (whole node) + p50 suggestion latency, Llama-3-8B TP=1"
+
+
+def log(rank: int, *a) -> None:
+    if rank == 0:
+        print("[bench]", *a, file=sys.stderr, flush=True)
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--model", default="llama-3-8b")
+    ap.add_argument("--batch", type=int, default=256, help="smart-reply requests per GPU per step")
+    ap.add_argument("--max-new-tokens", type=int, default=48)
+    ap.add_argument("--history", type=int, default=5)
+    ap.add_argument("--greedy", action="store_true")
+    ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--max-model-len", type=int, default=2048)
+    args = ap.parse_args()
+
+    rank, world = init_distributed()
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if torch.cuda.is_available():
+        torch.cuda.set_device(local)
+        device = torch.device("cuda", local)
+    else:
+        device = torch.device("cpu")
+    if world != args.gpus:
+        log(rank, f"warning: --gpus {args.gpus} but WORLD_SIZE {world}")
+
+    cfg = get_config(args.model)
+    t0 = time.perf_counter()
+    model = TransformerLM(cfg, device, seed=1234, full_then_shard=False)
+    eng = LLMEngine(model, max_batch=args.batch, max_model_len=args.max_model_len,
+                    max_prefill_tokens=max(16384, args.batch * 400),
+                    use_graphs=not args.no_graphs, seed=rank)
+    eng.warmup(capture=True)
+    if device.type == "cuda":
+        torch.cuda.synchronize()
+    log(rank, f"model {cfg.name} {model.weight_bytes() / 1e9:.1f} GB, kv {eng.kv.bytes / 1e9:.1f} GB "
+              f"({eng.kv.capacity_tokens} tokens), init {time.perf_counter() - t0:.1f}s")
+
+    tok = ChatTokenizer(cfg.vocab_size, cfg.bos_token_id, cfg.eos_token_id)
+    params = (SamplingParams.greedy(args.max_new_tokens, ignore_eos=True) if args.greedy else
+              SamplingParams(max_new_tokens=args.max_new_tokens, temperature=1.0, top_k=64,
+                             top_p=0.95, ignore_eos=True))
+
+    def make_prompts(step: int) -> list[list[int]]:
+        hist = smart_reply_workload(args.batch, seed=rank * 100003 + step, history=args.history)
+        return [tok.encode(smart_reply_prompt(h)) for h in hist]
+
+    def serve(prompts):
+        reqs = [eng.add_request(Request(p, params)) for p in prompts]
+        while eng.has_work():
+            eng.step()
+        return reqs
+
+    for w in range(args.warmup):
+        serve(make_prompts(-1 - w))
+    prompts = [make_prompts(s) for s in range(args.steps)]
+    prompt_tokens = sum(len(p) for ps in prompts for p in ps)
+
+    if world > 1:
+        dist.barrier()
+    if device.type == "cuda":
+        torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    lat, gen = [], 0
+    for s in range(args.steps):
+        reqs = serve(prompts[s])
+        lat.extend(r.latency for r in reqs)
+        gen += sum(len(r.output_ids) for r in reqs)
+    if device.type == "cuda":
+        torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t_start
+
+    p50 = statistics.median(lat)
+    stats = torch.tensor([elapsed, float(gen), float(prompt_tokens), p50], dtype=torch.float64,
+                         device=device)
+    if world > 1:
+        mx = stats.clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        sm = stats.clone()
+        dist.all_reduce(sm, op=dist.ReduceOp.SUM)
+        elapsed, p50 = float(mx[0]), float(mx[3])
+        gen, prompt_tokens = float(sm[1]), float(sm[2])
+    tps = gen / elapsed
+    if rank == 0:
+        out = {
+            "metric": METRIC,
+            "value": round(tps, 1),
+            "unit": "tokens/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(1000 * elapsed / args.steps, 2),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic chat logs (5-message smart-reply contexts), random-init weights",
+            "config": {"model": cfg.name, "global_batch": args.batch * world,
+                       "seq_len": args.max_new_tokens, "parallelism": f"dp{world}",
+                       "max_new_tokens": args.max_new_tokens,
+                       "avg_prompt_tokens": round(prompt_tokens / (args.batch * world * args.steps), 1),
+                       "sampling": "greedy" if args.greedy else "t=1.0,top_k=64,top_p=0.95",
+                       "graphs": not args.no_graphs},
+            "p50_latency_ms": round(1000 * p50, 1),
+            "total_tokens_per_s": round((gen + prompt_tokens) / elapsed, 1),
+            "engine_stats": dict(eng.stats),
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,268 @@
+// Paged decode attention on MFMA (gfx950): one query token per sequence
+// against a paged KV cache, GQA/MQA-aware.
+//
+// Work decomposition
+//   grid = (B * Hkv, max_partitions); one 256-thread workgroup (4 waves) per
+//   (sequence, kv head, context partition).  All G = Hq/Hkv query heads that
+//   share a kv head are processed together, so every K/V byte is read from
+//   HBM once per step.  Waves take the partition's 32-token cache blocks
+//   round-robin, keep an online softmax each, and merge through LDS; when a
+//   sequence spans several partitions the fp32 partials are merged by
+//   `decode_reduce_kernel` (flash-decoding split-K).
+//
+// MFMA formulation (16x16x32 bf16, operand maps in common.h)
+//   S^T[tok, head] = K[tok, :] . Q[head, :]    A = K rows (16-B loads straight
+//                                             from the token-major K block),
+//                                             B = Q^T (registers, whole step)
+//   O^T[d, head]  += V^T[d, tok] . P^T[tok, head]
+//   The S^T accumulators of the two 16-token halves of a block are fed back
+//   as the P^T B-operand with NO lane movement: lane l (g = l>>4) holds tokens
+//   {4g..4g+3} and {16+4g..16+4g+3}; the V^T A-operand is loaded with the
+//   same token permutation from the dim-major V block (two 8-B loads).
+//   Columns are query heads: G <= 16 (Llama-3 4, 70B 8, Gemma-2B 8).
+#include "common.h"
+#include "launchers.h"
+
+namespace drtc {
+
+constexpr int kBS = 32;  // tokens per KV-cache block (fixed by the layout)
+
+template <int D>
+struct KVRegs {
+  bf16x8 k0[D / 32], k1[D / 32];  // tokens 0..15 / 16..31 of the block
+  bf16x4 vlo[D / 16], vhi[D / 16];
+};
+
+template <int D>
+DRTC_DEVICE void load_kv_block(KVRegs<D>& r, const bf16_t* kb, const bf16_t* vb,
+                               int lane) {
+  const int t = lane & 15, g = lane >> 4;
+#pragma unroll
+  for (int s = 0; s < D / 32; ++s) {
+    r.k0[s] = load_bf16x8(kb + t * D + 32 * s + 8 * g);
+    r.k1[s] = load_bf16x8(kb + (16 + t) * D + 32 * s + 8 * g);
+  }
+#pragma unroll
+  for (int i = 0; i < D / 16; ++i) {
+    const bf16_t* vrow = vb + (16 * i + t) * kBS;
+    r.vlo[i] = load_bf16x4(vrow + 4 * g);
+    r.vhi[i] = load_bf16x4(vrow + 16 + 4 * g);
+  }
+}
+
+template <int D>
+__global__ __launch_bounds__(256, 2) void paged_decode_kernel(
+    bf16_t* __restrict__ out, float* __restrict__ part_o,
+    float* __restrict__ part_ml, const bf16_t* __restrict__ q, int q_stride,
+    const bf16_t* __restrict__ k_cache, const bf16_t* __restrict__ v_cache,
+    const int* __restrict__ block_tables, int bt_stride,
+    const int* __restrict__ context_lens, int Hq, int Hkv, float scale_log2e,
+    int max_parts, int blocks_per_part) {
+  constexpr int NT = D / 16;  // output d-tiles
+  constexpr int KS = D / 32;  // k-steps of the QK product
+  const int b = blockIdx.x / Hkv;
+  const int h = blockIdx.x - b * Hkv;
+  const int p = blockIdx.y;
+  const int G = Hq / Hkv;
+  const int ctx = context_lens[b];
+  const int nblk = (ctx + kBS - 1) / kBS;
+  const int nparts = (nblk + blocks_per_part - 1) / blocks_per_part;
+  const int lane = threadIdx.x & 63;
+  const int w = wave_id_uniform();
+  const int col = lane & 15, g = lane >> 4;
+
+  if (ctx <= 0) {  // padded batch slot: deterministic zeros, no cache reads
+    if (p == 0)
+      for (int i = threadIdx.x; i < G * D; i += 256)
+        out[(int64_t)b * Hq * D + (int64_t)h * G * D + i] = f2bf(0.f);
+    return;
+  }
+  if (p >= nparts) return;
+
+  const int blk_begin = p * blocks_per_part;
+  const int blk_end = min(nblk, blk_begin + blocks_per_part);
+
+  // Q^T B-operand fragments (zero for padding columns col >= G).
+  bf16x8 qf[KS];
+  const bf16_t* qrow = q + (int64_t)b * q_stride + (int64_t)(h * G + col) * D;
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    if (col < G) qf[s] = load_bf16x8(qrow + 32 * s + 8 * g);
+    else for (int j = 0; j < 8; ++j) qf[s][j] = f2bf(0.f);
+  }
+
+  f32x4 o[NT];
+#pragma unroll
+  for (int i = 0; i < NT; ++i) o[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  float m = kNegBig, lsum = 0.f;
+
+  const int* bt = block_tables + (int64_t)b * bt_stride;
+  const int64_t blk_elems = (int64_t)kBS * D;
+  KVRegs<D> cur, nxt;
+  int blk = blk_begin + w;
+  if (blk < blk_end) {
+    const int64_t phys = bt[blk];
+    load_kv_block<D>(cur, k_cache + (phys * Hkv + h) * blk_elems,
+                     v_cache + (phys * Hkv + h) * blk_elems, lane);
+  }
+  for (; blk < blk_end; blk += 4) {
+    const int nb = blk + 4;
+    if (nb < blk_end) {  // register double-buffer: next block in flight
+      const int64_t phys = bt[nb];
+      load_kv_block<D>(nxt, k_cache + (phys * Hkv + h) * blk_elems,
+                       v_cache + (phys * Hkv + h) * blk_elems, lane);
+    }
+    f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      s0 = mfma16(cur.k0[s], qf[s], s0);
+      s1 = mfma16(cur.k1[s], qf[s], s1);
+    }
+    const int tok0 = blk * kBS + 4 * g;
+    float bmax = kNegBig;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      s0[r] = (tok0 + r < ctx) ? s0[r] * scale_log2e : kNegBig;
+      s1[r] = (tok0 + 16 + r < ctx) ? s1[r] * scale_log2e : kNegBig;
+      bmax = fmaxf(bmax, fmaxf(s0[r], s1[r]));
+    }
+    bmax = fmaxf(bmax, __shfl_xor(bmax, 16, 64));
+    bmax = fmaxf(bmax, __shfl_xor(bmax, 32, 64));
+    const float m_new = fmaxf(m, bmax);
+    const float alpha = fast_exp2(m - m_new);
+    m = m_new;
+    bf16x8 pf;
+    float psum = 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float p0 = fast_exp2(s0[r] - m_new);
+      const float p1 = fast_exp2(s1[r] - m_new);
+      psum += p0 + p1;
+      pf[r] = f2bf(p0);
+      pf[4 + r] = f2bf(p1);
+    }
+    lsum = lsum * alpha + psum;
+#pragma unroll
+    for (int i = 0; i < NT; ++i) {
+      o[i] *= alpha;
+      bf16x8 a;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        a[j] = cur.vlo[i][j];
+        a[4 + j] = cur.vhi[i][j];
+      }
+      o[i] = mfma16(a, pf, o[i]);
+    }
+    if (nb < blk_end) cur = nxt;
+  }
+  lsum += __shfl_xor(lsum, 16, 64);
+  lsum += __shfl_xor(lsum, 32, 64);
+
+  // ---- merge the 4 waves through LDS
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* sm_m = smem;              // [4][16]
+  float* sm_l = smem + 64;         // [4][16]
+  float* sm_o = smem + 128;        // [4][D][16]
+  if (lane < 16) {
+    sm_m[w * 16 + lane] = m;
+    sm_l[w * 16 + lane] = lsum;
+  }
+#pragma unroll
+  for (int i = 0; i < NT; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      sm_o[(w * D + 16 * i + 4 * g + r) * 16 + col] = o[i][r];
+  __syncthreads();
+
+  const bool single = (nparts == 1);
+  for (int item = threadIdx.x; item < G * D; item += 256) {
+    const int hh = item / D;
+    const int d = item - hh * D;
+    float M = kNegBig;
+#pragma unroll
+    for (int ww = 0; ww < 4; ++ww) M = fmaxf(M, sm_m[ww * 16 + hh]);
+    float L = 0.f, O = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < 4; ++ww) {
+      const float f = fast_exp2(sm_m[ww * 16 + hh] - M);
+      L += sm_l[ww * 16 + hh] * f;
+      O += sm_o[(ww * D + d) * 16 + hh] * f;
+    }
+    const int hq = h * G + hh;
+    if (single) {
+      out[((int64_t)b * Hq + hq) * D + d] = f2bf(O / L);
+    } else {
+      const int64_t pi = ((int64_t)b * Hq + hq) * max_parts + p;
+      part_o[pi * D + d] = O;
+      if (d == 0) {
+        part_ml[pi * 2 + 0] = M;
+        part_ml[pi * 2 + 1] = L;
+      }
+    }
+  }
+}
+
+// Merge the per-partition partials of sequences that span > 1 partition.
+__global__ __launch_bounds__(256) void decode_reduce_kernel(
+    bf16_t* __restrict__ out, const float* __restrict__ part_o,
+    const float* __restrict__ part_ml, const int* __restrict__ context_lens,
+    int Hq, int D, int max_parts, int blocks_per_part) {
+  const int bh = blockIdx.x;  // b * Hq + hq
+  const int b = bh / Hq;
+  const int ctx = context_lens[b];
+  const int nblk = (ctx + kBS - 1) / kBS;
+  const int nparts = (nblk + blocks_per_part - 1) / blocks_per_part;
+  if (nparts <= 1) return;
+  const float* ml = part_ml + (int64_t)bh * max_parts * 2;
+  float M = kNegBig;
+  for (int p = 0; p < nparts; ++p) M = fmaxf(M, ml[2 * p]);
+  float L = 0.f;
+  for (int p = 0; p < nparts; ++p) L += ml[2 * p + 1] * fast_exp2(ml[2 * p] - M);
+  const float invL = 1.f / L;
+  for (int d = threadIdx.x; d < D; d += 256) {
+    float O = 0.f;
+    for (int p = 0; p < nparts; ++p)
+      O += part_o[((int64_t)bh * max_parts + p) * D + d] * fast_exp2(ml[2 * p] - M);
+    out[(int64_t)bh * D + d] = f2bf(O * invL);
+  }
+}
+
+int launch_paged_decode(void* out, float* part_o, float* part_ml, const void* q,
+                        int q_stride, const void* k_cache, const void* v_cache,
+                        const int* block_tables, int bt_stride,
+                        const int* context_lens, int B, int Hq, int Hkv, int D,
+                        float scale, int max_parts, int blocks_per_part,
+                        hipStream_t st) {
+  if (B == 0) return 0;
+  if (Hkv <= 0 || Hq % Hkv != 0 || Hq / Hkv > 16) return -1;
+  if (max_parts > 1 && (!part_o || !part_ml)) return -2;
+  const float sl2 = scale * kLog2e;
+  dim3 grid(B * Hkv, max_parts), block(256);
+  const size_t lds = (128 + 4 * (size_t)D * 16) * sizeof(float);
+  switch (D) {
+    case 64:
+      hipLaunchKernelGGL(paged_decode_kernel<64>, grid, block, lds, st, (bf16_t*)out, part_o, part_ml, (const bf16_t*)q, q_stride, (const bf16_t*)k_cache, (const bf16_t*)v_cache, block_tables, bt_stride, context_lens, Hq, Hkv, sl2, max_parts, blocks_per_part);
+      break;
+    case 128:
+      hipLaunchKernelGGL(paged_decode_kernel<128>, grid, block, lds, st, (bf16_t*)out, part_o, part_ml, (const bf16_t*)q, q_stride, (const bf16_t*)k_cache, (const bf16_t*)v_cache, block_tables, bt_stride, context_lens, Hq, Hkv, sl2, max_parts, blocks_per_part);
+      break;
+    case 256:
+      hipLaunchKernelGGL(paged_decode_kernel<256>, grid, block, lds, st, (bf16_t*)out, part_o, part_ml, (const bf16_t*)q, q_stride, (const bf16_t*)k_cache, (const bf16_t*)v_cache, block_tables, bt_stride, context_lens, Hq, Hkv, sl2, max_parts, blocks_per_part);
+      break;
+    default:
+      return -1;
+  }
+  if (max_parts > 1)
+    hipLaunchKernelGGL(decode_reduce_kernel, dim3(B * Hq), dim3(256), 0, st,
+                       (bf16_t*)out, (const float*)part_o, (const float*)part_ml,
+                       context_lens, Hq, D, max_parts, blocks_per_part);
+  return (int)hipGetLastError();
+}
+
+int configure_decode() {
+  const int lds = (128 + 4 * 256 * 16) * sizeof(float);
+  return (int)hipFuncSetAttribute((const void*)paged_decode_kernel<256>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+}
+
+}  // namespace drtc

@@ -1,0 +1,68 @@
+// pybind11 module `_hipk`: thin bindings over the HIP launchers.
+//
+// Tensors cross the boundary as raw device addresses (Python passes
+// `tensor.data_ptr()`) and the stream as `torch.cuda.current_stream()
+// .cuda_stream`; shape/dtype validation happens in the Python op wrappers
+// (drtc_amd/ops), which also check every launcher's return code.
+#include <pybind11/pybind11.h>
+
+#include "launchers.h"
+
+namespace py = pybind11;
+using u64 = std::uintptr_t;
+
+template <class T>
+static T* P(u64 p) { return reinterpret_cast<T*>(p); }
+static hipStream_t S(u64 s) { return reinterpret_cast<hipStream_t>(s); }
+
+PYBIND11_MODULE(_hipk, m) {
+  m.doc() = "drtc_amd CDNA4 (gfx950) HIP kernels";
+  m.def("configure", []() { return drtc::configure_kernels(); });
+  m.def("rmsnorm",
+        [](u64 out, u64 residual, u64 x, u64 w, int rows, int H, float eps,
+           int x_stride, int out_stride, int res_stride, bool gemma, u64 st) {
+          return drtc::launch_rmsnorm(P<void>(out), P<void>(residual), P<void>(x),
+                                      P<void>(w), rows, H, eps, x_stride,
+                                      out_stride, res_stride, gemma, S(st));
+        });
+  m.def("act_glu", [](u64 out, u64 gu, int64_t T, int I, int gu_stride, int act,
+                      u64 st) {
+    return drtc::launch_act_glu(P<void>(out), P<void>(gu), T, I, gu_stride, act, S(st));
+  });
+  m.def("rope_kv", [](u64 qkv, int T, int qkv_stride, u64 positions, u64 slots,
+                      u64 cos_sin, int Hq, int Hkv, int D, u64 k_cache,
+                      u64 v_cache, int block_size, u64 st) {
+    return drtc::launch_rope_kv(P<void>(qkv), T, qkv_stride, P<const int>(positions),
+                                P<const int64_t>(slots), P<const float>(cos_sin), Hq,
+                                Hkv, D, P<void>(k_cache), P<void>(v_cache),
+                                block_size, S(st));
+  });
+  m.def("paged_decode",
+        [](u64 out, u64 part_o, u64 part_ml, u64 q, int q_stride, u64 k_cache,
+           u64 v_cache, u64 block_tables, int bt_stride, u64 context_lens, int B,
+           int Hq, int Hkv, int D, float scale, int max_parts,
+           int blocks_per_part, u64 st) {
+          return drtc::launch_paged_decode(
+              P<void>(out), P<float>(part_o), P<float>(part_ml), P<const void>(q),
+              q_stride, P<const void>(k_cache), P<const void>(v_cache),
+              P<const int>(block_tables), bt_stride, P<const int>(context_lens), B,
+              Hq, Hkv, D, scale, max_parts, blocks_per_part, S(st));
+        });
+  m.def("prefill_attn",
+        [](u64 out, int out_stride, u64 qkv, int qkv_stride, int Hq, int Hkv,
+           int D, u64 cu_seqlens, u64 tile_seq, u64 tile_q0, int ntiles,
+           float scale, int causal, u64 st) {
+          return drtc::launch_prefill_attn(
+              P<void>(out), out_stride, P<const void>(qkv), qkv_stride, Hq, Hkv, D,
+              P<const int>(cu_seqlens), P<const int>(tile_seq),
+              P<const int>(tile_q0), ntiles, scale, causal, S(st));
+        });
+  m.def("sample", [](u64 out_tokens, u64 logits, int B, int V, int ld,
+                     u64 temperature, u64 top_k, u64 top_p, uint64_t seed,
+                     u64 step, u64 st) {
+    return drtc::launch_sample(P<int>(out_tokens), P<const void>(logits), B, V, ld,
+                               P<const float>(temperature), P<const int>(top_k),
+                               P<const float>(top_p), seed,
+                               P<const int64_t>(step), S(st));
+  });
+}

@@ -1,0 +1,10 @@
+// One-time kernel attribute setup (dynamic LDS > 64 KiB for head_dim 256).
+#include "launchers.h"
+
+namespace drtc {
+int configure_kernels() {
+  int e = configure_decode();
+  if (e) return e;
+  return configure_prefill();
+}
+}  // namespace drtc

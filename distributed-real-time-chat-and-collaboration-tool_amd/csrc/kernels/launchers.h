@@ -1,0 +1,46 @@
+// Host-side launchers of the drtc_amd HIP kernels.  Every launcher enqueues
+// on the caller's stream only (no allocation, no synchronisation) so the
+// whole decode step can be captured into a hipGraph.  Return value: 0 on
+// success, a negative code on an unsupported shape, else a hipError_t.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace drtc {
+
+int launch_rmsnorm(void* out, void* residual, const void* x, const void* w,
+                   int rows, int H, float eps, int x_stride, int out_stride,
+                   int res_stride, bool gemma, hipStream_t st);
+
+int launch_act_glu(void* out, const void* gu, int64_t T, int I, int gu_stride,
+                   int act, hipStream_t st);
+
+int launch_rope_kv(void* qkv, int T, int qkv_stride, const int* positions,
+                   const int64_t* slots, const float* cos_sin, int Hq, int Hkv,
+                   int D, void* k_cache, void* v_cache, int block_size,
+                   hipStream_t st);
+
+int launch_paged_decode(void* out, float* part_o, float* part_ml, const void* q,
+                        int q_stride, const void* k_cache, const void* v_cache,
+                        const int* block_tables, int bt_stride,
+                        const int* context_lens, int B, int Hq, int Hkv, int D,
+                        float scale, int max_parts, int blocks_per_part,
+                        hipStream_t st);
+
+int launch_prefill_attn(void* out, int out_stride, const void* qkv,
+                        int qkv_stride, int Hq, int Hkv, int D,
+                        const int* cu_seqlens, const int* tile_seq,
+                        const int* tile_q0, int ntiles, float scale, int causal,
+                        hipStream_t st);
+
+int launch_sample(int* out_tokens, const void* logits, int B, int V, int ld,
+                  const float* temperature, const int* top_k, const float* top_p,
+                  uint64_t seed, const int64_t* step, hipStream_t st);
+
+// Raise the dynamic-LDS ceiling of the kernels that need > 64 KiB (head_dim
+// 256).  Called once at import, before any graph capture.
+int configure_kernels();
+int configure_decode();
+int configure_prefill();
+
+}  // namespace drtc

@@ -1,0 +1,157 @@
+"""Static-buffer decode step with per-batch-bucket hipGraph capture.
+
+The whole decode step - embedding, 32 x (QKV GEMM, RoPE+KV write, paged MFMA
+attention, o_proj, add+norm, gate|up GEMM, act, down, add+norm), LM head and
+the sampler, plus the RNG-step increment - is captured once per batch bucket
+and replayed with a single ``hipGraphLaunch``.  Per step the host only
+uploads three packed staging buffers (int32 / int64 / fp32) and reads back
+the sampled token ids.
+"""
+from __future__ import annotations
+
+import bisect
+
+import numpy as np
+import torch
+
+from .. import ops
+from ..models.transformer import DecodeMeta, TransformerLM
+
+DEFAULT_BUCKETS = (1, 2, 4, 8, 16, 24, 32, 48, 64, 96, 128, 160, 192, 224, 256, 320, 384,
+                   448, 512, 640, 768, 896, 1024)
+
+
+class DecodeRunner:
+    def __init__(self, model: TransformerLM, kv_cache, max_batch: int, max_blocks: int,
+                 use_graphs: bool = True, seed: int = 0, buckets=DEFAULT_BUCKETS):
+        self.model = model
+        self.kv = kv_cache
+        self.max_batch = max_batch
+        self.max_blocks = max_blocks
+        self.seed = seed
+        dev = model.device
+        self.device = dev
+        self.use_graphs = bool(use_graphs and dev.type == "cuda")
+        self.buckets = sorted({b for b in buckets if b < max_batch} | {max_batch})
+        cfg, sh = model.cfg, model.sh
+        B, MB = max_batch, max_blocks
+        # ---- device buffers (persistent: graphs capture these addresses)
+        n_i32 = 3 * B + B * MB + B
+        self.i32 = torch.zeros(n_i32, dtype=torch.int32, device=dev)
+        self.ids = self.i32[0:B]
+        self.positions = self.i32[B:2 * B]
+        self.ctx = self.i32[2 * B:3 * B]
+        self.topk = self.i32[3 * B:4 * B]
+        self.bt = self.i32[4 * B:4 * B + B * MB].view(B, MB)
+        self.slots = torch.full((B,), -1, dtype=torch.int64, device=dev)
+        self.f32 = torch.zeros(2 * B, dtype=torch.float32, device=dev)
+        self.temp = self.f32[0:B]
+        self.topp = self.f32[B:2 * B]
+        self.step_ctr = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.out = torch.zeros(B, dtype=torch.int32, device=dev)
+        self.attn_out = torch.zeros((B, sh.hq, cfg.head_dim), dtype=model.dtype, device=dev)
+        # ---- pinned host staging
+        pin = dev.type == "cuda"
+        self.h_i32 = torch.zeros(n_i32, dtype=torch.int32, pin_memory=pin)
+        self.h_slots = torch.full((B,), -1, dtype=torch.int64, pin_memory=pin)
+        self.h_f32 = torch.zeros(2 * B, dtype=torch.float32, pin_memory=pin)
+        self.h_out = torch.zeros(B, dtype=torch.int32, pin_memory=pin)
+        self.n_i32 = n_i32
+        self._metas = {}
+        self._graphs = {}
+        self._pool = None
+
+    # ------------------------------------------------------------------
+    def bucket(self, n: int) -> int:
+        i = bisect.bisect_left(self.buckets, n)
+        if i >= len(self.buckets):
+            raise ValueError(f"batch {n} exceeds max_batch {self.max_batch}")
+        return self.buckets[i]
+
+    def _meta(self, Bb: int) -> DecodeMeta:
+        m = self._metas.get(Bb)
+        if m is None:
+            sh = self.model.sh
+            bpp, max_parts = ops.decode_partitioning(Bb, sh.hkv, self.max_blocks)
+            ws = ops.DecodeWorkspace(Bb, sh.hq, self.model.cfg.head_dim, max_parts, self.device)
+            m = DecodeMeta(positions=self.positions[:Bb], slots=self.slots[:Bb],
+                           block_tables=self.bt[:Bb], context_lens=self.ctx[:Bb],
+                           blocks_per_part=bpp, workspace=ws)
+            self._metas[Bb] = m
+        return m
+
+    def _forward(self, Bb: int) -> None:
+        meta = self._meta(Bb)
+        logits = self.model.forward_decode(self.ids[:Bb], meta, self.kv, self.attn_out[:Bb])
+        ops.sample(logits, self.temp[:Bb], self.topk[:Bb], self.topp[:Bb], seed=self.seed,
+                   step=self.step_ctr, out=self.out[:Bb])
+        self.step_ctr.add_(1)
+
+    def capture(self, Bb: int) -> None:
+        if not self.use_graphs or Bb in self._graphs:
+            return
+        # warm up on a side stream (lazy hipBLASLt / allocator init), then capture
+        s = torch.cuda.Stream(self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(s):
+            self._forward(Bb)
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        torch.cuda.synchronize(self.device)
+        if self._pool is None:
+            self._pool = torch.cuda.graph_pool_handle()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, pool=self._pool):
+            self._forward(Bb)
+        torch.cuda.synchronize(self.device)
+        self._graphs[Bb] = g
+
+    def capture_all(self, up_to: int | None = None) -> None:
+        for Bb in sorted(self.buckets, reverse=True):
+            if up_to is None or Bb <= self.bucket(min(up_to, self.max_batch)):
+                self.capture(Bb)
+
+    # ------------------------------------------------------------------
+    def run(self, n: int, ids: np.ndarray, positions: np.ndarray, ctx: np.ndarray,
+            slots: np.ndarray, block_rows: np.ndarray, temp: np.ndarray, topk: np.ndarray,
+            topp: np.ndarray) -> np.ndarray:
+        """Run one decode step for ``n`` sequences (arrays of length n, block_rows
+        [n, max_blocks]) and return the sampled token ids."""
+        Bb = self.bucket(n)
+        B, MB = self.max_batch, self.max_blocks
+        hi = self.h_i32.numpy()
+        hi[0:n] = ids
+        hi[n:Bb] = 0
+        hi[B:B + n] = positions
+        hi[B + n:B + Bb] = 0
+        hi[2 * B:2 * B + n] = ctx
+        hi[2 * B + n:2 * B + Bb] = 0
+        hi[3 * B:3 * B + n] = topk
+        hi[3 * B + n:3 * B + Bb] = 0
+        btv = hi[4 * B:4 * B + B * MB].reshape(B, MB)
+        btv[:n] = block_rows
+        btv[n:Bb] = 0
+        hs = self.h_slots.numpy()
+        hs[:n] = slots
+        hs[n:Bb] = -1
+        hf = self.h_f32.numpy()
+        hf[:n] = temp
+        hf[n:Bb] = 0.0
+        hf[B:B + n] = topp
+        hf[B + n:B + Bb] = 1.0
+        nb = self.device.type == "cuda"
+        self.i32.copy_(self.h_i32, non_blocking=nb)
+        self.slots.copy_(self.h_slots, non_blocking=nb)
+        self.f32.copy_(self.h_f32, non_blocking=nb)
+        g = self._graphs.get(Bb)
+        if g is None and self.use_graphs:
+            self.capture(Bb)
+            g = self._graphs[Bb]
+        if g is not None:
+            g.replay()
+        else:
+            self._forward(Bb)
+        if nb:
+            self.h_out[:n].copy_(self.out[:n], non_blocking=True)
+            torch.cuda.current_stream(self.device).synchronize()
+            return self.h_out[:n].numpy().copy()
+        return self.out[:n].numpy().copy()

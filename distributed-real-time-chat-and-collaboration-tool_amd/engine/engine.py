@@ -1,0 +1,333 @@
+"""Continuous-batching LLM serving engine (one engine per GPU / TP group).
+
+Scheduling (one iteration = one ``step()``):
+  * prefill-first: while requests wait and the batch has free slots and KV
+    blocks, admit as many as fit in ``max_prefill_tokens`` and run ONE packed
+    varlen prefill for all of them (MFMA flash attention, KV written in the
+    fused RoPE kernel), sampling each request's first token;
+  * otherwise one decode step for every running request through the
+    hipGraph of its batch bucket (engine/decode_runner.py);
+  * on KV exhaustion the most recently admitted request is preempted
+    (blocks freed, re-queued at the front for recomputation).
+
+Running requests occupy dense "slots" 0..n-1 whose block-table rows live in
+a persistent numpy array, so building a decode step's metadata is a handful
+of vectorised numpy ops (no per-request Python loops on the hot path except
+token bookkeeping).
+"""
+from __future__ import annotations
+
+import collections
+import math
+import threading
+import time
+
+import numpy as np
+import torch
+
+from .. import ops
+from ..models.transformer import PrefillMeta, TransformerLM
+from .decode_runner import DEFAULT_BUCKETS, DecodeRunner
+from .kv_cache import PagedKVCache
+from .request import Request, RequestState, SamplingParams
+
+BS = ops.KV_BLOCK
+
+
+class LLMEngine:
+    def __init__(self, model: TransformerLM, max_batch: int = 256, max_model_len: int = 4096,
+                 max_prefill_tokens: int = 16384, num_blocks: int | None = None,
+                 kv_fraction: float = 0.85, use_graphs: bool = True, seed: int = 0,
+                 buckets=DEFAULT_BUCKETS):
+        self.model = model
+        cfg = model.cfg
+        self.cfg = cfg
+        self.device = model.device
+        self.max_batch = max_batch
+        self.max_model_len = min(max_model_len, cfg.max_position)
+        self.max_prefill_tokens = max_prefill_tokens
+        self.max_blocks = math.ceil(self.max_model_len / BS)
+        if num_blocks is None:
+            num_blocks = PagedKVCache.auto_num_blocks(cfg, model.sh.hkv, self.device, kv_fraction)
+        self.kv = PagedKVCache(cfg, model.sh.hkv, num_blocks, self.device, model.dtype)
+        self.alloc = self.kv.allocator
+        self.runner = DecodeRunner(model, self.kv, max_batch, self.max_blocks,
+                                   use_graphs=use_graphs, seed=seed, buckets=buckets)
+        self.seed = seed
+        self._prefill_step = 0
+        # slot state
+        self.bt = np.zeros((max_batch, self.max_blocks), dtype=np.int32)
+        self.ctx = np.zeros(max_batch, dtype=np.int32)        # tokens in the KV cache
+        self.last = np.zeros(max_batch, dtype=np.int32)       # last sampled token
+        self.temp = np.zeros(max_batch, dtype=np.float32)
+        self.topk = np.zeros(max_batch, dtype=np.int32)
+        self.topp = np.ones(max_batch, dtype=np.float32)
+        self.running: list[Request] = []
+        self.waiting: collections.deque[Request] = collections.deque()
+        self.lock = threading.Lock()
+        self.stats = collections.Counter()
+        # admission watermark + anti-thrash latch: after a preemption no new
+        # request is admitted until some running request finishes
+        self.watermark = max(1, self.kv.num_blocks // 100)
+        self._pressure = False
+
+    # ------------------------------------------------------------ API
+    def add_request(self, req: Request) -> Request:
+        n = len(req.prompt_ids)
+        if n == 0:
+            raise ValueError("empty prompt")
+        if n >= self.max_model_len:
+            raise ValueError(f"prompt of {n} tokens exceeds max_model_len {self.max_model_len}")
+        if n > self.max_prefill_tokens:
+            raise ValueError("prompt exceeds max_prefill_tokens")
+        with self.lock:
+            req.state = RequestState.WAITING
+            self.waiting.append(req)
+        return req
+
+    def has_work(self) -> bool:
+        return bool(self.running or self.waiting)
+
+    def warmup(self, capture: bool = True, up_to: int | None = None) -> None:
+        """Capture decode graphs up front (zeroed staging: no cache reads/writes)."""
+        if capture and self.runner.use_graphs:
+            self.runner.capture_all(up_to)
+
+    def generate(self, prompts: list[list[int]], params: SamplingParams | list) -> list[Request]:
+        if isinstance(params, SamplingParams):
+            params = [params] * len(prompts)
+        reqs = [self.add_request(Request(list(p), prm)) for p, prm in zip(prompts, params)]
+        while any(r.state != RequestState.FINISHED for r in reqs):
+            self.step()
+        return reqs
+
+    def step(self) -> list[Request]:
+        """One scheduler iteration. Returns requests finished in it."""
+        with self.lock:
+            batch = self._admit()
+        if batch:
+            return self._run_prefill(batch)
+        if self.running:
+            return self._run_decode()
+        return []
+
+    # ------------------------------------------------------------ admission
+    def _admit(self) -> list[Request]:
+        batch, tokens = [], 0
+        if self._pressure and self.running:
+            return batch
+        self._pressure = False
+        while self.waiting and len(self.running) + len(batch) < self.max_batch:
+            r = self.waiting[0]
+            ids = r.all_ids  # recomputation after preemption includes outputs
+            n = len(ids)
+            if batch and tokens + n > self.max_prefill_tokens:
+                break
+            need = math.ceil((n + 1) / BS)
+            busy = bool(self.running or batch)
+            if not self.alloc.can_allocate(need + (self.watermark if busy else 0)):
+                if not busy and need > self.alloc.num_blocks - 1:
+                    self.waiting.popleft()
+                    r.mark_finished("error: request exceeds KV-cache capacity")
+                    continue
+                break
+            self.waiting.popleft()
+            r.blocks = list(self.alloc.allocate(need))
+            batch.append(r)
+            tokens += n
+        return batch
+
+    def _assign_slot(self, r: Request) -> int:
+        s = len(self.running)
+        self.running.append(r)
+        r.slot = s
+        r.state = RequestState.RUNNING
+        self.bt[s, :] = 0
+        self.bt[s, :len(r.blocks)] = r.blocks
+        self.temp[s] = r.params.temperature
+        self.topk[s] = r.params.top_k
+        self.topp[s] = r.params.top_p
+        return s
+
+    def _release_slot(self, r: Request) -> None:
+        s = r.slot
+        last = len(self.running) - 1
+        if s != last:
+            m = self.running[last]
+            self.running[s] = m
+            m.slot = s
+            for arr in (self.bt, self.ctx, self.last, self.temp, self.topk, self.topp):
+                arr[s] = arr[last]
+        self.running.pop()
+        r.slot = -1
+        if r.blocks:
+            self.alloc.free(r.blocks)
+            r.blocks = []
+
+    def _finish_check(self, r: Request, tok: int) -> str:
+        p = r.params
+        if not p.ignore_eos and (tok == self.cfg.eos_token_id or tok in p.stop_token_ids):
+            return "stop"
+        if len(r.output_ids) >= p.max_new_tokens:
+            return "length"
+        if r.num_tokens >= self.max_model_len:
+            return "length"
+        return ""
+
+    # ------------------------------------------------------------ prefill
+    def _run_prefill(self, batch: list[Request]) -> list[Request]:
+        dev = self.device
+        seqs = [r.all_ids for r in batch]
+        lens = [len(s) for s in seqs]
+        cu = [0]
+        for n in lens:
+            cu.append(cu[-1] + n)
+        T = cu[-1]
+        ids = np.concatenate([np.asarray(s, dtype=np.int32) for s in seqs])
+        pos = np.concatenate([np.arange(n, dtype=np.int32) for n in lens])
+        slots = np.empty(T, dtype=np.int64)
+        for r, a, n in zip(batch, cu[:-1], lens):
+            blk = np.asarray(r.blocks, dtype=np.int64)
+            p = np.arange(n)
+            slots[a:a + n] = blk[p // BS] * BS + p % BS
+        last_idx = np.asarray(cu[1:], dtype=np.int64) - 1
+        ts, tq = ops.prefill_tiles(cu)
+        t_i32 = torch.from_numpy(np.concatenate([ids, pos, np.asarray(cu, np.int32),
+                                                 np.asarray(ts, np.int32),
+                                                 np.asarray(tq, np.int32)])).to(dev, non_blocking=True)
+        t_i64 = torch.from_numpy(np.concatenate([slots, last_idx])).to(dev, non_blocking=True)
+        nseq, nt = len(batch), len(ts)
+        o = 0
+        d_ids = t_i32[o:o + T]; o += T
+        d_pos = t_i32[o:o + T]; o += T
+        d_cu = t_i32[o:o + nseq + 1]; o += nseq + 1
+        d_ts = t_i32[o:o + nt]; o += nt
+        d_tq = t_i32[o:o + nt]
+        meta = PrefillMeta(positions=d_pos, slots=t_i64[:T], cu_seqlens=d_cu, cu_host=cu,
+                           tiles=(d_ts, d_tq), last_idx=t_i64[T:])
+        logits = self.model.forward_prefill(d_ids, meta, self.kv)
+        temp = torch.tensor([r.params.temperature for r in batch], dtype=torch.float32, device=dev)
+        topk = torch.tensor([r.params.top_k for r in batch], dtype=torch.int32, device=dev)
+        topp = torch.tensor([r.params.top_p for r in batch], dtype=torch.float32, device=dev)
+        self._prefill_step += 1
+        step = torch.tensor([self._prefill_step + (1 << 40)], dtype=torch.int64, device=dev)
+        toks = ops.sample(logits, temp, topk, topp, seed=self.seed, step=step).cpu().numpy()
+        self.stats["prefill_steps"] += 1
+        self.stats["prefill_tokens"] += T
+        now = time.perf_counter()
+        finished = []
+        for r, n, tok in zip(batch, lens, toks):
+            tok = int(tok)
+            s = self._assign_slot(r)
+            self.ctx[s] = n
+            self.last[s] = tok
+            r.output_ids.append(tok)
+            if not r.first_token_time:
+                r.first_token_time = now
+            reason = self._finish_check(r, tok)
+            if reason:
+                self._release_slot(r)
+                r.mark_finished(reason)
+                finished.append(r)
+        return finished
+
+    # ------------------------------------------------------------ decode
+    def _ensure_blocks(self) -> None:
+        """Give every running request room for its next token; preempt the
+        newest requests when the cache is exhausted."""
+        n = len(self.running)
+        pos = self.ctx[:n]
+        need = (pos % BS == 0) & (pos // BS >= np.array([len(r.blocks) for r in self.running]))
+        for s in np.nonzero(need)[0].tolist():
+            if s >= len(self.running):
+                continue
+            r = self.running[s]
+            while not self.alloc.can_allocate(1):
+                victim = self.running[-1]
+                self._preempt(victim)
+                if victim is r:
+                    break
+            if r.slot < 0:
+                continue
+            b = self.alloc.allocate_one()
+            r.blocks.append(b)
+            self.bt[r.slot, len(r.blocks) - 1] = b
+
+    def _preempt(self, r: Request) -> None:
+        self._pressure = True
+        self._release_slot(r)
+        r.state = RequestState.WAITING
+        r.num_preemptions += 1
+        self.stats["preemptions"] += 1
+        self.waiting.appendleft(r)
+
+    def _run_decode(self) -> list[Request]:
+        with self.lock:
+            self._ensure_blocks()
+        n = len(self.running)
+        if n == 0:
+            return []
+        pos = self.ctx[:n].copy()
+        bidx = pos // BS
+        slots = self.bt[np.arange(n), bidx].astype(np.int64) * BS + pos % BS
+        toks = self.runner.run(n, self.last[:n], pos, pos + 1, slots, self.bt[:n],
+                               self.temp[:n], self.topk[:n], self.topp[:n])
+        self.stats["decode_steps"] += 1
+        self.stats["decode_tokens"] += n
+        self.ctx[:n] += 1
+        self.last[:n] = toks
+        finished = []
+        reqs = list(self.running)
+        for r, tok in zip(reqs, toks.tolist()):
+            r.output_ids.append(tok)
+            reason = self._finish_check(r, tok)
+            if reason:
+                finished.append((r, reason))
+        for r, reason in finished:
+            self._release_slot(r)
+            r.mark_finished(reason)
+        if finished:
+            self._pressure = False
+        return [r for r, _ in finished]
+
+
+class EngineLoop:
+    """Background thread that drives an engine; used by the LLM gRPC service
+    so concurrent RPCs are batched together (continuous batching)."""
+
+    def __init__(self, engine: LLMEngine, idle_sleep: float = 0.0005):
+        self.engine = engine
+        self.idle_sleep = idle_sleep
+        self._stop = threading.Event()
+        self._wake = threading.Event()
+        self.thread = threading.Thread(target=self._loop, name="llm-engine", daemon=True)
+        self.error: BaseException | None = None
+
+    def start(self) -> "EngineLoop":
+        self.thread.start()
+        return self
+
+    def submit(self, req: Request) -> Request:
+        self.engine.add_request(req)
+        self._wake.set()
+        return req
+
+    def _loop(self) -> None:
+        try:
+            while not self._stop.is_set():
+                if self.engine.has_work():
+                    self.engine.step()
+                else:
+                    self._wake.wait(0.05)
+                    self._wake.clear()
+        except BaseException as e:  # surface engine faults to callers
+            self.error = e
+            with self.engine.lock:
+                pending = list(self.engine.waiting) + list(self.engine.running)
+            for r in pending:
+                r.mark_finished("error")
+
+    def stop(self) -> None:
+        self._stop.set()
+        self._wake.set()
+        self.thread.join(timeout=10)

@@ -1,0 +1,303 @@
+"""Decoder-only transformer (Llama-3 / Gemma / Mixtral families), inference-only.
+
+MI355X-first layout decisions
+  * fused projections: one QKV GEMM and one gate|up GEMM per layer
+    (hipBLASLt via ``F.linear``); everything between the GEMMs is a fused HIP
+    kernel: add+RMSNorm, RoPE + paged-KV write (in place on the QKV output),
+    MFMA attention reading q/k/v straight out of the QKV buffer, act*up;
+  * tensor parallel over RCCL: heads / intermediate columns sharded, one
+    all-reduce after o_proj and one after down_proj (or the MoE combine),
+    vocab-parallel LM head + all-gather;
+  * expert parallel for MoE: each rank owns E/ep experts, partial expert
+    outputs are summed by the EP all-reduce;
+  * decode is static-shaped (persistent metadata buffers) so the whole step
+    is hipGraph-capturable by the engine.
+
+Random-init bf16 weights (no checkpoints in this environment); a fixed seed
+and ``full_then_shard=True`` make TP=N numerically comparable to TP=1.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import torch
+import torch.nn.functional as F
+
+from .. import ops
+from ..parallel.comm import ParallelContext
+from .config import ModelConfig
+
+
+@dataclass
+class PrefillMeta:
+    positions: torch.Tensor      # int32 [T]
+    slots: torch.Tensor          # int64 [T]  (-1: do not cache)
+    cu_seqlens: torch.Tensor     # int32 [n+1]
+    cu_host: list
+    tiles: tuple | None          # (tile_seq, tile_q0) int32 device tensors
+    last_idx: torch.Tensor       # int64 [n] index of each sequence's last token
+
+
+@dataclass
+class DecodeMeta:
+    positions: torch.Tensor      # int32 [B]
+    slots: torch.Tensor          # int64 [B]
+    block_tables: torch.Tensor   # int32 [B, max_blocks]
+    context_lens: torch.Tensor   # int32 [B]
+    blocks_per_part: int
+    workspace: object            # ops.DecodeWorkspace
+
+
+class ShardInfo:
+    def __init__(self, cfg: ModelConfig, pc: ParallelContext):
+        tp, r = pc.tp_size, pc.tp_rank
+        assert cfg.num_heads % tp == 0, "num_heads must divide by TP"
+        self.hq = cfg.num_heads // tp
+        if cfg.num_kv_heads >= tp:
+            assert cfg.num_kv_heads % tp == 0
+            self.hkv = cfg.num_kv_heads // tp
+            self.kv_heads = list(range(r * self.hkv, (r + 1) * self.hkv))
+        else:  # fewer kv heads than ranks: replicate (e.g. MQA)
+            self.hkv = 1
+            self.kv_heads = [r * cfg.num_kv_heads // tp]
+        assert cfg.intermediate_size % tp == 0 and cfg.vocab_size % tp == 0
+        self.inter = cfg.intermediate_size // tp
+        self.vocab = cfg.vocab_size // tp
+        self.q_heads = list(range(r * self.hq, (r + 1) * self.hq))
+        ep = pc.ep_size
+        if cfg.is_moe:
+            assert cfg.num_experts % ep == 0
+            self.n_local_experts = cfg.num_experts // ep
+            self.expert_offset = pc.ep_rank * self.n_local_experts
+            # experts are not TP-sharded when EP is used; with EP=1 they are
+            self.expert_inter = cfg.intermediate_size if ep > 1 else self.inter
+        self.tp, self.rank = tp, r
+
+
+class TransformerLM:
+    """Weights + forward for one model shard on one device."""
+
+    def __init__(self, cfg: ModelConfig, device: torch.device | str = "cpu",
+                 pc: ParallelContext | None = None, seed: int = 0,
+                 full_then_shard: bool | None = None, dtype=torch.bfloat16):
+        self.cfg = cfg
+        self.device = torch.device(device)
+        self.pc = pc or ParallelContext.single()
+        self.dtype = dtype
+        self.sh = ShardInfo(cfg, self.pc)
+        if full_then_shard is None:
+            full_then_shard = cfg.num_params() < 200_000_000
+        self._init_weights(seed, full_then_shard)
+        self.cos_sin = ops.build_rope_cache(cfg.max_position, cfg.head_dim, cfg.rope_theta,
+                                            cfg.rope_scaling, device=self.device)
+        self.qkv_dim = (self.sh.hq + 2 * self.sh.hkv) * cfg.head_dim
+
+    # ------------------------------------------------------------ weights
+    def _init_weights(self, seed: int, full_then_shard: bool) -> None:
+        cfg, sh, dev, dt = self.cfg, self.sh, self.device, self.dtype
+        std = cfg.init_std
+        H, D, I = cfg.hidden_size, cfg.head_dim, cfg.intermediate_size
+        gen = torch.Generator(device="cpu").manual_seed(seed)
+        dev_gen = None
+        if not full_then_shard and dev.type == "cuda":
+            dev_gen = torch.Generator(device=dev).manual_seed(seed * 1000 + 7 + self.pc.tp_rank)
+
+        def rnd(*shape):
+            if full_then_shard:
+                return (torch.randn(*shape, generator=gen, dtype=torch.float32) * std).to(dt)
+            t = torch.empty(*shape, dtype=dt, device=dev)
+            if dev_gen is not None:
+                return t.normal_(0.0, std, generator=dev_gen)
+            return t.normal_(0.0, std, generator=gen)
+
+        def put(t):
+            return t.to(dev).contiguous()
+
+        def rows(t, idx_blocks, block):
+            return torch.cat([t[i * block:(i + 1) * block] for i in idx_blocks], dim=0)
+
+        def norm_w():
+            if cfg.gemma_norm:
+                return torch.zeros(H, dtype=dt, device=dev)  # (1 + w) = 1
+            return torch.ones(H, dtype=dt, device=dev)
+
+        self.embed = put(rnd(cfg.vocab_size, H))
+        self.layers = []
+        for _ in range(cfg.num_layers):
+            L = {}
+            if full_then_shard:
+                wq = rnd(cfg.num_heads * D, H)
+                wk = rnd(cfg.num_kv_heads * D, H)
+                wv = rnd(cfg.num_kv_heads * D, H)
+                wo = rnd(H, cfg.num_heads * D)
+                L["qkv"] = put(torch.cat([rows(wq, sh.q_heads, D), rows(wk, sh.kv_heads, D),
+                                          rows(wv, sh.kv_heads, D)], 0))
+                cols = torch.cat([torch.arange(h * D, (h + 1) * D) for h in sh.q_heads])
+                L["o"] = put(wo[:, cols])
+            else:
+                L["qkv"] = put(rnd((sh.hq + 2 * sh.hkv) * D, H))
+                L["o"] = put(rnd(H, sh.hq * D))
+            L["ln_in"] = norm_w()
+            L["ln_post"] = norm_w()
+            if cfg.is_moe:
+                E, EI = sh.n_local_experts, sh.expert_inter
+                if full_then_shard:
+                    wr = rnd(cfg.num_experts, H)
+                    gus, downs = [], []
+                    for e in range(cfg.num_experts):
+                        g, u, d = rnd(I, H), rnd(I, H), rnd(H, I)
+                        if sh.expert_offset <= e < sh.expert_offset + E:
+                            if self.pc.ep_size > 1 or sh.tp == 1:
+                                gus.append(torch.cat([g, u], 0))
+                                downs.append(d)
+                            else:
+                                r0 = sh.rank * sh.inter
+                                gus.append(torch.cat([g[r0:r0 + sh.inter], u[r0:r0 + sh.inter]], 0))
+                                downs.append(d[:, r0:r0 + sh.inter])
+                    L["router"] = put(wr)
+                    L["gate_up"] = put(torch.stack(gus))
+                    L["down"] = put(torch.stack(downs))
+                else:
+                    L["router"] = put(rnd(cfg.num_experts, H))
+                    L["gate_up"] = put(rnd(E, 2 * EI, H))
+                    L["down"] = put(rnd(E, H, EI))
+            else:
+                if full_then_shard:
+                    g, u, d = rnd(I, H), rnd(I, H), rnd(H, I)
+                    r0 = sh.rank * sh.inter
+                    L["gate_up"] = put(torch.cat([g[r0:r0 + sh.inter], u[r0:r0 + sh.inter]], 0))
+                    L["down"] = put(d[:, r0:r0 + sh.inter])
+                else:
+                    L["gate_up"] = put(rnd(2 * sh.inter, H))
+                    L["down"] = put(rnd(H, sh.inter))
+            self.layers.append(L)
+        self.final_norm = norm_w()
+        if cfg.tie_embeddings:
+            v0 = sh.rank * sh.vocab
+            self.lm_head = self.embed[v0:v0 + sh.vocab]
+        else:
+            if full_then_shard:
+                full = rnd(cfg.vocab_size, H)
+                v0 = sh.rank * sh.vocab
+                self.lm_head = put(full[v0:v0 + sh.vocab])
+            else:
+                self.lm_head = put(rnd(sh.vocab, H))
+
+    def weight_bytes(self) -> int:
+        n = self.embed.numel() + self.final_norm.numel()
+        for L in self.layers:
+            n += sum(t.numel() for t in L.values())
+        if not self.cfg.tie_embeddings:
+            n += self.lm_head.numel()
+        return n * self.embed.element_size()
+
+    # ------------------------------------------------------------ forward
+    def _embed(self, ids: torch.Tensor) -> torch.Tensor:
+        h = F.embedding(ids, self.embed)
+        if self.cfg.embed_scale:
+            h = h * torch.tensor(math.sqrt(self.cfg.hidden_size), dtype=h.dtype, device=h.device)
+        return h
+
+    def _mlp(self, L: dict, x: torch.Tensor) -> torch.Tensor:
+        if self.cfg.is_moe:
+            return self._moe(L, x)
+        gu = F.linear(x, L["gate_up"])
+        a = ops.act_glu(gu, self.cfg.act)
+        y = F.linear(a, L["down"])
+        return self.pc.all_reduce_tp(y)
+
+    def _moe(self, L: dict, x: torch.Tensor) -> torch.Tensor:
+        """Top-k routed experts (Mixtral: softmax over the top-2 logits)."""
+        cfg, sh = self.cfg, self.sh
+        logits = F.linear(x, L["router"]).float()
+        topv, topi = logits.topk(cfg.experts_per_token, dim=-1)
+        wts = torch.softmax(topv, dim=-1)
+        out = torch.zeros(x.shape[0], x.shape[1], dtype=torch.float32, device=x.device)
+        for le in range(sh.n_local_experts):
+            e = sh.expert_offset + le
+            tok, slot = torch.nonzero(topi == e, as_tuple=True)
+            if tok.numel() == 0:
+                continue
+            xe = x.index_select(0, tok)
+            h = ops.act_glu(F.linear(xe, L["gate_up"][le]), cfg.act)
+            ye = F.linear(h, L["down"][le]).float() * wts[tok, slot].unsqueeze(1)
+            out.index_add_(0, tok, ye)
+        out = out.to(x.dtype)
+        if self.pc.ep_size > 1:
+            return self.pc.all_reduce_ep(out)
+        return self.pc.all_reduce_tp(out)
+
+    def _layers(self, h: torch.Tensor, attn_fn) -> torch.Tensor:
+        cfg = self.cfg
+        residual = h
+        x = ops.rmsnorm(h, self.layers[0]["ln_in"], cfg.rms_eps, cfg.gemma_norm)
+        n = len(self.layers)
+        for i, L in enumerate(self.layers):
+            o = attn_fn(i, L, x)
+            x = ops.rmsnorm(o, L["ln_post"], cfg.rms_eps, cfg.gemma_norm, residual=residual)
+            m = self._mlp(L, x)
+            nxt = self.layers[i + 1]["ln_in"] if i + 1 < n else self.final_norm
+            x = ops.rmsnorm(m, nxt, cfg.rms_eps, cfg.gemma_norm, residual=residual)
+        return x
+
+    def _logits(self, x: torch.Tensor) -> torch.Tensor:
+        logits = F.linear(x, self.lm_head)
+        return self.pc.all_gather_tp_lastdim(logits)
+
+    def forward_prefill(self, ids: torch.Tensor, meta: PrefillMeta, kv_caches) -> torch.Tensor:
+        """Packed varlen prefill. Returns logits of each sequence's last token."""
+        cfg, sh = self.cfg, self.sh
+        D = cfg.head_dim
+
+        def attn(i, L, x):
+            qkv = F.linear(x, L["qkv"])
+            kc, vc = kv_caches[i] if kv_caches is not None else (None, None)
+            ops.rope_kv_(qkv, meta.positions, meta.slots if kc is not None else None,
+                         self.cos_sin, sh.hq, sh.hkv, D, kc, vc, ops.KV_BLOCK)
+            a = ops.prefill_attention(qkv, meta.cu_seqlens, sh.hq, sh.hkv, D, cfg.attn_scale,
+                                      True, tiles=meta.tiles, cu_host=meta.cu_host)
+            return self.pc.all_reduce_tp(F.linear(a, L["o"]))
+
+        x = self._layers(self._embed(ids), attn)
+        return self._logits(x.index_select(0, meta.last_idx))
+
+    def forward_decode(self, ids: torch.Tensor, meta: DecodeMeta, kv_caches,
+                       attn_out: torch.Tensor | None = None) -> torch.Tensor:
+        """One token per sequence; static shapes (graph-capturable)."""
+        cfg, sh = self.cfg, self.sh
+        D = cfg.head_dim
+        B = ids.shape[0]
+
+        def attn(i, L, x):
+            qkv = F.linear(x, L["qkv"])
+            kc, vc = kv_caches[i]
+            ops.rope_kv_(qkv, meta.positions, meta.slots, self.cos_sin, sh.hq, sh.hkv, D,
+                         kc, vc, ops.KV_BLOCK)
+            q = qkv.as_strided((B, sh.hq, D), (qkv.stride(0), D, 1))
+            a = ops.paged_decode_attention(q, kc, vc, meta.block_tables, meta.context_lens,
+                                           cfg.attn_scale, out=attn_out,
+                                           blocks_per_part=meta.blocks_per_part,
+                                           workspace=meta.workspace)
+            return self.pc.all_reduce_tp(F.linear(a.view(B, sh.hq * D), L["o"]))
+
+        x = self._layers(self._embed(ids), attn)
+        return self._logits(x)
+
+    # ------------------------------------------------------------ reference
+    def forward_reference(self, ids_list: list[list[int]]) -> list[torch.Tensor]:
+        """Plain full-sequence causal forward (no cache) -> per-sequence logits
+        of every position; used by tests to check prefill+decode equivalence."""
+        outs = []
+        cfg, sh = self.cfg, self.sh
+        for ids in ids_list:
+            n = len(ids)
+            t = torch.tensor(ids, dtype=torch.long, device=self.device)
+            meta = PrefillMeta(
+                positions=torch.arange(n, dtype=torch.int32, device=self.device),
+                slots=torch.full((n,), -1, dtype=torch.int64, device=self.device),
+                cu_seqlens=torch.tensor([0, n], dtype=torch.int32, device=self.device),
+                cu_host=[0, n], tiles=None,
+                last_idx=torch.arange(n, dtype=torch.int64, device=self.device))
+            outs.append(self.forward_prefill(t, meta, None))
+        return outs

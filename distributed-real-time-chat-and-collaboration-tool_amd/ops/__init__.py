@@ -1,0 +1,23 @@
+"""Hot ops of the inference engine.
+
+Each op dispatches on the tensor's device: GPU tensors run the hand-written
+CDNA4 HIP kernel (``csrc/kernels``), CPU tensors run the fp32 PyTorch
+reference of the same op (used by the CPU tests and as the GPU numerics
+oracle).  Plain projection GEMMs are ``torch.nn.functional.linear``
+(hipBLASLt on ROCm); everything around them is fused here.
+"""
+from ._ext import reference_mode
+from .activation import act_glu, act_glu_ref
+from .attention import (KV_BLOCK, DecodeWorkspace, decode_partitioning, paged_decode_attention,
+                        paged_decode_ref, prefill_attention, prefill_attention_ref, prefill_tiles)
+from .norm import rmsnorm, rmsnorm_ref
+from .rope import build_rope_cache, rope_kv_, rope_kv_ref
+from .sampling import sample, sample_ref
+
+__all__ = [
+    "reference_mode",
+    "act_glu", "act_glu_ref", "KV_BLOCK", "DecodeWorkspace", "decode_partitioning",
+    "paged_decode_attention", "paged_decode_ref", "prefill_attention", "prefill_attention_ref",
+    "prefill_tiles", "rmsnorm", "rmsnorm_ref", "build_rope_cache", "rope_kv_", "rope_kv_ref",
+    "sample", "sample_ref",
+]

@@ -1,0 +1,169 @@
+"""Attention: varlen causal prefill and paged decode (GQA/MQA).
+
+HIP kernels: csrc/kernels/attention_prefill.hip, csrc/kernels/attention_decode.hip.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from ._ext import check, hipk, on_gpu, ptr, stream_ptr
+
+KV_BLOCK = 32  # tokens per cache block (fixed by the decode kernel)
+PREFILL_QTILE = 64
+
+
+# ----------------------------------------------------------------- prefill
+def prefill_tiles(cu_seqlens: list[int]) -> tuple[list[int], list[int]]:
+    """Host-side 64-row query tile map for a packed batch, longest sequences
+    first (causal tiles near the end of long sequences are the heaviest)."""
+    seqs = []
+    for s in range(len(cu_seqlens) - 1):
+        n = cu_seqlens[s + 1] - cu_seqlens[s]
+        for q0 in range(0, n, PREFILL_QTILE):
+            seqs.append((-(q0 + PREFILL_QTILE), s, q0))
+    seqs.sort()
+    return [s for _, s, _ in seqs], [q for _, _, q in seqs]
+
+
+def prefill_attention_ref(qkv, cu_seqlens, Hq, Hkv, D, scale, causal=True):
+    T = qkv.shape[0]
+    out = torch.empty((T, Hq * D), dtype=qkv.dtype, device=qkv.device)
+    G = Hq // Hkv
+    cu = [int(x) for x in cu_seqlens]
+    for s in range(len(cu) - 1):
+        a, b = cu[s], cu[s + 1]
+        if b == a:
+            continue
+        n = b - a
+        q = qkv[a:b, : Hq * D].reshape(n, Hq, D).float().transpose(0, 1)
+        k = qkv[a:b, Hq * D:(Hq + Hkv) * D].reshape(n, Hkv, D).float().transpose(0, 1)
+        v = qkv[a:b, (Hq + Hkv) * D:(Hq + 2 * Hkv) * D].reshape(n, Hkv, D).float().transpose(0, 1)
+        k = k.repeat_interleave(G, dim=0)
+        v = v.repeat_interleave(G, dim=0)
+        sc = torch.matmul(q, k.transpose(1, 2)) * scale
+        if causal:
+            mask = torch.ones(n, n, dtype=torch.bool, device=qkv.device).triu(1)
+            sc = sc.masked_fill(mask, float("-inf"))
+        o = torch.matmul(torch.softmax(sc, dim=-1), v)
+        out[a:b] = o.transpose(0, 1).reshape(n, Hq * D).to(qkv.dtype)
+    return out
+
+
+def prefill_attention(qkv: torch.Tensor, cu_seqlens: torch.Tensor, Hq: int, Hkv: int,
+                      D: int, scale: float, causal: bool = True,
+                      tiles: tuple[torch.Tensor, torch.Tensor] | None = None,
+                      cu_host: list[int] | None = None,
+                      out: torch.Tensor | None = None) -> torch.Tensor:
+    """Packed varlen attention reading q/k/v from the fused QKV buffer.
+
+    qkv: [T, >= (Hq + 2Hkv) * D] bf16 (RoPE already applied);
+    cu_seqlens: int32 [nseq + 1]. Returns [T, Hq * D]."""
+    if not on_gpu(qkv):
+        return prefill_attention_ref(qkv, cu_host if cu_host is not None else cu_seqlens.tolist(),
+                                     Hq, Hkv, D, scale, causal)
+    assert qkv.dtype == torch.bfloat16 and qkv.stride(1) == 1
+    assert qkv.shape[1] >= (Hq + 2 * Hkv) * D and Hq % Hkv == 0
+    assert cu_seqlens.dtype == torch.int32 and cu_seqlens.is_cuda
+    T = qkv.shape[0]
+    if out is None:
+        out = torch.empty((T, Hq * D), dtype=qkv.dtype, device=qkv.device)
+    assert out.stride(1) == 1 and out.shape[0] == T and out.shape[1] >= Hq * D
+    if tiles is None:
+        cu = cu_host if cu_host is not None else cu_seqlens.tolist()
+        assert cu[-1] <= T
+        ts, tq = prefill_tiles(cu)
+        dev = qkv.device
+        tiles = (torch.tensor(ts, dtype=torch.int32, device=dev),
+                 torch.tensor(tq, dtype=torch.int32, device=dev))
+    ntiles = tiles[0].numel()
+    check(hipk().prefill_attn(out.data_ptr(), out.stride(0), qkv.data_ptr(), qkv.stride(0),
+                              Hq, Hkv, D, cu_seqlens.data_ptr(), tiles[0].data_ptr(),
+                              tiles[1].data_ptr(), ntiles, float(scale), int(causal),
+                              stream_ptr(qkv)), "prefill_attn")
+    return out
+
+
+# ------------------------------------------------------------------ decode
+def decode_partitioning(batch: int, Hkv: int, max_blocks: int, target_wgs: int = 2048):
+    """Static (graph-capturable) split of the context into partitions.
+
+    Returns (blocks_per_part, max_parts): enough partitions to put roughly
+    ``target_wgs`` workgroups on the 256 CUs when the batch alone cannot."""
+    parts_wanted = max(1, math.ceil(target_wgs / max(1, batch * Hkv)))
+    bpp = max(4, math.ceil(max_blocks / parts_wanted))
+    bpp = ((bpp + 3) // 4) * 4
+    max_parts = max(1, math.ceil(max_blocks / bpp))
+    return bpp, max_parts
+
+
+def paged_decode_ref(q, k_cache, v_cache, block_tables, context_lens, scale):
+    B, Hq, D = q.shape
+    Hkv, bs = k_cache.shape[1], k_cache.shape[2]
+    G = Hq // Hkv
+    out = torch.zeros((B, Hq, D), dtype=q.dtype, device=q.device)
+    for b in range(B):
+        ctx = int(context_lens[b])
+        if ctx <= 0:
+            continue
+        nblk = (ctx + bs - 1) // bs
+        blocks = block_tables[b, :nblk].long()
+        k = k_cache[blocks].permute(1, 0, 2, 3).reshape(Hkv, nblk * bs, D)[:, :ctx].float()
+        v = v_cache[blocks].permute(1, 0, 3, 2).reshape(Hkv, nblk * bs, D)[:, :ctx].float()
+        qh = q[b].reshape(Hkv, G, D).float()
+        s = torch.einsum("hgd,htd->hgt", qh, k) * scale
+        p = torch.softmax(s, dim=-1)
+        out[b] = torch.einsum("hgt,htd->hgd", p, v).reshape(Hq, D).to(q.dtype)
+    return out
+
+
+class DecodeWorkspace:
+    """fp32 split-K partial buffers for one (batch bucket, partitioning)."""
+
+    def __init__(self, batch: int, Hq: int, D: int, max_parts: int, device):
+        self.max_parts = max_parts
+        if max_parts > 1:
+            self.part_o = torch.empty((batch, Hq, max_parts, D), dtype=torch.float32, device=device)
+            self.part_ml = torch.empty((batch, Hq, max_parts, 2), dtype=torch.float32, device=device)
+        else:
+            self.part_o = self.part_ml = None
+
+
+def paged_decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
+                           block_tables: torch.Tensor, context_lens: torch.Tensor,
+                           scale: float, out: torch.Tensor | None = None,
+                           blocks_per_part: int | None = None,
+                           workspace: DecodeWorkspace | None = None) -> torch.Tensor:
+    """One query token per sequence against the paged cache.
+
+    q: [B, Hq, D] view (row stride may exceed Hq*D, e.g. the fused QKV row);
+    block_tables: int32 [B, max_blocks]; context_lens: int32 [B]."""
+    if not on_gpu(q):
+        r = paged_decode_ref(q, k_cache, v_cache, block_tables, context_lens, scale)
+        if out is not None:
+            out.copy_(r)
+            return out
+        return r
+    B, Hq, D = q.shape
+    assert q.dtype == torch.bfloat16 and q.stride(2) == 1 and q.stride(1) == D
+    nb, Hkv, bs, D2 = k_cache.shape
+    assert bs == KV_BLOCK and D2 == D and k_cache.is_contiguous() and v_cache.is_contiguous()
+    assert v_cache.shape == (nb, Hkv, D, bs)
+    assert Hq % Hkv == 0 and Hq // Hkv <= 16
+    assert block_tables.dtype == torch.int32 and block_tables.stride(1) == 1
+    assert context_lens.dtype == torch.int32 and context_lens.numel() >= B
+    max_blocks = block_tables.shape[1]
+    if blocks_per_part is None or workspace is None:
+        blocks_per_part, max_parts = decode_partitioning(B, Hkv, max_blocks)
+        workspace = DecodeWorkspace(B, Hq, D, max_parts, q.device)
+    if out is None:
+        out = torch.empty((B, Hq, D), dtype=q.dtype, device=q.device)
+    assert out.is_contiguous() and out.shape == (B, Hq, D)
+    check(hipk().paged_decode(out.data_ptr(), ptr(workspace.part_o), ptr(workspace.part_ml),
+                              q.data_ptr(), q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
+                              block_tables.data_ptr(), block_tables.stride(0),
+                              context_lens.data_ptr(), B, Hq, Hkv, D, float(scale),
+                              workspace.max_parts, blocks_per_part, stream_ptr(q)),
+          "paged_decode")
+    return out

@@ -1,0 +1,48 @@
+"""RMSNorm (+ fused residual add).  HIP kernel: csrc/kernels/norm_act_rope.hip."""
+from __future__ import annotations
+
+import torch
+
+from ._ext import check, hipk, on_gpu, ptr, stream_ptr
+
+
+def rmsnorm_ref(x: torch.Tensor, w: torch.Tensor, eps: float, gemma: bool = False,
+                residual: torch.Tensor | None = None) -> torch.Tensor:
+    """fp32 PyTorch reference.  With ``residual`` the sum x + residual is
+    rounded to the activation dtype, written back into ``residual`` and
+    normalised (the HF pre-norm residual stream semantics)."""
+    if residual is not None:
+        s = (x.float() + residual.float()).to(residual.dtype)
+        residual.copy_(s)
+        x = s
+    xf = x.float()
+    r = torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps)
+    ww = w.float() + (1.0 if gemma else 0.0)
+    return (xf * r * ww).to(x.dtype)
+
+
+def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float, gemma: bool = False,
+            residual: torch.Tensor | None = None,
+            out: torch.Tensor | None = None) -> torch.Tensor:
+    """out = norm(x [+ residual]) * w (Gemma: * (1 + w)); x: [rows, H]."""
+    if not on_gpu(x):
+        r = rmsnorm_ref(x, w, eps, gemma, residual)
+        if out is not None:
+            out.copy_(r)
+            return out
+        return r
+    assert x.dim() == 2 and x.dtype == torch.bfloat16 and x.stride(1) == 1
+    rows, H = x.shape
+    assert w.shape == (H,) and w.dtype == torch.bfloat16 and w.is_contiguous()
+    assert H % 8 == 0 and H <= 8192 * 2
+    if out is None:
+        out = torch.empty((rows, H), dtype=x.dtype, device=x.device)
+    assert out.stride(1) == 1 and out.shape == (rows, H)
+    res_stride = 0
+    if residual is not None:
+        assert residual.shape == (rows, H) and residual.stride(1) == 1
+        res_stride = residual.stride(0)
+    check(hipk().rmsnorm(out.data_ptr(), ptr(residual), x.data_ptr(), w.data_ptr(),
+                         rows, H, float(eps), x.stride(0), out.stride(0), res_stride,
+                         bool(gemma), stream_ptr(x)), "rmsnorm")
+    return out

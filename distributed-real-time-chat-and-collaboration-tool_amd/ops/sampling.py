@@ -1,0 +1,65 @@
+"""Token sampling: greedy / temperature + top-k + top-p.
+
+HIP kernel: csrc/kernels/sampling.hip (one workgroup per row; graph-replayable
+because the RNG step counter lives in device memory).
+"""
+from __future__ import annotations
+
+import torch
+
+from ._ext import check, hipk, on_gpu, ptr, stream_ptr
+
+MAX_CANDIDATES = 1024
+
+
+def sample_ref(logits: torch.Tensor, temperature: torch.Tensor | None = None,
+               top_k: torch.Tensor | None = None, top_p: torch.Tensor | None = None,
+               generator: torch.Generator | None = None) -> torch.Tensor:
+    B, V = logits.shape
+    out = torch.empty(B, dtype=torch.int32, device=logits.device)
+    lf = logits.float()
+    for b in range(B):
+        t = float(temperature[b]) if temperature is not None else 0.0
+        if t <= 0:
+            out[b] = int(torch.argmax(lf[b]))
+            continue
+        k = int(top_k[b]) if top_k is not None and int(top_k[b]) > 0 else MAX_CANDIDATES
+        k = min(k, MAX_CANDIDATES, V)
+        vals, idx = torch.topk(lf[b], k)
+        p = torch.softmax(vals / t, dim=-1)
+        pp = float(top_p[b]) if top_p is not None and 0 < float(top_p[b]) < 1 else 1.0
+        cum = torch.cumsum(p, 0)
+        cut = int(torch.searchsorted(cum, torch.tensor(pp * float(cum[-1]))))
+        cut = min(cut, k - 1)
+        p = p[: cut + 1]
+        j = int(torch.multinomial(p / p.sum(), 1, generator=generator))
+        out[b] = int(idx[j])
+    return out
+
+
+def sample(logits: torch.Tensor, temperature: torch.Tensor | None = None,
+           top_k: torch.Tensor | None = None, top_p: torch.Tensor | None = None,
+           seed: int = 0, step: torch.Tensor | None = None,
+           out: torch.Tensor | None = None) -> torch.Tensor:
+    """logits [B, V] bf16 -> int32 token ids [B].
+
+    temperature/top_k/top_p are per-row device tensors (float32 / int32 /
+    float32); ``step`` is an int64 device scalar the caller advances."""
+    if not on_gpu(logits):
+        r = sample_ref(logits, temperature, top_k, top_p)
+        if out is not None:
+            out.copy_(r)
+            return out
+        return r
+    assert logits.dim() == 2 and logits.dtype == torch.bfloat16 and logits.stride(1) == 1
+    B, V = logits.shape
+    for t, dt in ((temperature, torch.float32), (top_k, torch.int32), (top_p, torch.float32)):
+        assert t is None or (t.dtype == dt and t.numel() >= B and t.is_cuda)
+    assert step is None or (step.dtype == torch.int64 and step.is_cuda)
+    if out is None:
+        out = torch.empty(B, dtype=torch.int32, device=logits.device)
+    assert out.dtype == torch.int32 and out.is_contiguous()
+    check(hipk().sample(out.data_ptr(), logits.data_ptr(), B, V, logits.stride(0),
+                        ptr(temperature), ptr(top_k), ptr(top_p), int(seed) & ((1 << 64) - 1),
+                        ptr(step), stream_ptr(logits)), "sample")
+    return out

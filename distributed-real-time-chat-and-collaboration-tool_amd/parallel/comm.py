@@ -1,0 +1,84 @@
+"""Process-group plumbing: one process per GPU, torch.distributed over RCCL.
+
+On ROCm the ``"nccl"`` backend *is* RCCL; on CPU (tests) ``"gloo"`` is used
+with the same code path.  A :class:`ParallelContext` carries the tensor-
+parallel (TP) and expert-parallel (EP) groups a model shard needs; the
+data-parallel (DP) dimension is replica-level (one engine per GPU, requests
+routed by the LLM service) and needs no collective on the hot path.
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass
+
+import torch
+import torch.distributed as dist
+
+
+def env_rank_world() -> tuple[int, int, int]:
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    return rank, world, local
+
+
+def init_distributed(backend: str | None = None, device: torch.device | None = None) -> tuple[int, int]:
+    """Initialise the default process group from torchrun's env (idempotent)."""
+    rank, world, local = env_rank_world()
+    if world <= 1:
+        return 0, 1
+    if dist.is_initialized():
+        return dist.get_rank(), dist.get_world_size()
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    if backend is None:
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+    kw = {}
+    if backend == "nccl":
+        torch.cuda.set_device(local)
+        kw["device_id"] = torch.device("cuda", local)
+    dist.init_process_group(backend=backend, rank=rank, world_size=world, **kw)
+    return rank, world
+
+
+@dataclass
+class ParallelContext:
+    tp_size: int = 1
+    tp_rank: int = 0
+    tp_group: object = None
+    ep_size: int = 1
+    ep_rank: int = 0
+    ep_group: object = None
+
+    @staticmethod
+    def single() -> "ParallelContext":
+        return ParallelContext()
+
+    @staticmethod
+    def from_world(tp: bool = True, ep: bool = False) -> "ParallelContext":
+        """Use the whole default group for TP (and/or EP)."""
+        if not dist.is_initialized() or dist.get_world_size() == 1:
+            return ParallelContext()
+        r, w = dist.get_rank(), dist.get_world_size()
+        ctx = ParallelContext()
+        if tp:
+            ctx.tp_size, ctx.tp_rank, ctx.tp_group = w, r, dist.group.WORLD
+        if ep:
+            ctx.ep_size, ctx.ep_rank, ctx.ep_group = w, r, dist.group.WORLD
+        return ctx
+
+    def all_reduce_tp(self, x: torch.Tensor) -> torch.Tensor:
+        if self.tp_size > 1:
+            dist.all_reduce(x, group=self.tp_group)
+        return x
+
+    def all_reduce_ep(self, x: torch.Tensor) -> torch.Tensor:
+        if self.ep_size > 1:
+            dist.all_reduce(x, group=self.ep_group)
+        return x
+
+    def all_gather_tp_lastdim(self, x: torch.Tensor) -> torch.Tensor:
+        if self.tp_size == 1:
+            return x
+        parts = [torch.empty_like(x) for _ in range(self.tp_size)]
+        dist.all_gather(parts, x.contiguous(), group=self.tp_group)
+        return torch.cat(parts, dim=-1)

@@ -1,0 +1,201 @@
+"""Numerics of every HIP kernel against the fp32 PyTorch reference of the same op."""
+import math
+
+import pytest
+import torch
+
+from drtc_amd import ops
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _close(a, b, atol, rtol=0.0, msg=""):
+    a, b = a.float(), b.float()
+    err = (a - b).abs()
+    tol = atol + rtol * b.abs()
+    bad = err > tol
+    assert not bad.any(), f"{msg} max err {err.max().item():.4g} at {bad.nonzero()[:4].tolist()}"
+
+
+@pytest.mark.parametrize("H", [256, 2048, 4096, 8192])
+@pytest.mark.parametrize("gemma", [False, True])
+@pytest.mark.parametrize("resid", [False, True])
+def test_rmsnorm(hipk, H, gemma, resid):
+    torch.manual_seed(0)
+    rows = 37
+    x = torch.randn(rows, H, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(H, device=DEV) * 0.1 + (0 if gemma else 1)).to(torch.bfloat16)
+    r1 = torch.randn(rows, H, device=DEV).to(torch.bfloat16) if resid else None
+    r2 = r1.clone() if resid else None
+    y = ops.rmsnorm(x, w, 1e-5, gemma, residual=r1)
+    with ops.reference_mode():
+        yr = ops.rmsnorm(x, w, 1e-5, gemma, residual=r2)
+    _close(y, yr, 2e-2, 2e-2, "rmsnorm")
+    if resid:
+        assert torch.equal(r1, r2)
+
+
+def test_rmsnorm_strided_input(hipk):
+    x = torch.randn(16, 1024, device=DEV).to(torch.bfloat16)[:, :512]
+    w = torch.ones(512, device=DEV, dtype=torch.bfloat16)
+    _close(ops.rmsnorm(x, w, 1e-6), ops.rmsnorm_ref(x, w, 1e-6), 2e-2, 2e-2)
+
+
+@pytest.mark.parametrize("act", ["silu", "gelu_tanh"])
+@pytest.mark.parametrize("T,I", [(1, 512), (33, 14336), (300, 2048)])
+def test_act_glu(hipk, act, T, I):
+    gu = torch.randn(T, 2 * I, device=DEV).to(torch.bfloat16) * 3
+    _close(ops.act_glu(gu, act), ops.act_glu_ref(gu, act), 3e-2, 1e-2, act)
+
+
+@pytest.mark.parametrize("D,Hq,Hkv", [(128, 32, 8), (256, 8, 1), (64, 4, 2)])
+def test_rope_kv(hipk, D, Hq, Hkv):
+    torch.manual_seed(1)
+    T, nb, bs = 70, 16, ops.KV_BLOCK
+    qkv = torch.randn(T, (Hq + 2 * Hkv) * D, device=DEV).to(torch.bfloat16)
+    pos = torch.randint(0, 4000, (T,), device=DEV, dtype=torch.int32)
+    perm = torch.randperm(nb * bs, device=DEV)[:T].to(torch.int64)
+    perm[5] = -1
+    cs = ops.build_rope_cache(4096, D, 5e5, device=DEV)
+    kc = torch.zeros(nb, Hkv, bs, D, device=DEV, dtype=torch.bfloat16)
+    vc = torch.zeros(nb, Hkv, D, bs, device=DEV, dtype=torch.bfloat16)
+    kc2, vc2, q2 = kc.clone(), vc.clone(), qkv.clone()
+    ops.rope_kv_(qkv, pos, perm, cs, Hq, Hkv, D, kc, vc, bs)
+    ops.rope_kv_ref(q2, pos, perm, cs, Hq, Hkv, D, kc2, vc2, bs)
+    _close(qkv, q2, 2e-2, 1e-2, "qkv")
+    _close(kc, kc2, 2e-2, 1e-2, "kcache")
+    assert torch.equal(vc, vc2)
+
+
+def _paged_setup(B, Hq, Hkv, D, ctx_lens, nb_total=None, seed=0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    bs = ops.KV_BLOCK
+    maxb = max(1, max(math.ceil(c / bs) for c in ctx_lens))
+    nb_total = nb_total or (B * maxb + 3)
+    kc = torch.randn(nb_total, Hkv, bs, D, generator=g).to(torch.bfloat16).to(DEV)
+    vc = torch.randn(nb_total, Hkv, D, bs, generator=g).to(torch.bfloat16).to(DEV)
+    perm = torch.randperm(nb_total - 1, generator=g) + 1
+    bt = torch.zeros(B, maxb, dtype=torch.int32)
+    k = 0
+    for b, c in enumerate(ctx_lens):
+        n = math.ceil(c / bs)
+        bt[b, :n] = perm[k:k + n].to(torch.int32)
+        k += n
+    q = torch.randn(B, Hq, D, generator=g).to(torch.bfloat16).to(DEV)
+    return q, kc, vc, bt.to(DEV), torch.tensor(ctx_lens, dtype=torch.int32, device=DEV)
+
+
+@pytest.mark.parametrize("D,Hq,Hkv", [(128, 32, 8), (128, 64, 8), (256, 8, 1), (64, 4, 2),
+                                      (128, 16, 16)])
+@pytest.mark.parametrize("ctx_lens", [[1, 31, 32, 33, 100, 257], [513, 1000, 2048], [5]])
+def test_paged_decode(hipk, D, Hq, Hkv, ctx_lens):
+    B = len(ctx_lens)
+    q, kc, vc, bt, cl = _paged_setup(B, Hq, Hkv, D, ctx_lens)
+    scale = D ** -0.5
+    ref = ops.paged_decode_ref(q, kc, vc, bt, cl, scale)
+    out = ops.paged_decode_attention(q, kc, vc, bt, cl, scale)
+    _close(out, ref, 2e-2, 2e-2, "decode")
+    # force a multi-partition split-K
+    ws = ops.DecodeWorkspace(B, Hq, D, math.ceil(bt.shape[1] / 4), DEV)
+    out2 = ops.paged_decode_attention(q, kc, vc, bt, cl, scale, blocks_per_part=4, workspace=ws)
+    _close(out2, ref, 2e-2, 2e-2, "decode split")
+
+
+def test_paged_decode_strided_q_and_padding(hipk):
+    Hq, Hkv, D = 32, 8, 128
+    ctx = [40, 0, 77]
+    q, kc, vc, bt, cl = _paged_setup(3, Hq, Hkv, D, [40, 1, 77])
+    cl[1] = 0
+    big = torch.zeros(3, (Hq + 2 * Hkv) * D, device=DEV, dtype=torch.bfloat16)
+    big[:, :Hq * D] = q.reshape(3, -1)
+    qv = big.as_strided((3, Hq, D), (big.stride(0), D, 1))
+    out = ops.paged_decode_attention(qv, kc, vc, bt, cl, D ** -0.5)
+    ref = ops.paged_decode_ref(q, kc, vc, bt, cl, D ** -0.5)
+    _close(out, ref, 2e-2, 2e-2)
+    assert out[1].abs().max().item() == 0.0
+    assert ctx
+
+
+def test_paged_decode_spike(hipk):
+    """One key dominating forces the online-softmax rescale branch."""
+    Hq, Hkv, D = 8, 2, 128
+    q, kc, vc, bt, cl = _paged_setup(2, Hq, Hkv, D, [300, 700])
+    kc[bt[0, 5].long(), :, 7, :] = q[0, 0].float().sign().to(torch.bfloat16) * 4
+    ref = ops.paged_decode_ref(q, kc, vc, bt, cl, D ** -0.5)
+    out = ops.paged_decode_attention(q, kc, vc, bt, cl, D ** -0.5)
+    _close(out, ref, 2e-2, 2e-2)
+
+
+@pytest.mark.parametrize("D,Hq,Hkv", [(128, 32, 8), (256, 8, 1), (64, 4, 4)])
+@pytest.mark.parametrize("lens", [[1], [7, 64, 65, 200], [513, 3]])
+def test_prefill_attention(hipk, D, Hq, Hkv, lens):
+    torch.manual_seed(2)
+    T = sum(lens)
+    qkv = torch.randn(T, (Hq + 2 * Hkv) * D, device=DEV).to(torch.bfloat16)
+    cu = [0]
+    for n in lens:
+        cu.append(cu[-1] + n)
+    cu_d = torch.tensor(cu, dtype=torch.int32, device=DEV)
+    scale = D ** -0.5
+    out = ops.prefill_attention(qkv, cu_d, Hq, Hkv, D, scale, True, cu_host=cu)
+    ref = ops.prefill_attention_ref(qkv, cu, Hq, Hkv, D, scale, True)
+    _close(out, ref, 2e-2, 2e-2, "prefill")
+
+
+def test_prefill_noncausal(hipk):
+    D, Hq, Hkv = 128, 4, 2
+    lens = [100, 30]
+    T = sum(lens)
+    qkv = torch.randn(T, (Hq + 2 * Hkv) * D, device=DEV).to(torch.bfloat16)
+    cu = [0, 100, 130]
+    cu_d = torch.tensor(cu, dtype=torch.int32, device=DEV)
+    out = ops.prefill_attention(qkv, cu_d, Hq, Hkv, D, 0.1, False, cu_host=cu)
+    ref = ops.prefill_attention_ref(qkv, cu, Hq, Hkv, D, 0.1, False)
+    _close(out, ref, 2e-2, 2e-2)
+
+
+def test_sample_greedy(hipk):
+    torch.manual_seed(3)
+    logits = torch.randn(9, 128256, device=DEV).to(torch.bfloat16)
+    logits[4, 77] = 50.0
+    t = torch.zeros(9, device=DEV)
+    out = ops.sample(logits, t)
+    assert torch.equal(out.cpu().long(), logits.float().argmax(-1).cpu())
+    assert int(out[4]) == 77
+    assert torch.equal(ops.sample(logits).cpu().long(), logits.float().argmax(-1).cpu())
+
+
+def test_sample_topk_topp(hipk):
+    torch.manual_seed(4)
+    B, V = 64, 32000
+    logits = torch.randn(B, V, device=DEV).to(torch.bfloat16)
+    temp = torch.full((B,), 1.0, device=DEV)
+    k = torch.full((B,), 5, dtype=torch.int32, device=DEV)
+    p = torch.ones(B, device=DEV)
+    step = torch.zeros(1, dtype=torch.int64, device=DEV)
+    top5 = logits.float().topk(5, dim=-1).indices
+    seen = set()
+    for i in range(20):
+        step.fill_(i)
+        out = ops.sample(logits, temp, k, p, seed=7, step=step).long()
+        assert (top5 == out[:, None]).any(-1).all()
+        seen.add(tuple(out.tolist()))
+    assert len(seen) > 1  # the step counter changes the draw
+    # top-p tiny -> always the argmax
+    p2 = torch.full((B,), 1e-4, device=DEV)
+    out = ops.sample(logits, temp, torch.zeros_like(k), p2, seed=1, step=step).long()
+    assert torch.equal(out, logits.float().argmax(-1))
+
+
+def test_sample_distribution(hipk):
+    """Empirical frequencies of a 3-way softmax match exp(l/T)."""
+    V = 1000
+    logits = torch.full((1, V), -30.0, device=DEV)
+    logits[0, 10], logits[0, 20], logits[0, 30] = 2.0, 1.0, 0.0
+    logits = logits.to(torch.bfloat16).repeat(4096, 1)
+    temp = torch.full((4096,), 1.0, device=DEV)
+    out = ops.sample(logits, temp, None, None, seed=3, step=None).long().cpu()
+    f = torch.bincount(out, minlength=V)[[10, 20, 30]].float() / 4096
+    e = torch.softmax(torch.tensor([2.0, 1.0, 0.0]), 0)
+    assert (f - e).abs().max() < 0.04, (f, e)
