@@ -34,6 +34,15 @@ from .request import Request, RequestState, SamplingParams
 BS = ops.KV_BLOCK
 
 
+def _pad_tokens(T: int) -> int:
+    """Prefill token-count bucket (<= ~1.5% padding above 4k tokens)."""
+    if T <= 256:
+        return -(-T // 32) * 32
+    if T <= 4096:
+        return -(-T // 256) * 256
+    return -(-T // 1024) * 1024
+
+
 class LLMEngine:
     def __init__(self, model: TransformerLM, max_batch: int = 256, max_model_len: int = 4096,
                  max_prefill_tokens: int = 16384, num_blocks: int | None = None,
@@ -183,9 +192,16 @@ class LLMEngine:
         for n in lens:
             cu.append(cu[-1] + n)
         T = cu[-1]
-        ids = np.concatenate([np.asarray(s, dtype=np.int32) for s in seqs])
-        pos = np.concatenate([np.arange(n, dtype=np.int32) for n in lens])
-        slots = np.empty(T, dtype=np.int64)
+        # pad the token count to a coarse bucket: hipBLASLt picks (and caches)
+        # its kernels per GEMM shape, so stable shapes avoid re-heuristics and
+        # first-use code-object loads on every prefill.  Padded rows carry
+        # position 0 and slot -1 (no cache write) and are never attended.
+        Tp = _pad_tokens(T)
+        ids = np.zeros(Tp, dtype=np.int32)
+        ids[:T] = np.concatenate([np.asarray(s, dtype=np.int32) for s in seqs])
+        pos = np.zeros(Tp, dtype=np.int32)
+        pos[:T] = np.concatenate([np.arange(n, dtype=np.int32) for n in lens])
+        slots = np.full(Tp, -1, dtype=np.int64)
         for r, a, n in zip(batch, cu[:-1], lens):
             blk = np.asarray(r.blocks, dtype=np.int64)
             p = np.arange(n)
@@ -198,13 +214,13 @@ class LLMEngine:
         t_i64 = torch.from_numpy(np.concatenate([slots, last_idx])).to(dev, non_blocking=True)
         nseq, nt = len(batch), len(ts)
         o = 0
-        d_ids = t_i32[o:o + T]; o += T
-        d_pos = t_i32[o:o + T]; o += T
+        d_ids = t_i32[o:o + Tp]; o += Tp
+        d_pos = t_i32[o:o + Tp]; o += Tp
         d_cu = t_i32[o:o + nseq + 1]; o += nseq + 1
         d_ts = t_i32[o:o + nt]; o += nt
         d_tq = t_i32[o:o + nt]
-        meta = PrefillMeta(positions=d_pos, slots=t_i64[:T], cu_seqlens=d_cu, cu_host=cu,
-                           tiles=(d_ts, d_tq), last_idx=t_i64[T:])
+        meta = PrefillMeta(positions=d_pos, slots=t_i64[:Tp], cu_seqlens=d_cu, cu_host=cu,
+                           tiles=(d_ts, d_tq), last_idx=t_i64[Tp:])
         logits = self.model.forward_prefill(d_ids, meta, self.kv)
         temp = torch.tensor([r.params.temperature for r in batch], dtype=torch.float32, device=dev)
         topk = torch.tensor([r.params.top_k for r in batch], dtype=torch.int32, device=dev)

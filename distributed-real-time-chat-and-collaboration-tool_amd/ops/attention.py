@@ -29,7 +29,7 @@ def prefill_tiles(cu_seqlens: list[int]) -> tuple[list[int], list[int]]:
 
 def prefill_attention_ref(qkv, cu_seqlens, Hq, Hkv, D, scale, causal=True):
     T = qkv.shape[0]
-    out = torch.empty((T, Hq * D), dtype=qkv.dtype, device=qkv.device)
+    out = torch.zeros((T, Hq * D), dtype=qkv.dtype, device=qkv.device)
     G = Hq // Hkv
     cu = [int(x) for x in cu_seqlens]
     for s in range(len(cu) - 1):
@@ -67,11 +67,13 @@ def prefill_attention(qkv: torch.Tensor, cu_seqlens: torch.Tensor, Hq: int, Hkv:
     assert qkv.shape[1] >= (Hq + 2 * Hkv) * D and Hq % Hkv == 0
     assert cu_seqlens.dtype == torch.int32 and cu_seqlens.is_cuda
     T = qkv.shape[0]
+    cu = cu_host if cu_host is not None else cu_seqlens.tolist()
     if out is None:
-        out = torch.empty((T, Hq * D), dtype=qkv.dtype, device=qkv.device)
+        # rows past cu[-1] (shape padding) are not written by the kernel
+        alloc = torch.zeros if cu[-1] < T else torch.empty
+        out = alloc((T, Hq * D), dtype=qkv.dtype, device=qkv.device)
     assert out.stride(1) == 1 and out.shape[0] == T and out.shape[1] >= Hq * D
     if tiles is None:
-        cu = cu_host if cu_host is not None else cu_seqlens.tolist()
         assert cu[-1] <= T
         ts, tq = prefill_tiles(cu)
         dev = qkv.device

@@ -1,0 +1,82 @@
+#!/usr/bin/env python3
+"""Summarise a rocprofv3 --kernel-trace CSV of bench.py by engine phase.
+
+Each forward pass ends with the fused sampler kernel; the kernels since the
+previous sampler form one pass, classified as prefill (it contains the
+prefill attention kernel) or decode (paged decode attention).  Prints, per
+phase: passes, mean GPU wall per pass, mean busy time per pass, and the
+per-kernel breakdown (shortened names) - a markdown table for profiles/.
+
+usage: prof_summary.py run_kernel_trace.csv [--top 15]
+"""
+import collections
+import csv
+import re
+import sys
+
+
+def short(name: str) -> str:
+    if name.startswith("Cijk") or name.startswith("Custom_Cijk"):
+        m = re.search(r"MT(\d+x\d+x\d+)", name)
+        return f"hipBLASLt GEMM MT{m.group(1) if m else '?'}"
+    m = re.search(r"drtc::(\w+)", name) or re.search(r"drtc(\d+)(\w+?)E", name)
+    if "drtc" in name:
+        for k in ("paged_decode_kernel", "decode_reduce_kernel", "prefill_attn_kernel",
+                  "rmsnorm_kernel", "act_glu_kernel", "rope_kv_kernel", "sample_kernel",
+                  "moe_", "allreduce"):
+            if k in name:
+                return "drtc::" + k
+    if "at::native" in name:
+        m = re.search(r"at::native::(?:\(anonymous namespace\)::)?(\w+)", name)
+        return "torch::" + (m.group(1) if m else "kernel")
+    return name[:60]
+
+
+def main():
+    path = sys.argv[1]
+    top = int(sys.argv[sys.argv.index("--top") + 1]) if "--top" in sys.argv else 15
+    rows = []
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"])))
+    rows.sort()
+    passes = []
+    cur = []
+    for r in rows:
+        cur.append(r)
+        if r[2] == "drtc::sample_kernel":
+            passes.append(cur)
+            cur = []
+    phase_k = {"prefill": collections.Counter(), "decode": collections.Counter()}
+    phase_n = collections.Counter()
+    phase_wall = collections.Counter()
+    phase_busy = collections.Counter()
+    for p in passes:
+        names = {x[2] for x in p}
+        ph = ("prefill" if "drtc::prefill_attn_kernel" in names else
+              "decode" if "drtc::paged_decode_kernel" in names else None)
+        if ph is None:
+            continue
+        # drop leading non-forward kernels (copies etc. are not kernels here)
+        phase_n[ph] += 1
+        phase_wall[ph] += p[-1][1] - p[0][0]
+        for s, e, n in p:
+            phase_k[ph][n] += e - s
+            phase_busy[ph] += e - s
+    print("| phase | passes | mean GPU wall / pass (ms) | mean kernel-busy / pass (ms) |")
+    print("|---|---|---|---|")
+    for ph in ("prefill", "decode"):
+        if phase_n[ph]:
+            print(f"| {ph} | {phase_n[ph]} | {phase_wall[ph] / phase_n[ph] / 1e6:.3f} | "
+                  f"{phase_busy[ph] / phase_n[ph] / 1e6:.3f} |")
+    for ph in ("prefill", "decode"):
+        if not phase_n[ph]:
+            continue
+        tot = sum(phase_k[ph].values())
+        print(f"\n**{ph}** (per pass)\n\n| kernel | ms / pass | share |\n|---|---|---|")
+        for n, t in phase_k[ph].most_common(top):
+            print(f"| {n} | {t / phase_n[ph] / 1e6:.3f} | {100 * t / tot:.1f}% |")
+
+
+if __name__ == "__main__":
+    main()

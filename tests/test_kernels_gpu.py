@@ -174,12 +174,13 @@ def test_sample_topk_topp(hipk):
     k = torch.full((B,), 5, dtype=torch.int32, device=DEV)
     p = torch.ones(B, device=DEV)
     step = torch.zeros(1, dtype=torch.int64, device=DEV)
-    top5 = logits.float().topk(5, dim=-1).indices
+    kth = logits.float().topk(5, dim=-1).values[:, -1]
     seen = set()
     for i in range(20):
         step.fill_(i)
         out = ops.sample(logits, temp, k, p, seed=7, step=step).long()
-        assert (top5 == out[:, None]).any(-1).all()
+        picked = logits.float().gather(1, out[:, None])[:, 0]
+        assert (picked >= kth).all()  # inside the top-5 (bf16 ties at the 5th value allowed)
         seen.add(tuple(out.tolist()))
     assert len(seen) > 1  # the step counter changes the draw
     # top-p tiny -> always the argmax
