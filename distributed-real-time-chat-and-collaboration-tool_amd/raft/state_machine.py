@@ -1,0 +1,244 @@
+"""Replicated chat state machine (the apply side of the Raft log).
+
+Log-entry commands and their JSON payloads are the reference's (SURVEY §2.7,
+server/raft_node.py:1196-1397); in-memory records keep the reference's dict
+schemas so the app-state pickles (users/channels/messages/direct_messages)
+stay byte-compatible.  Differences, all deliberate:
+
+* idempotency by id *sets* (O(1)) instead of linear scans (raft_node.py:1354,1376);
+* secondary indexes for the read RPCs (DMs by user pair / by user id);
+* JOIN_CHANNEL for an unknown channel is dropped instead of silently joining
+  the first default channel found (survey quirk Q13);
+* ``apply`` is deterministic given the entry - nothing node-local (sessions,
+  presence) is touched, so every replica converges to the same state.
+"""
+from __future__ import annotations
+
+import datetime as _dt
+import logging
+import os
+from collections import defaultdict
+
+from ..utils import pickle_compat
+
+log = logging.getLogger(__name__)
+
+DEFAULT_USERS = (("alice", "alice123"), ("bob", "bob123"), ("charlie", "charlie123"))
+DEFAULT_CHANNELS = ("general", "random", "tech")
+
+COMMANDS = ("CREATE_USER", "LOGIN_USER", "CREATE_CHANNEL", "JOIN_CHANNEL", "LEAVE_CHANNEL",
+            "SEND_MESSAGE", "SEND_DM", "UPLOAD_FILE")
+
+
+def _utcnow() -> _dt.datetime:
+    return _dt.datetime.now(_dt.timezone.utc)
+
+
+class ChatState:
+    def __init__(self):
+        self.users: dict[str, dict] = {}
+        self.users_by_id: dict[str, str] = {}
+        self.channels: dict[str, dict] = {}
+        self.channel_messages: dict[str, list] = {}
+        self.direct_messages: list[dict] = []
+        self.files: dict[str, dict] = {}
+        self.online_users: set[str] = set()
+        self._msg_ids: set[str] = set()
+        self._dm_ids: set[str] = set()
+        self._dm_pair: dict[tuple, list] = defaultdict(list)
+        self._dm_user: dict[str, list] = defaultdict(list)
+        self.dirty: set[str] = set()
+
+    # --------------------------------------------------------------- apply
+    def apply(self, command: str, data: dict) -> bool:
+        """Apply one committed entry. Returns False for unknown commands."""
+        fn = getattr(self, "_apply_" + command.lower(), None)
+        if fn is None:
+            log.warning("unknown command %s", command)
+            return False
+        fn(data)
+        return True
+
+    def _apply_create_user(self, d: dict) -> None:
+        name = d["username"]
+        if name in self.users:
+            return
+        self.users[name] = {
+            "id": d["user_id"], "username": name,
+            "password": d["password"].encode("latin1"),
+            "email": d["email"], "display_name": d["display_name"],
+            "is_admin": d["is_admin"], "status": "offline",
+        }
+        self.users_by_id[d["user_id"]] = name
+        self.dirty.add("users")
+
+    def _apply_login_user(self, d: dict) -> None:
+        name = d["username"]
+        if name in self.users:
+            self.users[name]["status"] = "online"
+            self.online_users.add(name)
+            self.dirty.add("users")
+
+    def _apply_create_channel(self, d: dict) -> None:
+        cid = d["channel_id"]
+        if cid in self.channels:
+            return
+        self.channels[cid] = {
+            "id": cid, "name": d["name"], "description": d["description"],
+            "is_private": d["is_private"], "members": set(d["members"]),
+            "admins": set(d["admins"]), "created_at": _utcnow(),
+        }
+        self.channel_messages.setdefault(cid, [])
+        self.dirty.add("channels")
+
+    def _apply_join_channel(self, d: dict) -> None:
+        ch = self.channels.get(d["channel_id"])
+        if ch is None:
+            log.info("JOIN_CHANNEL for unknown channel %s dropped", d["channel_id"])
+            return
+        ch["members"].add(d["user_id"])
+        self.dirty.add("channels")
+
+    def _apply_leave_channel(self, d: dict) -> None:
+        ch = self.channels.get(d["channel_id"])
+        if ch is not None:
+            ch["members"].discard(d["user_id"])
+            self.dirty.add("channels")
+
+    def _apply_send_message(self, d: dict) -> None:
+        mid = d.get("id")
+        if mid in self._msg_ids:
+            return
+        self.channel_messages.setdefault(d["channel_id"], []).append(d)
+        self._msg_ids.add(mid)
+        self.dirty.add("messages")
+
+    def _apply_send_dm(self, d: dict) -> None:
+        did = d.get("id")
+        if did and did in self._dm_ids:
+            return
+        self._index_dm(d)
+        self.direct_messages.append(d)
+        self.dirty.add("direct_messages")
+
+    def _index_dm(self, d: dict) -> None:
+        if d.get("id"):
+            self._dm_ids.add(d["id"])
+        self._dm_pair[tuple(sorted((d["sender_name"], d["recipient_name"])))].append(d)
+        self._dm_user[d["sender_id"]].append(d)
+        if d["recipient_id"] != d["sender_id"]:
+            self._dm_user[d["recipient_id"]].append(d)
+
+    def _apply_upload_file(self, d: dict) -> None:
+        fid = d["file_id"]
+        if fid in self.files:
+            return
+        rec = dict(d)
+        if isinstance(rec.get("data"), str):
+            rec["data"] = bytes.fromhex(rec["data"])
+        self.files[fid] = rec
+
+    # ------------------------------------------------------------- queries
+    def channel_by_name(self, name: str) -> dict | None:
+        for ch in self.channels.values():
+            if ch["name"] == name:
+                return ch
+        return None
+
+    def conversation(self, a: str, b: str) -> list:
+        conv = list(self._dm_pair.get(tuple(sorted((a, b))), ()))
+        conv.sort(key=lambda m: m["timestamp"])
+        return conv
+
+    def dms_of_user(self, user_id: str) -> list:
+        return self._dm_user.get(user_id, [])
+
+    # ------------------------------------------------------------- seeding
+    def seed_defaults(self, hash_password) -> None:
+        """Default users/channels with deterministic ids (username / channel
+        name), identical on every node (server/raft_node.py:426-467)."""
+        ids = []
+        for name, pw in DEFAULT_USERS:
+            self.users[name] = {
+                "id": name, "username": name, "password": hash_password(pw.encode()),
+                "email": f"{name}@chat.com", "display_name": name.title(),
+                "is_admin": False, "status": "offline",
+            }
+            self.users_by_id[name] = name
+            ids.append(name)
+        for cname in DEFAULT_CHANNELS:
+            self.channels[cname] = {
+                "id": cname, "name": cname, "description": f"Default {cname} channel (public)",
+                "is_private": False, "members": set(ids), "admins": set(ids),
+                "created_at": _utcnow(),
+            }
+            self.channel_messages[cname] = []
+        self.dirty.update(("users", "channels"))
+
+    # --------------------------------------------------------- persistence
+    FILES = {"users": "users.pkl", "channels": "channels.pkl", "messages": "messages.pkl",
+             "direct_messages": "direct_messages.pkl"}
+
+    def snapshot_obj(self, which: str):
+        if which == "users":
+            return {"users": self.users, "users_by_id": self.users_by_id}
+        if which == "channels":
+            out = {}
+            for cid, ch in self.channels.items():
+                c = dict(ch)
+                c["members"] = list(ch["members"])
+                c["admins"] = list(ch["admins"]) if isinstance(ch["admins"], set) else ch["admins"]
+                if isinstance(c.get("created_at"), _dt.datetime):
+                    c["created_at"] = c["created_at"].isoformat()
+                out[cid] = c
+            return out
+        if which == "messages":
+            return self.channel_messages
+        if which == "direct_messages":
+            return self.direct_messages
+        raise KeyError(which)
+
+    def save(self, data_dir: str, which=None, fsync: bool = False) -> None:
+        for w in (which or list(self.dirty)):
+            pickle_compat.dump(self.snapshot_obj(w), os.path.join(data_dir, self.FILES[w]), fsync)
+            self.dirty.discard(w)
+
+    def save_all(self, data_dir: str, fsync: bool = False) -> None:
+        self.save(data_dir, list(self.FILES), fsync)
+
+    def load(self, data_dir: str) -> None:
+        """Load app-state pickles (reference layout; also accepts the legacy
+        server's users.pkl with naive datetimes and users_by_email)."""
+        p = os.path.join(data_dir, "users.pkl")
+        if os.path.exists(p):
+            d = pickle_compat.safe_load(p)
+            self.users = d.get("users", {})
+            self.users_by_id = d.get("users_by_id", {})
+        p = os.path.join(data_dir, "channels.pkl")
+        if os.path.exists(p):
+            for cid, ch in pickle_compat.safe_load(p).items():
+                if isinstance(ch.get("members"), (list, tuple)):
+                    ch["members"] = set(ch["members"])
+                if isinstance(ch.get("admins"), (list, tuple)):
+                    ch["admins"] = set(ch["admins"])
+                if isinstance(ch.get("created_at"), str):
+                    try:
+                        ch["created_at"] = _dt.datetime.fromisoformat(ch["created_at"])
+                    except ValueError:
+                        ch["created_at"] = _utcnow()
+                self.channels[cid] = ch
+        p = os.path.join(data_dir, "messages.pkl")
+        if os.path.exists(p):
+            self.channel_messages = pickle_compat.safe_load(p)
+        p = os.path.join(data_dir, "direct_messages.pkl")
+        if os.path.exists(p):
+            self.direct_messages = pickle_compat.safe_load(p)
+        self.reindex()
+
+    def reindex(self) -> None:
+        self._msg_ids = {m.get("id") for ms in self.channel_messages.values() for m in ms}
+        self._dm_ids = set()
+        self._dm_pair = defaultdict(list)
+        self._dm_user = defaultdict(list)
+        for d in self.direct_messages:
+            self._index_dm(d)

@@ -1,0 +1,104 @@
+"""Raft chat node entry point: ``python -m drtc_amd.server.node --node-id 1 --port 50051``.
+
+Defaults mirror the reference (server/raft_node.py:2358-2418): a 3-node
+cluster on localhost:50051-50053, 50 MB gRPC messages, data under
+``./raft_node_{id}_data``, the LLM service at localhost:50055, and a status
+line every 2 s.  Everything is overridable (peers, timings, storage, LLM
+address, token mode, local-commit compatibility mode).
+"""
+from __future__ import annotations
+
+import argparse
+import logging
+import signal
+import threading
+import time
+from concurrent import futures
+
+import grpc
+
+from ..protos import RAFT_SERVICE, add_servicer
+from ..raft.core import RaftConfig
+from ..utils.logging_utils import setup_logging
+from .raft_service import ChatNode, NodeConfig
+
+log = logging.getLogger("drtc_amd.server.node")
+
+DEFAULT_PEERS = {1: "localhost:50051", 2: "localhost:50052", 3: "localhost:50053"}
+SERVER_OPTS = [
+    ("grpc.max_send_message_length", 50 * 1024 * 1024),
+    ("grpc.max_receive_message_length", 50 * 1024 * 1024),
+    ("grpc.keepalive_time_ms", 10000),
+    ("grpc.keepalive_timeout_ms", 5000),
+]
+
+
+def parse_peers(s: str | None) -> dict:
+    if not s:
+        return dict(DEFAULT_PEERS)
+    out = {}
+    for part in s.split(","):
+        k, v = part.split("=", 1)
+        out[int(k)] = v
+    return out
+
+
+def serve(cfg: NodeConfig, block: bool = True, bind: str = "[::]"):
+    node = ChatNode(cfg)
+    server = grpc.server(futures.ThreadPoolExecutor(max_workers=cfg.grpc_workers), options=SERVER_OPTS)
+    add_servicer(server, RAFT_SERVICE, node)
+    port = server.add_insecure_port(f"{bind}:{cfg.port}")
+    if port == 0:
+        raise RuntimeError(f"cannot bind port {cfg.port}")
+    server.start()
+    node.start()
+    log.info("raft chat node %d on port %d (peers %s)", cfg.node_id, cfg.port, cfg.peers)
+    if not block:
+        return node, server
+    stop = threading.Event()
+    signal.signal(signal.SIGINT, lambda *a: stop.set())
+    signal.signal(signal.SIGTERM, lambda *a: stop.set())
+    while not stop.wait(2.0):
+        i = node.rt.leader_info()
+        with node.rt.state_lock:
+            nu, nc, nf = len(node.st.users), len(node.st.channels), len(node.st.files)
+        role = i["state"].upper()
+        lead = f"leader {i['leader_id']}" if i["leader_id"] is not None else "no leader"
+        log.info("node %d %s | term %d | log %d (commit %d) | %d users | %d channels | %d files | %s",
+                 cfg.node_id, role, i["term"], i["log"], i["commit"], nu, nc, nf, lead)
+    server.stop(1.0)
+    node.stop()
+    return node, server
+
+
+def main(argv=None) -> None:
+    ap = argparse.ArgumentParser(description="drtc_amd Raft chat node")
+    ap.add_argument("--node-id", type=int, required=True)
+    ap.add_argument("--port", type=int, required=True)
+    ap.add_argument("--peers", default=None, help="id=host:port,... (default: 3 nodes on localhost)")
+    ap.add_argument("--data-root", default=".")
+    ap.add_argument("--storage", choices=("native", "pickle"), default="native")
+    ap.add_argument("--llm", default="localhost:50055", help="LLM service address ('' disables)")
+    ap.add_argument("--election-timeout", default="1.5,3.0", help="min,max seconds")
+    ap.add_argument("--reference-timing", action="store_true", help="10-15 s election timeout")
+    ap.add_argument("--heartbeat", type=float, default=0.05)
+    ap.add_argument("--local-commit", action="store_true", help="reference quirk Q1 behaviour")
+    ap.add_argument("--token-mode", choices=("replicated", "reference"), default="replicated")
+    ap.add_argument("--bcrypt-rounds", type=int, default=12)
+    ap.add_argument("--fsync", action="store_true")
+    ap.add_argument("--log-level", default="INFO")
+    a = ap.parse_args(argv)
+    setup_logging(a.log_level)
+    lo, hi = (10.0, 15.0) if a.reference_timing else tuple(float(x) for x in a.election_timeout.split(","))
+    cfg = NodeConfig(node_id=a.node_id, port=a.port, peers=parse_peers(a.peers), data_root=a.data_root,
+                     storage=a.storage, llm_address=a.llm or None,
+                     raft=RaftConfig(election_timeout=(lo, hi), heartbeat_interval=a.heartbeat,
+                                     local_commit=a.local_commit),
+                     token_mode=a.token_mode, bcrypt_rounds=a.bcrypt_rounds, fsync=a.fsync)
+    print(f"\n{'=' * 60}\n  Raft Chat Node {a.node_id}\n  Port: {a.port}\n"
+          f"  Features: Consensus + Full Chat Application + on-GPU AI\n{'=' * 60}\n", flush=True)
+    serve(cfg)
+
+
+if __name__ == "__main__":
+    main()
