@@ -1,0 +1,101 @@
+"""LLM service entry point: ``python -m drtc_amd.llm.server``.
+
+Replaces the reference's Gemini proxy (llm_server/llm_server.py:476-523) with
+on-node inference:
+
+  --backend engine   (default) random-init model on the local MI355X GPUs;
+                     ``--gpus N`` runs N data-parallel engine replicas, one
+                     process per GPU, behind a least-outstanding router;
+                     ``--tp N`` runs one tensor-parallel engine over N GPUs
+                     (RCCL all-reduce over xGMI), e.g. Llama-3-70B TP=8;
+  --backend scripted deterministic format-correct text (no model; CPU tests).
+
+Port 50055 and the thread-pool server match the reference.
+"""
+from __future__ import annotations
+
+import argparse
+import logging
+import signal
+import threading
+from concurrent import futures
+
+import grpc
+
+from ..protos import LLM_SERVICE, add_servicer
+from ..utils.logging_utils import setup_logging
+from .backends import ScriptedBackend
+from .service import FeatureParams, LLMServicer
+
+log = logging.getLogger("drtc_amd.llm.server")
+
+
+def build_backend(args):
+    if args.backend == "scripted":
+        return ScriptedBackend()
+    from ..engine import ChatTokenizer
+    from ..models import get_config
+
+    cfg = get_config(args.model)
+    tok = ChatTokenizer(cfg.vocab_size, cfg.bos_token_id, cfg.eos_token_id)
+    engine_kw = dict(max_batch=args.max_batch, max_model_len=args.max_model_len,
+                     use_graphs=not args.no_graphs)
+    if args.tp > 1:
+        from ..parallel.tp_engine import TPEngineGroup
+
+        return TPEngineGroup(args.model, args.tp, engine_kw, tok)
+    n = args.gpus
+    if n <= 1:
+        import torch
+
+        from ..engine.engine import LLMEngine
+        from ..models import TransformerLM
+        from .backends import EngineBackend
+
+        dev = "cuda:0" if torch.cuda.is_available() else "cpu"
+        model = TransformerLM(cfg, dev, seed=1234, full_then_shard=False)
+        eng = LLMEngine(model, **engine_kw)
+        eng.warmup(capture=True)
+        return EngineBackend(eng, tok)
+    from .backends import ReplicaRouter, WorkerPool
+
+    pool = WorkerPool(args.model, [f"cuda:{i}" for i in range(n)], engine_kw)
+    return ReplicaRouter(pool, tok, args.max_model_len)
+
+
+def serve(backend, port: int = 50055, workers: int = 64, bind: str = "[::]", params=None):
+    server = grpc.server(futures.ThreadPoolExecutor(max_workers=workers))
+    add_servicer(server, LLM_SERVICE, LLMServicer(backend, params))
+    if server.add_insecure_port(f"{bind}:{port}") == 0:
+        raise RuntimeError(f"cannot bind port {port}")
+    server.start()
+    return server
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(description="drtc_amd LLM service (on-GPU inference)")
+    ap.add_argument("--port", type=int, default=50055)
+    ap.add_argument("--backend", choices=("engine", "scripted"), default="engine")
+    ap.add_argument("--model", default="llama-3-8b")
+    ap.add_argument("--gpus", type=int, default=1, help="data-parallel replicas (1 process/GPU)")
+    ap.add_argument("--tp", type=int, default=1, help="tensor-parallel degree")
+    ap.add_argument("--max-batch", type=int, default=256)
+    ap.add_argument("--max-model-len", type=int, default=4096)
+    ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--workers", type=int, default=64)
+    ap.add_argument("--log-level", default="INFO")
+    args = ap.parse_args(argv)
+    setup_logging(args.log_level)
+    backend = build_backend(args)
+    server = serve(backend, args.port, args.workers)
+    log.info("LLM server on port %d (backend=%s model=%s gpus=%d tp=%d)", args.port, args.backend,
+             args.model, args.gpus, args.tp)
+    stop = threading.Event()
+    signal.signal(signal.SIGINT, lambda *a: stop.set())
+    signal.signal(signal.SIGTERM, lambda *a: stop.set())
+    stop.wait()
+    server.stop(1.0)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,98 @@
+"""``llm.LLMService``: all four RPCs (the reference registers only two:
+survey quirk Q15) over a text backend (on-GPU engine, DP router, scripted).
+
+Each handler: build the feature's prompt (llm/prompts.py), generate with the
+feature's sampling settings, parse into the response contract; any backend
+failure yields the same fallback responses as the reference service
+(llm_server/llm_server.py:45-145).  Handlers run concurrently on the gRPC
+thread pool and meet in the engine's continuous batch.
+"""
+from __future__ import annotations
+
+import logging
+import time
+
+from ..engine.request import SamplingParams
+from ..protos import llm_pb
+from ..utils.metrics import METRICS
+from . import prompts as P
+
+log = logging.getLogger(__name__)
+
+
+class FeatureParams:
+    """Sampling per feature.  Ask-AI uses the reference's explicit settings
+    (temperature 0.7, 150 tokens: llm_server.py:168-172); the other three
+    used the hosted SDK defaults (temperature 1.0, top-k 64, top-p 0.95)
+    with output budgets sized to their format contracts."""
+
+    def __init__(self, ignore_eos: bool = False):
+        sdk = dict(temperature=1.0, top_k=64, top_p=0.95, ignore_eos=ignore_eos)
+        self.answer = SamplingParams(max_new_tokens=150, temperature=0.7, top_k=64, top_p=0.95,
+                                     ignore_eos=ignore_eos)
+        self.smart = SamplingParams(max_new_tokens=48, **sdk)
+        self.summary = SamplingParams(max_new_tokens=128, **sdk)
+        self.suggest = SamplingParams(max_new_tokens=96, **sdk)
+
+
+class LLMServicer:
+    def __init__(self, backend, params: FeatureParams | None = None, timeout: float = 60.0):
+        self.backend = backend
+        self.p = params or FeatureParams()
+        self.timeout = timeout
+
+    def _gen(self, feature: str, prompt: str, params: SamplingParams) -> str:
+        t0 = time.perf_counter()
+        text = self.backend.generate([prompt], [params], timeout=self.timeout)[0]
+        METRICS.observe(f"llm.{feature}.latency_s", time.perf_counter() - t0)
+        METRICS.inc(f"llm.{feature}.requests")
+        return text
+
+    def GetLLMAnswer(self, request, context):
+        try:
+            text = self._gen("answer", P.answer_prompt(request.query, list(request.context)), self.p.answer)
+            return llm_pb.LLMResponse(request_id=request.request_id, answer=P.parse_answer(text),
+                                      confidence=0.95)
+        except Exception as e:
+            log.error("LLM answer failed: %s", e)
+            return llm_pb.LLMResponse(request_id=request.request_id, answer=P.ANSWER_ERROR, confidence=0.0)
+
+    def GetSmartReply(self, request, context):
+        msgs = list(request.recent_messages)
+        if not msgs:
+            return llm_pb.SmartReplyResponse(request_id=request.request_id, suggestions=P.SMART_REPLY_EMPTY)
+        try:
+            text = self._gen("smart_reply", P.smart_reply_prompt(msgs), self.p.smart)
+            return llm_pb.SmartReplyResponse(request_id=request.request_id,
+                                             suggestions=P.parse_smart_replies(text))
+        except Exception as e:
+            log.error("smart reply failed: %s", e)
+            return llm_pb.SmartReplyResponse(request_id=request.request_id,
+                                             suggestions=P.SMART_REPLY_FALLBACK)
+
+    def SummarizeConversation(self, request, context):
+        msgs = list(request.messages)
+        max_len = request.max_length if request.max_length > 0 else 200
+        if not msgs:
+            return llm_pb.SummarizeResponse(request_id=request.request_id,
+                                            summary="No messages to summarize", key_points=[])
+        try:
+            text = self._gen("summarize", P.summarize_prompt(msgs, max_len), self.p.summary)
+            summary, points = P.parse_summary(text, msgs, max_len)
+            return llm_pb.SummarizeResponse(request_id=request.request_id, summary=summary,
+                                            key_points=points)
+        except Exception as e:
+            log.error("summarize failed: %s", e)
+            return llm_pb.SummarizeResponse(request_id=request.request_id, summary=P.SUMMARY_ERROR,
+                                            key_points=[])
+
+    def GetContextSuggestions(self, request, context):
+        msgs = list(request.context)
+        try:
+            text = self._gen("suggest", P.suggestions_prompt(msgs, request.current_input), self.p.suggest)
+            s, t = P.parse_suggestions(text, request.current_input)
+            return llm_pb.SuggestionsResponse(request_id=request.request_id, suggestions=s, topics=t)
+        except Exception as e:
+            log.error("suggestions failed: %s", e)
+            return llm_pb.SuggestionsResponse(request_id=request.request_id,
+                                              suggestions=P.SUGGEST_ERROR, topics=[])

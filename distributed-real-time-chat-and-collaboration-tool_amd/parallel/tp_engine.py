@@ -1,0 +1,151 @@
+"""Tensor-parallel serving: N lockstep engine replicas (one process per GPU).
+
+SPMD design: every TP rank runs the *same* deterministic scheduler on the
+*same* request stream, so ranks agree on every batch without exchanging
+plans - only newly arrived requests are broadcast (a few bytes, over a gloo
+CPU group) at each step boundary.  Inside a step the model's collectives
+(all-reduce after o_proj/down_proj, all-gather of vocab-parallel logits) run
+on RCCL over xGMI and are captured in the decode hipGraphs.  Logits are
+bitwise identical on every rank after the all-gather and the fused sampler
+is a pure function of (logits, seed, step), so every rank samples the same
+tokens.  Rank 0 reports results to the front-end.
+"""
+from __future__ import annotations
+
+import itertools
+import multiprocessing as mp
+import os
+import queue
+import socket
+import threading
+import time
+
+from ..engine.request import Request, SamplingParams
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def tp_worker(rank: int, world: int, port: int, model_name: str, engine_kw: dict, inq, outq):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    import torch
+    import torch.distributed as dist
+
+    from ..engine.engine import LLMEngine
+    from ..models import TransformerLM, get_config
+    from .comm import ParallelContext, init_distributed
+
+    try:
+        init_distributed()
+        cpu = dist.new_group(backend="gloo")
+        dev = torch.device("cuda", rank) if torch.cuda.is_available() else torch.device("cpu")
+        pc = ParallelContext.from_world(tp=True)
+        cfg = get_config(model_name)
+        model = TransformerLM(cfg, dev, pc=pc, seed=1234)
+        eng = LLMEngine(model, seed=0, **engine_kw)
+        eng.warmup(capture=True)
+        if rank == 0:
+            outq.put(("ready", 0, None))
+    except BaseException as e:
+        if rank == 0:
+            outq.put(("fatal", 0, repr(e)))
+        raise
+    while True:
+        new = []
+        if rank == 0:
+            block = not eng.has_work()
+            try:
+                new.append(inq.get(timeout=0.05) if block else inq.get_nowait())
+                while True:
+                    new.append(inq.get_nowait())
+            except queue.Empty:
+                pass
+        box = [new]
+        dist.broadcast_object_list(box, src=0, group=cpu)
+        new = box[0]
+        stop = any(m is None for m in new)
+        for m in new:
+            if m is not None:
+                rid, ids, prm = m
+                eng.add_request(Request(ids, prm, request_id=rid))
+        if stop:
+            break
+        if eng.has_work():
+            done = eng.step()
+            if rank == 0:
+                for r in done:
+                    outq.put(("done", r.request_id, (r.output_ids, r.finish_reason)))
+    dist.barrier(group=cpu)
+    dist.destroy_process_group()
+
+
+class TPEngineGroup:
+    """Front-end handle: generate() on a TP group of ``world`` GPUs."""
+
+    def __init__(self, model_name: str, world: int, engine_kw: dict, tokenizer,
+                 start_timeout: float = 1800):
+        ctx = mp.get_context("spawn")
+        self.inq, self.outq = ctx.Queue(), ctx.Queue()
+        port = _free_port()
+        self.procs = [ctx.Process(target=tp_worker, daemon=True,
+                                  args=(r, world, port, model_name, engine_kw,
+                                        self.inq if r == 0 else None, self.outq if r == 0 else None))
+                      for r in range(world)]
+        for p in self.procs:
+            p.start()
+        kind, _, info = self.outq.get(timeout=start_timeout)
+        if kind != "ready":
+            raise RuntimeError(f"TP engine failed to start: {info}")
+        self.tok = tokenizer
+        self.max_model_len = engine_kw.get("max_model_len", 4096)
+        self._futs: dict[str, tuple] = {}
+        self._lock = threading.Lock()
+        self._ids = itertools.count()
+        threading.Thread(target=self._collect, daemon=True).start()
+
+    def _collect(self):
+        while True:
+            kind, rid, payload = self.outq.get()
+            with self._lock:
+                f = self._futs.pop(rid, None)
+            if f is not None:
+                f[1].append(payload)
+                f[0].set()
+
+    def generate(self, prompts, params, timeout=None):
+        if isinstance(params, SamplingParams):
+            params = [params] * len(prompts)
+        hs = []
+        for p, prm in zip(prompts, params):
+            ids = self.tok.encode(p)
+            limit = self.max_model_len - prm.max_new_tokens - 1
+            if len(ids) > limit:
+                ids = ids[:1] + ids[len(ids) - limit + 1:]
+            rid = f"tp-{next(self._ids)}"
+            ev, slot = threading.Event(), []
+            with self._lock:
+                self._futs[rid] = (ev, slot)
+            self.inq.put((rid, ids, prm))
+            hs.append((ev, slot))
+        deadline = None if timeout is None else time.monotonic() + timeout
+        out = []
+        for ev, slot in hs:
+            left = None if deadline is None else max(0.0, deadline - time.monotonic())
+            if not ev.wait(left):
+                raise TimeoutError("generation timed out")
+            ids, reason = slot[0]
+            if reason.startswith("error"):
+                raise RuntimeError(reason)
+            out.append(self.tok.decode(ids))
+        return out
+
+    def close(self):
+        self.inq.put(None)
+        for p in self.procs:
+            p.join(timeout=30)

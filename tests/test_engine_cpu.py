@@ -1,0 +1,139 @@
+"""Engine, model and op references on CPU (tiny configs)."""
+import math
+
+import pytest
+import torch
+
+from drtc_amd import ops
+from drtc_amd.engine import ChatTokenizer, LLMEngine, SamplingParams
+from drtc_amd.engine.block_allocator import BlockAllocator, PyBlockAllocator
+from drtc_amd.models import (GEMMA_2B, LLAMA3_8B, LLAMA3_70B, MIXTRAL_8X7B, TINY_GEMMA, TINY_LLAMA,
+                             TINY_MIXTRAL, TransformerLM)
+
+
+@pytest.mark.parametrize("cfg", [TINY_LLAMA, TINY_GEMMA, TINY_MIXTRAL], ids=lambda c: c.name)
+def test_engine_greedy_matches_full_forward(cfg):
+    m = TransformerLM(cfg, "cpu", seed=3)
+    eng = LLMEngine(m, max_batch=8, max_model_len=256, num_blocks=64, use_graphs=False)
+    prompts = [[1, 5, 9], [1, 5, 9, 13, 22, 40, 41, 42], list(range(1, 70)), [7] * 33]
+    reqs = eng.generate(prompts, SamplingParams.greedy(6, ignore_eos=True))
+    for p, r in zip(prompts, reqs):
+        ref = m.forward_reference([p + r.output_ids[:-1]])[0].float()
+        got = ref[len(p) - 1:]
+        for j, tok in enumerate(r.output_ids):
+            assert got[j, tok] >= got[j].max() - 1e-3 * max(1.0, got[j].abs().max().item())
+    assert eng.alloc.num_used == 0
+
+
+def test_engine_preemption_and_recompute():
+    m = TransformerLM(TINY_LLAMA, "cpu", seed=3)
+    eng = LLMEngine(m, max_batch=8, max_model_len=512, num_blocks=12, use_graphs=False)
+    reqs = eng.generate([list(range(1, 50))] * 6, SamplingParams(max_new_tokens=40, temperature=0.8,
+                                                                 top_k=20, top_p=0.9, ignore_eos=True))
+    assert all(len(r.output_ids) == 40 for r in reqs)
+    assert eng.stats["preemptions"] > 0 and eng.alloc.num_used == 0
+
+
+def test_engine_stop_conditions():
+    m = TransformerLM(TINY_LLAMA, "cpu", seed=4)
+    eng = LLMEngine(m, max_batch=4, max_model_len=64, num_blocks=32, use_graphs=False)
+    r = eng.generate([list(range(1, 60))], SamplingParams.greedy(100, ignore_eos=True))[0]
+    assert r.finish_reason == "length" and r.num_tokens == 64
+    first = eng.generate([[1, 2, 3]], SamplingParams.greedy(1, ignore_eos=True))[0].output_ids[0]
+    r = eng.generate([[1, 2, 3]], SamplingParams(max_new_tokens=10, temperature=0.0, top_k=0, top_p=1.0,
+                                                 stop_token_ids=(first,)))[0]
+    assert r.finish_reason == "stop" and r.output_ids == [first]
+    with pytest.raises(ValueError):
+        eng.add_request(__import__("drtc_amd.engine", fromlist=["Request"]).Request([1] * 100))
+
+
+def test_tp2_matches_tp1_logits():
+    """TP sharding math (head/column split + reductions) on one process by
+    summing the shards' partial outputs by hand."""
+    from drtc_amd.parallel.comm import ParallelContext
+
+    cfg = TINY_LLAMA
+    full = TransformerLM(cfg, "cpu", seed=9)
+
+    class FakeTP(ParallelContext):
+        pass
+
+    shards = [TransformerLM(cfg, "cpu", pc=FakeTP(tp_size=2, tp_rank=r), seed=9) for r in range(2)]
+    H = cfg.hidden_size
+    x = torch.randn(5, H).to(torch.bfloat16)
+    L0 = full.layers[0]
+    y_full = torch.nn.functional.linear(ops.act_glu(torch.nn.functional.linear(x, L0["gate_up"])), L0["down"])
+    y_tp = sum(torch.nn.functional.linear(ops.act_glu(torch.nn.functional.linear(x, s.layers[0]["gate_up"])),
+                                          s.layers[0]["down"]).float() for s in shards)
+    assert (y_full.float() - y_tp).abs().max() < 0.02
+    q_full = torch.nn.functional.linear(x, L0["qkv"])
+    q_cat = torch.cat([torch.nn.functional.linear(x, s.layers[0]["qkv"])[:, :s.sh.hq * cfg.head_dim]
+                       for s in shards], -1)
+    assert torch.equal(q_full[:, :cfg.num_heads * cfg.head_dim], q_cat)
+
+
+def test_block_allocators_agree():
+    for cls in (PyBlockAllocator, BlockAllocator):
+        a = cls(10, 1)
+        b = a.allocate(4)
+        assert a.num_free == 5 and len(set(b)) == 4 and 0 not in b
+        a.incref(b[:1])
+        a.free(b)
+        assert a.num_free == 8 and a.refcount(b[0]) == 1
+        a.free(b[:1])
+        assert a.num_free == 9
+        with pytest.raises(Exception):
+            a.free(b[:1])
+        with pytest.raises(Exception):
+            a.allocate(10)
+
+
+def test_reference_ops_consistency():
+    """The paged-decode reference equals the last row of the prefill
+    reference when the KV cache holds the same sequence."""
+    torch.manual_seed(0)
+    Hq, Hkv, D, n = 4, 2, 64, 45
+    qkv = torch.randn(n, (Hq + 2 * Hkv) * D).to(torch.bfloat16)
+    pre = ops.prefill_attention_ref(qkv, [0, n], Hq, Hkv, D, D ** -0.5)
+    bs = ops.KV_BLOCK
+    nb = math.ceil(n / bs)
+    kc = torch.zeros(nb + 1, Hkv, bs, D, dtype=torch.bfloat16)
+    vc = torch.zeros(nb + 1, Hkv, D, bs, dtype=torch.bfloat16)
+    slots = torch.arange(n) + bs  # blocks 1..nb
+    cs = ops.build_rope_cache(64, D, 1e4)
+    pos = torch.zeros(n, dtype=torch.int32)  # identity rotation
+    ops.rope_kv_ref(qkv.clone(), pos, slots, cs, Hq, Hkv, D, kc, vc, bs)
+    q = qkv[-1:, :Hq * D].reshape(1, Hq, D)
+    bt = torch.arange(1, nb + 1, dtype=torch.int32)[None]
+    dec = ops.paged_decode_ref(q, kc, vc, bt, torch.tensor([n], dtype=torch.int32), D ** -0.5)
+    assert (dec.reshape(1, -1).float() - pre[-1:].float()).abs().max() < 0.02
+
+
+def test_rope_llama3_scaling_and_sampler_ref():
+    t = ops.build_rope_cache(16, 128, 5e5, {"rope_type": "llama3", "factor": 8.0, "low_freq_factor": 1.0,
+                                           "high_freq_factor": 4.0, "original_max_position_embeddings": 8192})
+    assert t.shape == (16, 128) and torch.allclose(t[0, :64], torch.ones(64))
+    logits = torch.randn(4, 50).to(torch.bfloat16)
+    assert torch.equal(ops.sample_ref(logits).long(), logits.float().argmax(-1))
+    out = ops.sample_ref(logits, torch.ones(4), torch.full((4,), 3, dtype=torch.int32), torch.ones(4))
+    top3 = logits.float().topk(3, -1).indices
+    assert (top3 == out.long()[:, None]).any(-1).all()
+
+
+def test_model_configs_param_counts():
+    assert abs(LLAMA3_8B.num_params() / 1e9 - 8.03) < 0.05
+    assert abs(LLAMA3_70B.num_params() / 1e9 - 70.6) < 0.3
+    assert abs(GEMMA_2B.num_params() / 1e9 - 2.51) < 0.05
+    assert abs(MIXTRAL_8X7B.num_params() / 1e9 - 46.7) < 0.3
+    assert LLAMA3_8B.kv_bytes_per_token() == 131072
+
+
+def test_tokenizer_roundtrip_and_density():
+    tok = ChatTokenizer(128256, 128000, 128001)
+    for text in ["Hello team, lunch tomorrow?", "naïve café — ünïcode ✓", "line1\nline2\n\n- bullet"]:
+        ids = tok.encode(text)
+        assert ids[0] == 128000 and tok.decode(ids) == text
+        assert all(0 <= i < 128256 for i in ids)
+    words = "should we review the project plan tomorrow after the meeting".split()
+    assert len(tok.encode(" ".join(words), add_bos=False)) == len(words)
+    assert len(tok.id_to_tok) == 128256

@@ -1,0 +1,210 @@
+"""LLM service contract (prompts/parsers, engine backend over gRPC, TP over
+gloo) and the legacy single-node chat.ChatService with streaming."""
+import os
+import sys
+import threading
+import time
+
+import grpc
+import pytest
+
+from drtc_amd.engine import ChatTokenizer, LLMEngine
+from drtc_amd.llm import prompts as P
+from drtc_amd.llm.backends import EngineBackend, ScriptedBackend
+from drtc_amd.llm.server import serve as serve_llm
+from drtc_amd.models import TINY_LLAMA, TransformerLM
+from drtc_amd.protos import CHAT_SERVICE, LLM_SERVICE, chat_pb, llm_pb, make_stub
+from drtc_amd.server.legacy import serve as serve_legacy
+from drtc_amd.utils.cluster import free_port
+
+M = P.ChatLine
+
+
+def test_prompt_templates():
+    msgs = [M("alice", f"m{i}") for i in range(8)]
+    p = P.smart_reply_prompt(msgs)
+    assert p.startswith("Based on this conversation:\nalice: m3\n") and "alice: m7\n\nGenerate exactly 3" in p
+    assert "alice: m2" not in p
+    s = P.summarize_prompt(msgs, 200)
+    assert s.startswith("Summarize this conversation concisely in under 200 characters:\n\nalice: m0")
+    assert P.answer_prompt("q?", []) == "q?\n\nProvide a short, helpful answer in 2 sentences or less."
+    a = P.answer_prompt("q?", [f"c{i}" for i in range(7)])
+    assert "c1" not in a and "c2\nc3" in a and "User's question: q?" in a
+    assert 'User started typing: "hel"' in P.suggestions_prompt(msgs, "hel")
+    assert "No previous context" in P.suggestions_prompt([], "")
+
+
+def test_parsers():
+    assert P.parse_smart_replies("1. Sure thing\n- Sounds good\n* OK!\nextra") == ["Sure thing", "Sounds good", "OK!"]
+    assert P.parse_smart_replies("only one") == ["only one", "I agree", "Interesting point"]
+    msgs = [M("a", "x"), M("b", "y")]
+    s, k = P.parse_summary("Summary: hello\nworld\n\nKey Points:\n- one\n• two\n- three\n- four", msgs, 200)
+    assert s == "hello world" and k == ["one", "two", "three"]
+    s, k = P.parse_summary("Summary: " + "z" * 300, msgs, 200)
+    assert len(s) == 200 and s.endswith("...") and k[0] == "2 messages exchanged"
+    s, k = P.parse_summary("no structure", msgs, 200)
+    assert s == "no structure"
+    sug, top = P.parse_suggestions("COMPLETIONS:\n- a\n- b\nTOPICS:\n- t1", "")
+    assert sug == ["a", "b"] and top == ["t1"]
+    sug, top = P.parse_suggestions("garbage", "I think")
+    assert sug[0] == "I think be the best option" and top == ["current discussion", "related ideas"]
+
+
+def _llm_stub(port):
+    return make_stub(grpc.insecure_channel(f"127.0.0.1:{port}"), LLM_SERVICE)
+
+
+def test_llm_service_all_four_rpcs_with_engine_backend():
+    m = TransformerLM(TINY_LLAMA, "cpu", seed=1)
+    eng = LLMEngine(m, max_batch=8, max_model_len=1024, num_blocks=256, use_graphs=False)
+    backend = EngineBackend(eng, ChatTokenizer(TINY_LLAMA.vocab_size))
+    from drtc_amd.llm.service import FeatureParams
+
+    fp = FeatureParams(ignore_eos=True)
+    for f in (fp.answer, fp.smart, fp.summary, fp.suggest):
+        f.max_new_tokens = 6
+    port = free_port()
+    srv = serve_llm(backend, port=port, bind="127.0.0.1", params=fp)
+    try:
+        s = _llm_stub(port)
+        msgs = [llm_pb.Message(sender="alice", content="lunch at noon?"),
+                llm_pb.Message(sender="bob", content="sure")]
+        r = s.GetSmartReply(llm_pb.SmartReplyRequest(request_id="r1", recent_messages=msgs), timeout=60)
+        assert r.request_id == "r1" and len(r.suggestions) == 3
+        r = s.SummarizeConversation(llm_pb.SummarizeRequest(request_id="r2", messages=msgs, max_length=50),
+                                    timeout=60)
+        assert len(r.summary) <= 50 and 1 <= len(r.key_points) <= 3
+        r = s.GetContextSuggestions(llm_pb.ContextRequest(request_id="r3", context=msgs, current_input="ok"),
+                                    timeout=60)
+        assert 1 <= len(r.suggestions) <= 5 and 1 <= len(r.topics) <= 3
+        r = s.GetLLMAnswer(llm_pb.LLMRequest(request_id="r4", query="why?"), timeout=60)
+        assert r.request_id == "r4" and r.confidence == pytest.approx(0.95)
+        # concurrent requests share the continuous batch
+        out = []
+        ths = [threading.Thread(target=lambda: out.append(s.GetSmartReply(
+            llm_pb.SmartReplyRequest(recent_messages=msgs), timeout=60))) for _ in range(6)]
+        [t.start() for t in ths]
+        [t.join() for t in ths]
+        assert len(out) == 6 and eng.stats["decode_steps"] > 0
+        e = s.GetSmartReply(llm_pb.SmartReplyRequest(recent_messages=[]), timeout=10)
+        assert list(e.suggestions) == P.SMART_REPLY_EMPTY
+    finally:
+        srv.stop(0)
+        backend.close()
+
+
+def test_llm_service_fallbacks_on_backend_error():
+    class Boom:
+        def generate(self, *a, **k):
+            raise RuntimeError("gpu on fire")
+
+    port = free_port()
+    srv = serve_llm(Boom(), port=port, bind="127.0.0.1")
+    try:
+        s = _llm_stub(port)
+        msgs = [llm_pb.Message(sender="a", content="x")]
+        assert list(s.GetSmartReply(llm_pb.SmartReplyRequest(recent_messages=msgs)).suggestions) == P.SMART_REPLY_FALLBACK
+        assert s.SummarizeConversation(llm_pb.SummarizeRequest(messages=msgs)).summary == P.SUMMARY_ERROR
+        assert s.GetLLMAnswer(llm_pb.LLMRequest(query="q")).confidence == 0.0
+        assert list(s.GetContextSuggestions(llm_pb.ContextRequest(context=msgs)).suggestions) == P.SUGGEST_ERROR
+    finally:
+        srv.stop(0)
+
+
+@pytest.mark.slow
+def test_tp2_engine_group_over_gloo():
+    """Two lockstep TP ranks (gloo, CPU) produce the same greedy text as TP=1."""
+    code = r"""
+import sys
+sys.path.insert(0, %r)
+from drtc_amd.parallel.tp_engine import TPEngineGroup
+from drtc_amd.engine import ChatTokenizer, SamplingParams, LLMEngine
+from drtc_amd.models import TINY_LLAMA, TransformerLM
+if __name__ == '__main__':
+    tok = ChatTokenizer(TINY_LLAMA.vocab_size)
+    kw = dict(max_batch=8, max_model_len=512, num_blocks=64, use_graphs=False)
+    g = TPEngineGroup('tiny-llama', 2, kw, tok)
+    a = g.generate(['hello world', 'lunch tomorrow?'], SamplingParams.greedy(8, ignore_eos=True), timeout=120)
+    g.close()
+    eng = LLMEngine(TransformerLM(TINY_LLAMA, 'cpu', seed=1234), seed=0, **kw)
+    b = [tok.decode(r.output_ids) for r in eng.generate([tok.encode('hello world'), tok.encode('lunch tomorrow?')],
+                                                        SamplingParams.greedy(8, ignore_eos=True))]
+    assert a == b, (a, b)
+    print('TP-OK')
+""" % os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    import subprocess
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300, env=env)
+    assert "TP-OK" in r.stdout, r.stderr[-2000:]
+
+
+def test_legacy_chat_service(tmp_path):
+    port = free_port()
+    srv, server = serve_legacy(port, str(tmp_path / "server_data"), block=False, bcrypt_rounds=4)
+    try:
+        s = make_stub(grpc.insecure_channel(f"127.0.0.1:{port}"), CHAT_SERVICE)
+        r = s.Signup(chat_pb.SignupRequest(username="x", password="pw", email="bad"))
+        assert r.code == 400 and "3-20" in r.message
+        r = s.Signup(chat_pb.SignupRequest(username="dave", password="nodigits", email="d@x.io"))
+        assert "number or special" in r.message
+        assert s.Signup(chat_pb.SignupRequest(username="dave", password="pw1234", email="d@x.io")).code == 201
+        ta = s.Login(chat_pb.LoginRequest(username="admin", password="admin123")).token
+        td = s.Login(chat_pb.LoginRequest(username="dave", password="pw1234")).token
+        chans = {c.name: c.channel_id for c in s.GetChannels(chat_pb.GetChannelsRequest(token=ta)).channels}
+        assert set(chans) == {"general", "random", "development"}
+        events = []
+        stream = s.StreamMessages(chat_pb.StreamRequest(token=td))
+
+        def consume():
+            try:
+                for ev in stream:
+                    events.append(ev)
+            except grpc.RpcError:
+                pass
+
+        th = threading.Thread(target=consume, daemon=True)
+        th.start()
+        time.sleep(0.3)
+        assert s.PostMessage(chat_pb.PostRequest(token=ta, channel_id=chans["general"], content="hi all",
+                                                 type="text")).success
+        assert s.SendDirectMessage(chat_pb.DirectMessageRequest(token=ta, recipient_username="dave",
+                                                                content="psst")).success
+        t_end = time.time() + 5
+        while len(events) < 2 and time.time() < t_end:
+            time.sleep(0.05)
+        stream.cancel()
+        assert [e.event_type for e in events[:2]] == ["message", "dm"]
+        assert events[0].message.content == "hi all" and events[1].direct_message.content == "psst"
+        for k in range(5):
+            s.PostMessage(chat_pb.PostRequest(token=ta, channel_id=chans["general"], content=str(k)))
+        page = s.GetMessages(chat_pb.GetRequest(token=ta, channel_id=chans["general"], limit=2, offset=1))
+        assert [m.content for m in page.messages] == ["0", "1"] and page.next_cursor == "3"
+        cid_r = s.CreateChannel(chat_pb.CreateChannelRequest(token=td, channel_name="ops"))
+        assert cid_r.success
+        ops_id = next(c.channel_id for c in s.GetChannels(chat_pb.GetChannelsRequest(token=td)).channels
+                      if c.name == "ops")
+        r = s.ManageChannel(chat_pb.ManageChannelRequest(token=td, channel_id=ops_id, action="add_user",
+                                                         parameters={"username": "user1"}))
+        assert r.success
+        assert not s.ManageChannel(chat_pb.ManageChannelRequest(token=ta, channel_id=ops_id,
+                                                                action="add_user")).success
+        # the reference's UNIMPLEMENTED four
+        assert s.UpdatePresence(chat_pb.UpdatePresenceRequest(token=td, status="away")).success
+        assert s.LeaveChannel(chat_pb.LeaveChannelRequest(token=ta, channel_id=chans["general"])).success
+        info = s.GetServerInfo(chat_pb.ServerInfoRequest())
+        assert info.is_leader and info.node_id == 1
+        uid = next(u.user_id for u in s.GetOnlineUsers(chat_pb.GetOnlineUsersRequest(token=ta)).users
+                   if u.username == "user2")
+        assert s.ManageUser(chat_pb.ManageUserRequest(token=ta, target_user_id=uid, action="disable")).success
+        assert not s.Login(chat_pb.LoginRequest(username="user2", password="user123")).success
+        up = s.UploadFile(chat_pb.FileUploadRequest(token=ta, channel_id=chans["general"], file_name="f.bin",
+                                                    file_data=b"\x00\x01"))
+        assert s.DownloadFile(chat_pb.FileDownloadRequest(token=ta, file_id=up.file_id)).file_data == b"\x00\x01"
+        conv = s.ListConversations(chat_pb.ListConversationsRequest(token=td)).conversations
+        assert conv[0].username == "admin" and conv[0].last_message.content == "psst"
+    finally:
+        server.stop(0)
+    # persistence in the reference layout
+    from drtc_amd.utils.pickle_compat import safe_load
+    d = safe_load(str(tmp_path / "server_data" / "users.pkl"))
+    assert {"users", "users_by_email", "users_by_id"} <= set(d) and "dave" in d["users"]

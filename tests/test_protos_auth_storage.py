@@ -1,0 +1,201 @@
+"""Wire contract, auth and on-disk compatibility with the reference."""
+import ast
+import ctypes
+import ctypes.util
+import datetime as dt
+import os
+import pickle
+import re
+
+import pytest
+from google.protobuf import descriptor_pb2
+
+from drtc_amd.protos import chat_pb, file_descriptor_protos, llm_pb, raft_pb
+from drtc_amd.raft.core import Entry
+from drtc_amd.raft.state_machine import ChatState
+from drtc_amd.raft.storage import NativeStorage, PickleStorage
+from drtc_amd.utils import auth, pickle_compat
+
+REF = "/root/reference"
+have_ref = pytest.mark.skipif(not os.path.isdir(REF), reason="reference checkout not mounted")
+
+
+def _ref_fdp(name):
+    src = open(f"{REF}/generated/{name}_pb2.py").read()
+    m = re.search(r"AddSerializedFile\((b'.*?')\)", src, re.S)
+    return descriptor_pb2.FileDescriptorProto.FromString(ast.literal_eval(m.group(1)))
+
+
+def _norm(fd):
+    msgs = {}
+    for m in fd.message_type:
+        msgs[m.name] = sorted((f.name, f.number, f.type, f.label, f.type_name) for f in m.field)
+        for n in m.nested_type:
+            msgs[m.name + "." + n.name] = sorted((f.name, f.number, f.type, f.label, f.type_name)
+                                                 for f in n.field)
+    svc = {s.name: [(x.name, x.input_type, x.output_type, x.server_streaming) for x in s.method]
+           for s in fd.service}
+    return fd.package, msgs, svc
+
+
+@have_ref
+@pytest.mark.parametrize("name", ["raft_node", "llm_service", "chat_service", "chat_client"])
+def test_descriptors_match_reference(name):
+    mine = file_descriptor_protos()[name + ".proto"]
+    assert _norm(mine) == _norm(_ref_fdp(name))
+
+
+def test_wire_roundtrip():
+    e = raft_pb.AppendEntriesRequest(term=3, leader_id=2, prev_log_index=-1, prev_log_term=0,
+                                     entries=[raft_pb.LogEntry(term=3, command="SEND_MESSAGE", data=b'{"a": 1}')],
+                                     leader_commit=-1)
+    b = e.SerializeToString()
+    assert raft_pb.AppendEntriesRequest.FromString(b) == e
+    r = llm_pb.LLMRequest(request_id="x", query="q", context=["a", "b"], parameters={"k": "v"})
+    assert llm_pb.LLMRequest.FromString(r.SerializeToString()).parameters["k"] == "v"
+    u = chat_pb.UserInfo(username="a")
+    u.last_seen.FromDatetime(dt.datetime(2025, 1, 1))
+    assert chat_pb.UserInfo.FromString(u.SerializeToString()).last_seen.seconds == 1735689600
+
+
+def test_jwt_pyjwt_byte_format():
+    exp = dt.datetime(2030, 1, 1, tzinfo=dt.timezone.utc)
+    tok = auth.jwt_encode({"user_id": "alice", "username": "alice", "exp": exp}, "raft-chat-secret-key")
+    h, p, s = tok.split(".")
+    assert h == "eyJhbGciOiJIUzI1NiIsInR5cCI6IkpXVCJ9"  # {"alg":"HS256","typ":"JWT"}
+    import base64
+    import json
+    body = base64.urlsafe_b64decode(p + "=" * (-len(p) % 4))
+    assert body == b'{"user_id":"alice","username":"alice","exp":1893456000}'
+    assert "=" not in tok
+    assert auth.jwt_decode(tok, "raft-chat-secret-key")["username"] == "alice"
+    with pytest.raises(auth.InvalidTokenError):
+        auth.jwt_decode(tok, "other-secret")
+    with pytest.raises(auth.InvalidTokenError):
+        auth.jwt_decode(tok[:-2] + "xx", "raft-chat-secret-key")
+    old = auth.jwt_encode({"username": "a", "exp": 1000}, "k")
+    with pytest.raises(auth.ExpiredSignatureError):
+        auth.jwt_decode(old, "k")
+
+
+def test_bcrypt_matches_libxcrypt():
+    lib = ctypes.util.find_library("crypt")
+    if not lib:
+        pytest.skip("libcrypt not available")
+    c = ctypes.CDLL(lib)
+    c.crypt.restype = ctypes.c_char_p
+    for pw in (b"alice123", b"", b"p\xc3\xa4ss", b"x" * 72, b"y" * 90):
+        salt = auth.bcrypt_gensalt(4)
+        assert auth.bcrypt_hashpw(pw, salt) == c.crypt(pw, salt)
+        assert auth.bcrypt_checkpw(pw, auth.bcrypt_hashpw(pw, salt))
+
+
+@have_ref
+def test_bcrypt_verifies_reference_hashes():
+    users = pickle_compat.safe_load(f"{REF}/server/server_data/users.pkl")["users"]
+    assert auth.bcrypt_checkpw(b"admin123", users["admin"]["password"])
+    assert auth.bcrypt_checkpw(b"user123", users["user1"]["password"])
+    assert not auth.bcrypt_checkpw(b"nope", users["user2"]["password"])
+
+
+def test_safe_unpickler_rejects_code():
+    class Evil:
+        def __reduce__(self):
+            return (os.system, ("true",))
+
+    with pytest.raises(pickle.UnpicklingError):
+        pickle_compat.safe_loads(pickle.dumps(Evil()))
+    ok = {"a": {1, 2}, "t": dt.datetime(2024, 1, 1, tzinfo=dt.timezone.utc), "b": b"x"}
+    assert pickle_compat.safe_loads(pickle.dumps(ok, protocol=4)) == ok
+
+
+@have_ref
+def test_state_loads_legacy_reference_pickles(tmp_path):
+    import shutil
+    shutil.copy(f"{REF}/server/server_data/users.pkl", tmp_path / "users.pkl")
+    shutil.copy(f"{REF}/server/server_data/channels.pkl", tmp_path / "channels.pkl")
+    st = ChatState()
+    st.load(str(tmp_path))
+    assert "admin" in st.users and isinstance(st.users["admin"]["password"], bytes)
+    assert {c["name"] for c in st.channels.values()} == {"general", "random", "development"}
+    assert all(isinstance(c["members"], set) for c in st.channels.values())
+
+
+def _apply_all(st):
+    st.apply("CREATE_USER", {"user_id": "u1", "username": "dave", "password": "$2b$04$abc",
+                             "email": "d@x.com", "display_name": "Dave", "is_admin": False})
+    st.apply("CREATE_CHANNEL", {"channel_id": "c1", "name": "proj", "description": "d", "is_private": True,
+                                "members": ["u1"], "admins": ["u1"]})
+    st.apply("JOIN_CHANNEL", {"channel_id": "c1", "user_id": "alice"})
+    st.apply("LEAVE_CHANNEL", {"channel_id": "c1", "user_id": "alice"})
+    m = {"id": "m1", "sender_id": "u1", "sender_name": "dave", "channel_id": "c1", "content": "hi",
+         "timestamp": 1}
+    st.apply("SEND_MESSAGE", m)
+    st.apply("SEND_MESSAGE", dict(m))  # duplicate id ignored
+    d = {"id": "d1", "sender_id": "u1", "sender_name": "dave", "recipient_id": "alice",
+         "recipient_name": "alice", "content": "yo", "timestamp": 2, "is_read": False}
+    st.apply("SEND_DM", d)
+    st.apply("SEND_DM", dict(d))
+    st.apply("UPLOAD_FILE", {"file_id": "f1", "name": "a.txt", "data": b"abc".hex(), "size": 3,
+                             "mime_type": "text/plain", "uploader_id": "u1", "uploader_name": "dave",
+                             "channel_id": "c1", "recipient": None, "description": ""})
+    st.apply("JOIN_CHANNEL", {"channel_id": "nope", "user_id": "u1"})  # Q13: dropped
+
+
+def test_state_machine_semantics_and_pickle_roundtrip(tmp_path):
+    st = ChatState()
+    _apply_all(st)
+    assert st.users["dave"]["password"] == b"$2b$04$abc"
+    assert st.channels["c1"]["members"] == {"u1"}
+    assert len(st.channel_messages["c1"]) == 1 and len(st.direct_messages) == 1
+    assert st.files["f1"]["data"] == b"abc"
+    assert st.conversation("alice", "dave")[0]["content"] == "yo"
+    st.save_all(str(tmp_path))
+    raw = open(tmp_path / "channels.pkl", "rb").read()
+    assert raw[:2] == b"\x80\x04"  # pickle protocol 4
+    ch = pickle_compat.safe_load(str(tmp_path / "channels.pkl"))
+    assert isinstance(ch["c1"]["members"], list) and isinstance(ch["c1"]["created_at"], str)
+    st2 = ChatState()
+    st2.load(str(tmp_path))
+    assert st2.channels["c1"]["members"] == {"u1"}
+    assert st2.users == st.users and st2.channel_messages == st.channel_messages
+    assert st2.conversation("dave", "alice") == st.conversation("dave", "alice")
+
+
+def test_native_log_store_recovery(tmp_path):
+    from drtc_amd import _native
+    p = str(tmp_path / "log.seg")
+    s = _native.LogStore(p, False)
+    for i in range(10):
+        s.append(i // 3, f"C{i}", bytes([i]) * i)
+    s.truncate_from(7)
+    s.close()
+    with open(p, "ab") as f:  # torn tail of a crashed append
+        f.write(b"TFAR\x10\x00\x00\x00garbage")
+    s2 = _native.LogStore(p, False)
+    assert s2.size() == 7
+    assert s2.get(6) == (2, "C6", b"\x06" * 6)
+    assert s2.term_at(3) == 1
+    s2.append(5, "X", b"y")
+    assert s2.size() == 8
+
+
+def test_storage_formats_and_migration(tmp_path):
+    d = str(tmp_path / "raft_node_1_data")
+    ps = PickleStorage(d, 50051)
+    ps.load()
+    ps.append([Entry(1, "SEND_MESSAGE", b"{}"), Entry(1, "SEND_DM", b"{}")])
+    ps.save_state({"current_term": 1, "voted_for": 2, "commit_index": 1, "last_applied": 1})
+    log = pickle_compat.safe_load(os.path.join(d, "raft_log_port_50051.pkl"))
+    assert log == [{"term": 1, "command": "SEND_MESSAGE", "data": b"{}"},
+                   {"term": 1, "command": "SEND_DM", "data": b"{}"}]
+    st = pickle_compat.safe_load(os.path.join(d, "raft_state_port_50051.pkl"))
+    assert st == {"current_term": 1, "voted_for": 2, "commit_index": 1, "last_applied": 1}
+    # a native store opened on the reference-format dir imports the log
+    ns = NativeStorage(d, 50051)
+    state, entries = ns.load()
+    assert [e.command for e in entries] == ["SEND_MESSAGE", "SEND_DM"] and state["voted_for"] == 2
+    ns.append([Entry(2, "NOOP", b"")])
+    ns.export()
+    assert len(pickle_compat.safe_load(os.path.join(d, "raft_log_port_50051.pkl"))) == 3
+    ns.close()
