@@ -53,7 +53,7 @@ def main() -> None:
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--model", default="llama-3-8b")
-    ap.add_argument("--batch", type=int, default=256, help="smart-reply requests per GPU per step")
+    ap.add_argument("--batch", type=int, default=512, help="smart-reply requests per GPU per step")
     ap.add_argument("--max-new-tokens", type=int, default=48)
     ap.add_argument("--history", type=int, default=5)
     ap.add_argument("--greedy", action="store_true")

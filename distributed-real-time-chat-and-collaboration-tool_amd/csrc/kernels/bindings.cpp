@@ -31,11 +31,18 @@ PYBIND11_MODULE(_hipk, m) {
   });
   m.def("rope_kv", [](u64 qkv, int T, int qkv_stride, u64 positions, u64 slots,
                       u64 cos_sin, int Hq, int Hkv, int D, u64 k_cache,
-                      u64 v_cache, int block_size, u64 st) {
+                      u64 v_cache, int block_size, int write_v, u64 st) {
     return drtc::launch_rope_kv(P<void>(qkv), T, qkv_stride, P<const int>(positions),
                                 P<const int64_t>(slots), P<const float>(cos_sin), Hq,
                                 Hkv, D, P<void>(k_cache), P<void>(v_cache),
-                                block_size, S(st));
+                                block_size, write_v, S(st));
+  });
+  m.def("kv_write_v", [](u64 v_cache, u64 qkv, int qkv_stride, u64 seg_tok, u64 seg_len,
+                         u64 seg_blk, int nseg, int Hq, int Hkv, int D, int block_size,
+                         u64 st) {
+    return drtc::launch_kv_write_v(P<void>(v_cache), P<const void>(qkv), qkv_stride,
+                                   P<const int>(seg_tok), P<const int>(seg_len),
+                                   P<const int>(seg_blk), nseg, Hq, Hkv, D, block_size, S(st));
   });
   m.def("paged_decode",
         [](u64 out, u64 part_o, u64 part_ml, u64 q, int q_stride, u64 k_cache,

@@ -17,8 +17,12 @@ int launch_act_glu(void* out, const void* gu, int64_t T, int I, int gu_stride,
 
 int launch_rope_kv(void* qkv, int T, int qkv_stride, const int* positions,
                    const int64_t* slots, const float* cos_sin, int Hq, int Hkv,
-                   int D, void* k_cache, void* v_cache, int block_size,
+                   int D, void* k_cache, void* v_cache, int block_size, int write_v,
                    hipStream_t st);
+
+int launch_kv_write_v(void* v_cache, const void* qkv, int qkv_stride, const int* seg_tok,
+                      const int* seg_len, const int* seg_blk, int nseg, int Hq, int Hkv,
+                      int D, int block_size, hipStream_t st);
 
 int launch_paged_decode(void* out, float* part_o, float* part_ml, const void* q,
                         int q_stride, const void* k_cache, const void* v_cache,

@@ -173,7 +173,7 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(
     bf16_t* __restrict__ qkv, int qkv_stride, const int* __restrict__ positions,
     const int64_t* __restrict__ slots, const float* __restrict__ cos_sin,
     int Hq, int Hkv, bf16_t* __restrict__ k_cache,
-    bf16_t* __restrict__ v_cache, int block_size) {
+    bf16_t* __restrict__ v_cache, int block_size, int write_v) {
   constexpr int HV = D / 16;  // 8-wide vectors per half-head
   const int t = blockIdx.x;
   const int pos = positions[t];
@@ -210,7 +210,7 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(
       store_bf16x8(kd + D / 2, o2);
     }
   }
-  if (slot < 0) return;
+  if (slot < 0 || !write_v) return;
   const int n_v = Hkv * (D / 8);
   for (int item = threadIdx.x; item < n_v; item += 256) {
     const int h = item / (D / 8);
@@ -224,19 +224,78 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(
 
 int launch_rope_kv(void* qkv, int T, int qkv_stride, const int* positions,
                    const int64_t* slots, const float* cos_sin, int Hq, int Hkv,
-                   int D, void* k_cache, void* v_cache, int block_size,
+                   int D, void* k_cache, void* v_cache, int block_size, int write_v,
                    hipStream_t st) {
   if (T == 0) return 0;
   dim3 grid(T), block(256);
   switch (D) {
     case 64:
-      hipLaunchKernelGGL(rope_kv_kernel<64>, grid, block, 0, st, (bf16_t*)qkv, qkv_stride, positions, slots, cos_sin, Hq, Hkv, (bf16_t*)k_cache, (bf16_t*)v_cache, block_size);
+      hipLaunchKernelGGL(rope_kv_kernel<64>, grid, block, 0, st, (bf16_t*)qkv, qkv_stride, positions, slots, cos_sin, Hq, Hkv, (bf16_t*)k_cache, (bf16_t*)v_cache, block_size, write_v);
       break;
     case 128:
-      hipLaunchKernelGGL(rope_kv_kernel<128>, grid, block, 0, st, (bf16_t*)qkv, qkv_stride, positions, slots, cos_sin, Hq, Hkv, (bf16_t*)k_cache, (bf16_t*)v_cache, block_size);
+      hipLaunchKernelGGL(rope_kv_kernel<128>, grid, block, 0, st, (bf16_t*)qkv, qkv_stride, positions, slots, cos_sin, Hq, Hkv, (bf16_t*)k_cache, (bf16_t*)v_cache, block_size, write_v);
       break;
     case 256:
-      hipLaunchKernelGGL(rope_kv_kernel<256>, grid, block, 0, st, (bf16_t*)qkv, qkv_stride, positions, slots, cos_sin, Hq, Hkv, (bf16_t*)k_cache, (bf16_t*)v_cache, block_size);
+      hipLaunchKernelGGL(rope_kv_kernel<256>, grid, block, 0, st, (bf16_t*)qkv, qkv_stride, positions, slots, cos_sin, Hq, Hkv, (bf16_t*)k_cache, (bf16_t*)v_cache, block_size, write_v);
+      break;
+    default:
+      return -1;
+  }
+  return (int)hipGetLastError();
+}
+
+// ------------------------------------------- prefill V write (transposed)
+// The decode kernel wants V dim-major inside each 32-token cache block.  A
+// per-token kernel would emit D scattered 2-byte stores per head; in prefill
+// a whole block's tokens are contiguous rows of the QKV buffer, so one
+// workgroup per (block segment, kv head) stages the [32][D] tile in LDS and
+// writes the [D][32] block with 16-byte stores (rows of 8 tokens).
+template <int D>
+__global__ __launch_bounds__(256) void kv_write_v_kernel(
+    bf16_t* __restrict__ v_cache, const bf16_t* __restrict__ qkv, int qkv_stride,
+    const int* __restrict__ seg_tok, const int* __restrict__ seg_len,
+    const int* __restrict__ seg_blk, int Hq, int Hkv) {
+  constexpr int BS = 32;
+  constexpr int ROW = D + 2;  // padded LDS row (elements)
+  __shared__ bf16_t tile[BS * ROW];
+  const int seg = blockIdx.x, h = blockIdx.y;
+  const int t0 = seg_tok[seg], n = seg_len[seg];
+  const int64_t blk = seg_blk[seg];
+  const int voff = (Hq + Hkv + h) * D;
+  for (int v = threadIdx.x; v < BS * (D / 8); v += 256) {
+    const int t = v / (D / 8), c = (v - t * (D / 8)) * 8;
+    bf16x8 x;
+    if (t < n) x = load_bf16x8(qkv + (int64_t)(t0 + t) * qkv_stride + voff + c);
+    else for (int j = 0; j < 8; ++j) x[j] = f2bf(0.f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) tile[t * ROW + c + j] = x[j];
+  }
+  __syncthreads();
+  bf16_t* dst = v_cache + (blk * Hkv + h) * (int64_t)D * BS;
+  for (int v = threadIdx.x; v < D * (BS / 8); v += 256) {
+    const int d = v / (BS / 8), g = (v - d * (BS / 8)) * 8;
+    bf16x8 y;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) y[j] = tile[(g + j) * ROW + d];
+    store_bf16x8(dst + d * BS + g, y);
+  }
+}
+
+int launch_kv_write_v(void* v_cache, const void* qkv, int qkv_stride, const int* seg_tok,
+                      const int* seg_len, const int* seg_blk, int nseg, int Hq, int Hkv,
+                      int D, int block_size, hipStream_t st) {
+  if (nseg == 0) return 0;
+  if (block_size != 32) return -1;
+  dim3 grid(nseg, Hkv), block(256);
+  switch (D) {
+    case 64:
+      hipLaunchKernelGGL(kv_write_v_kernel<64>, grid, block, 0, st, (bf16_t*)v_cache, (const bf16_t*)qkv, qkv_stride, seg_tok, seg_len, seg_blk, Hq, Hkv);
+      break;
+    case 128:
+      hipLaunchKernelGGL(kv_write_v_kernel<128>, grid, block, 0, st, (bf16_t*)v_cache, (const bf16_t*)qkv, qkv_stride, seg_tok, seg_len, seg_blk, Hq, Hkv);
+      break;
+    case 256:
+      hipLaunchKernelGGL(kv_write_v_kernel<256>, grid, block, 0, st, (bf16_t*)v_cache, (const bf16_t*)qkv, qkv_stride, seg_tok, seg_len, seg_blk, Hq, Hkv);
       break;
     default:
       return -1;

@@ -202,25 +202,34 @@ class LLMEngine:
         pos = np.zeros(Tp, dtype=np.int32)
         pos[:T] = np.concatenate([np.arange(n, dtype=np.int32) for n in lens])
         slots = np.full(Tp, -1, dtype=np.int64)
+        seg_tok, seg_len, seg_blk = [], [], []
         for r, a, n in zip(batch, cu[:-1], lens):
             blk = np.asarray(r.blocks, dtype=np.int64)
             p = np.arange(n)
             slots[a:a + n] = blk[p // BS] * BS + p % BS
+            nb = -(-n // BS)
+            seg_tok.append(a + BS * np.arange(nb))
+            seg_len.append(np.minimum(BS, n - BS * np.arange(nb)))
+            seg_blk.append(blk[:nb])
+        seg_tok = np.concatenate(seg_tok).astype(np.int32)
+        seg_len = np.concatenate(seg_len).astype(np.int32)
+        seg_blk = np.concatenate(seg_blk).astype(np.int32)
         last_idx = np.asarray(cu[1:], dtype=np.int64) - 1
         ts, tq = ops.prefill_tiles(cu)
         t_i32 = torch.from_numpy(np.concatenate([ids, pos, np.asarray(cu, np.int32),
-                                                 np.asarray(ts, np.int32),
-                                                 np.asarray(tq, np.int32)])).to(dev, non_blocking=True)
+                                                 np.asarray(ts, np.int32), np.asarray(tq, np.int32),
+                                                 seg_tok, seg_len, seg_blk])).to(dev, non_blocking=True)
         t_i64 = torch.from_numpy(np.concatenate([slots, last_idx])).to(dev, non_blocking=True)
-        nseq, nt = len(batch), len(ts)
+        nseq, nt, ns = len(batch), len(ts), len(seg_tok)
         o = 0
         d_ids = t_i32[o:o + Tp]; o += Tp
         d_pos = t_i32[o:o + Tp]; o += Tp
         d_cu = t_i32[o:o + nseq + 1]; o += nseq + 1
         d_ts = t_i32[o:o + nt]; o += nt
-        d_tq = t_i32[o:o + nt]
+        d_tq = t_i32[o:o + nt]; o += nt
+        d_segs = (t_i32[o:o + ns], t_i32[o + ns:o + 2 * ns], t_i32[o + 2 * ns:o + 3 * ns])
         meta = PrefillMeta(positions=d_pos, slots=t_i64[:Tp], cu_seqlens=d_cu, cu_host=cu,
-                           tiles=(d_ts, d_tq), last_idx=t_i64[Tp:])
+                           tiles=(d_ts, d_tq), last_idx=t_i64[Tp:], v_segs=d_segs)
         logits = self.model.forward_prefill(d_ids, meta, self.kv)
         temp = torch.tensor([r.params.temperature for r in batch], dtype=torch.float32, device=dev)
         topk = torch.tensor([r.params.top_k for r in batch], dtype=torch.int32, device=dev)

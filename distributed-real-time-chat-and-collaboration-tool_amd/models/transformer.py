@@ -37,6 +37,7 @@ class PrefillMeta:
     cu_host: list
     tiles: tuple | None          # (tile_seq, tile_q0) int32 device tensors
     last_idx: torch.Tensor       # int64 [n] index of each sequence's last token
+    v_segs: tuple | None = None  # (tok, len, block) int32: block-wise V write
 
 
 @dataclass
@@ -208,12 +209,29 @@ class TransformerLM:
         return self.pc.all_reduce_tp(y)
 
     def _moe(self, L: dict, x: torch.Tensor) -> torch.Tensor:
-        """Top-k routed experts (Mixtral: softmax over the top-2 logits)."""
+        """Top-k routed experts (Mixtral: softmax over the top-2 logits).
+
+        Eager (prefill): tokens are gathered per expert (sparse, exact FLOPs).
+        Under hipGraph capture (decode) shapes must be static, so every local
+        expert runs on the whole (small) batch and its output is weighted by
+        the dense routing matrix (zero for unrouted tokens) - same result,
+        no host synchronisation."""
         cfg, sh = self.cfg, self.sh
         logits = F.linear(x, L["router"]).float()
         topv, topi = logits.topk(cfg.experts_per_token, dim=-1)
         wts = torch.softmax(topv, dim=-1)
         out = torch.zeros(x.shape[0], x.shape[1], dtype=torch.float32, device=x.device)
+        if x.is_cuda and torch.cuda.is_current_stream_capturing():
+            dense = torch.zeros(x.shape[0], cfg.num_experts, dtype=torch.float32, device=x.device)
+            dense.scatter_(1, topi, wts)
+            for le in range(sh.n_local_experts):
+                e = sh.expert_offset + le
+                h = ops.act_glu(F.linear(x, L["gate_up"][le]), cfg.act)
+                out.add_(F.linear(h, L["down"][le]).float() * dense[:, e:e + 1])
+            out = out.to(x.dtype)
+            if self.pc.ep_size > 1:
+                return self.pc.all_reduce_ep(out)
+            return self.pc.all_reduce_tp(out)
         for le in range(sh.n_local_experts):
             e = sh.expert_offset + le
             tok, slot = torch.nonzero(topi == e, as_tuple=True)
@@ -253,8 +271,12 @@ class TransformerLM:
         def attn(i, L, x):
             qkv = F.linear(x, L["qkv"])
             kc, vc = kv_caches[i] if kv_caches is not None else (None, None)
+            blockwise_v = kc is not None and meta.v_segs is not None
             ops.rope_kv_(qkv, meta.positions, meta.slots if kc is not None else None,
-                         self.cos_sin, sh.hq, sh.hkv, D, kc, vc, ops.KV_BLOCK)
+                         self.cos_sin, sh.hq, sh.hkv, D, kc, vc, ops.KV_BLOCK,
+                         write_v=not blockwise_v)
+            if blockwise_v:
+                ops.kv_write_v(vc, qkv, meta.v_segs, sh.hq, sh.hkv, D)
             a = ops.prefill_attention(qkv, meta.cu_seqlens, sh.hq, sh.hkv, D, cfg.attn_scale,
                                       True, tiles=meta.tiles, cu_host=meta.cu_host)
             return self.pc.all_reduce_tp(F.linear(a, L["o"]))

@@ -11,7 +11,7 @@ from .activation import act_glu, act_glu_ref
 from .attention import (KV_BLOCK, DecodeWorkspace, decode_partitioning, paged_decode_attention,
                         paged_decode_ref, prefill_attention, prefill_attention_ref, prefill_tiles)
 from .norm import rmsnorm, rmsnorm_ref
-from .rope import build_rope_cache, rope_kv_, rope_kv_ref
+from .rope import build_rope_cache, kv_write_v, kv_write_v_ref, rope_kv_, rope_kv_ref
 from .sampling import sample, sample_ref
 
 __all__ = [
@@ -19,5 +19,6 @@ __all__ = [
     "act_glu", "act_glu_ref", "KV_BLOCK", "DecodeWorkspace", "decode_partitioning",
     "paged_decode_attention", "paged_decode_ref", "prefill_attention", "prefill_attention_ref",
     "prefill_tiles", "rmsnorm", "rmsnorm_ref", "build_rope_cache", "rope_kv_", "rope_kv_ref",
+    "kv_write_v", "kv_write_v_ref",
     "sample", "sample_ref",
 ]

@@ -59,18 +59,46 @@ def rope_kv_ref(qkv, positions, slots, cos_sin, Hq, Hkv, D, k_cache, v_cache, bl
         k = new[:, Hq:][valid]
         v = qkv[:, nh * D:(nh + Hkv) * D].reshape(T, Hkv, D)[valid]
         k_cache[blk, :, off, :] = k
-        v_cache[blk, :, :, off] = v
+        if v_cache is not None:
+            v_cache[blk, :, :, off] = v
     return qkv
+
+
+def kv_write_v_ref(v_cache, qkv, seg_tok, seg_len, seg_blk, Hq, Hkv, D):
+    bs = v_cache.shape[-1]
+    for t0, n, b in zip(seg_tok.tolist(), seg_len.tolist(), seg_blk.tolist()):
+        v = qkv[t0:t0 + n, (Hq + Hkv) * D:(Hq + 2 * Hkv) * D].reshape(n, Hkv, D)
+        blk = torch.zeros(Hkv, D, bs, dtype=v_cache.dtype, device=v_cache.device)
+        blk[:, :, :n] = v.permute(1, 2, 0)
+        v_cache[b] = blk
+
+
+def kv_write_v(v_cache: torch.Tensor, qkv: torch.Tensor, segs, Hq: int, Hkv: int, D: int) -> None:
+    """Prefill V write: ``segs`` = (tok_start, n_tokens, block) int32 tensors,
+    one entry per 32-token cache block of the packed prompt batch."""
+    seg_tok, seg_len, seg_blk = segs
+    if not on_gpu(qkv):
+        kv_write_v_ref(v_cache, qkv, seg_tok, seg_len, seg_blk, Hq, Hkv, D)
+        return
+    nb, hkv, d, bs = v_cache.shape
+    assert hkv == Hkv and d == D and v_cache.is_contiguous() and qkv.stride(1) == 1
+    for t in segs:
+        assert t.dtype == torch.int32 and t.is_cuda and t.numel() == seg_tok.numel()
+    check(hipk().kv_write_v(v_cache.data_ptr(), qkv.data_ptr(), qkv.stride(0), seg_tok.data_ptr(),
+                            seg_len.data_ptr(), seg_blk.data_ptr(), seg_tok.numel(), Hq, Hkv, D, bs,
+                            stream_ptr(qkv)), "kv_write_v")
 
 
 def rope_kv_(qkv: torch.Tensor, positions: torch.Tensor, slots: torch.Tensor | None,
              cos_sin: torch.Tensor, Hq: int, Hkv: int, D: int,
              k_cache: torch.Tensor | None, v_cache: torch.Tensor | None,
-             block_size: int) -> torch.Tensor:
-    """Rotate q/k heads of ``qkv`` [T, (Hq+2Hkv)*D] in place; write k/v of
-    tokens with ``slots[t] >= 0`` into the paged cache."""
+             block_size: int, write_v: bool = True) -> torch.Tensor:
+    """Rotate q/k heads of ``qkv`` [T, (Hq+2Hkv)*D] in place; write k (and v,
+    unless ``write_v`` is False) of tokens with ``slots[t] >= 0`` into the
+    paged cache."""
     if not on_gpu(qkv):
-        return rope_kv_ref(qkv, positions, slots, cos_sin, Hq, Hkv, D, k_cache, v_cache, block_size)
+        return rope_kv_ref(qkv, positions, slots, cos_sin, Hq, Hkv, D, k_cache,
+                           v_cache if write_v else None, block_size)
     T = qkv.shape[0]
     assert qkv.dtype == torch.bfloat16 and qkv.stride(1) == 1
     assert qkv.shape[1] >= (Hq + 2 * Hkv) * D
@@ -83,5 +111,5 @@ def rope_kv_(qkv: torch.Tensor, positions: torch.Tensor, slots: torch.Tensor | N
         assert v_cache.shape[1:] == (Hkv, D, block_size) and v_cache.is_contiguous()
     check(hipk().rope_kv(qkv.data_ptr(), T, qkv.stride(0), positions.data_ptr(), ptr(slots),
                          cos_sin.data_ptr(), Hq, Hkv, D, ptr(k_cache), ptr(v_cache),
-                         block_size, stream_ptr(qkv)), "rope_kv")
+                         block_size, int(write_v), stream_ptr(qkv)), "rope_kv")
     return qkv

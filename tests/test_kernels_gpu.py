@@ -68,6 +68,29 @@ def test_rope_kv(hipk, D, Hq, Hkv):
     assert torch.equal(vc, vc2)
 
 
+@pytest.mark.parametrize("D,Hq,Hkv", [(128, 32, 8), (256, 8, 1), (64, 4, 2)])
+def test_kv_write_v_blockwise(hipk, D, Hq, Hkv):
+    torch.manual_seed(5)
+    lens = [70, 32, 1, 33]
+    T = sum(lens)
+    qkv = torch.randn(T, (Hq + 2 * Hkv) * D, device=DEV).to(torch.bfloat16)
+    nb = 12
+    vc = torch.randn(nb, Hkv, D, ops.KV_BLOCK, device=DEV).to(torch.bfloat16)
+    vc2 = vc.clone()
+    tok, ln, blk, a, b = [], [], [], 0, 1
+    for n in lens:
+        for j in range(0, n, 32):
+            tok.append(a + j)
+            ln.append(min(32, n - j))
+            blk.append(b)
+            b += 1
+        a += n
+    segs = tuple(torch.tensor(x, dtype=torch.int32, device=DEV) for x in (tok, ln, blk))
+    ops.kv_write_v(vc, qkv, segs, Hq, Hkv, D)
+    ops.kv_write_v_ref(vc2, qkv, *segs, Hq, Hkv, D)
+    assert torch.equal(vc, vc2)
+
+
 def _paged_setup(B, Hq, Hkv, D, ctx_lens, nb_total=None, seed=0):
     g = torch.Generator(device="cpu").manual_seed(seed)
     bs = ops.KV_BLOCK

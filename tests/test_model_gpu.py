@@ -10,7 +10,11 @@ from drtc_amd.models import TINY_GEMMA, TINY_LLAMA, TINY_MIXTRAL, TransformerLM
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("cfg", [TINY_LLAMA, TINY_GEMMA, TINY_MIXTRAL], ids=lambda c: c.name)
+@pytest.mark.parametrize("cfg", [TINY_LLAMA, TINY_GEMMA,
+                                 # all experts active: no routing discontinuity between
+                                 # the bf16 HIP path and the fp32 reference path
+                                 TINY_MIXTRAL.replace(experts_per_token=TINY_MIXTRAL.num_experts)],
+                         ids=lambda c: c.name)
 def test_prefill_logits_match_reference(hipk, cfg):
     m = TransformerLM(cfg, "cuda", seed=5)
     seqs = [list(range(3, 60)), [7, 8, 9], list(range(100, 300))]
@@ -22,7 +26,7 @@ def test_prefill_logits_match_reference(hipk, cfg):
         assert err < 0.05 * max(1.0, b.float().abs().max().item()), err
 
 
-@pytest.mark.parametrize("cfg", [TINY_LLAMA, TINY_GEMMA], ids=lambda c: c.name)
+@pytest.mark.parametrize("cfg", [TINY_LLAMA, TINY_GEMMA, TINY_MIXTRAL], ids=lambda c: c.name)
 def test_engine_decode_matches_reference(hipk, cfg):
     """Greedy decode through paged KV + graphs agrees with a full-sequence
     forward on every generated position (logit-level, bf16 tolerance)."""
