@@ -34,12 +34,23 @@ import torch.distributed as dist
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 from drtc_amd.engine import ChatTokenizer, LLMEngine, Request, SamplingParams  # noqa: E402
-from drtc_amd.llm.prompts import smart_reply_prompt  # noqa: E402
+from drtc_amd.llm import prompts as P  # noqa: E402
+from drtc_amd.llm.service import FeatureParams  # noqa: E402
 from drtc_amd.models import TransformerLM, get_config  # noqa: E402
 from drtc_amd.parallel import init_distributed  # noqa: E402
-from drtc_amd.utils.synthetic import smart_reply_workload  # noqa: E402
+from drtc_amd.utils.synthetic import channel_history  # noqa: E402
 
 METRIC = "smart-reply tokens/sec (whole node) + p50 suggestion latency, Llama-3-8B TP=1"
+
+# workload -> (history messages per request, prompt builder, FeatureParams attribute)
+WORKLOADS = {
+    "smart_reply": (5, lambda h, rng: P.smart_reply_prompt(h), "smart"),
+    "summarize": (20, lambda h, rng: P.summarize_prompt(h, 200), "summary"),
+    "suggest": (5, lambda h, rng: P.suggestions_prompt(h, rng.choice(["I think", "maybe we", "sure"])),
+                "suggest"),
+    "ask": (5, lambda h, rng: P.answer_prompt(rng.choice(h).content + "?", [m.content for m in h]),
+            "answer"),
+}
 
 
 def log(rank: int, *a) -> None:
@@ -53,12 +64,15 @@ def main() -> None:
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--model", default="llama-3-8b")
-    ap.add_argument("--batch", type=int, default=512, help="smart-reply requests per GPU per step")
-    ap.add_argument("--max-new-tokens", type=int, default=48)
-    ap.add_argument("--history", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=1024, help="requests per GPU per step")
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="smart_reply")
+    ap.add_argument("--max-new-tokens", type=int, default=None,
+                    help="default: the feature's output budget (smart reply 48)")
+    ap.add_argument("--history", type=int, default=None)
     ap.add_argument("--greedy", action="store_true")
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--max-model-len", type=int, default=2048)
+    ap.add_argument("--tp", type=int, default=1, help="tensor-parallel degree (= WORLD_SIZE)")
     args = ap.parse_args()
 
     rank, world = init_distributed()
@@ -73,10 +87,18 @@ def main() -> None:
 
     cfg = get_config(args.model)
     t0 = time.perf_counter()
-    model = TransformerLM(cfg, device, seed=1234, full_then_shard=False)
+    tp = args.tp
+    if tp > 1:
+        assert tp == world, "--tp must equal WORLD_SIZE (one TP group per node)"
+        from drtc_amd.parallel import ParallelContext
+        pc = ParallelContext.from_world(tp=True, ep=cfg.is_moe)
+    else:
+        pc = None
+    dp_rank = 0 if tp > 1 else rank
+    model = TransformerLM(cfg, device, pc=pc, seed=1234, full_then_shard=False)
     eng = LLMEngine(model, max_batch=args.batch, max_model_len=args.max_model_len,
                     max_prefill_tokens=max(16384, args.batch * 400),
-                    use_graphs=not args.no_graphs, seed=rank)
+                    use_graphs=not args.no_graphs, seed=dp_rank)
     eng.warmup(capture=True)
     if device.type == "cuda":
         torch.cuda.synchronize()
@@ -84,13 +106,19 @@ def main() -> None:
               f"({eng.kv.capacity_tokens} tokens), init {time.perf_counter() - t0:.1f}s")
 
     tok = ChatTokenizer(cfg.vocab_size, cfg.bos_token_id, cfg.eos_token_id)
-    params = (SamplingParams.greedy(args.max_new_tokens, ignore_eos=True) if args.greedy else
-              SamplingParams(max_new_tokens=args.max_new_tokens, temperature=1.0, top_k=64,
-                             top_p=0.95, ignore_eos=True))
+    n_hist, build, feat = WORKLOADS[args.workload]
+    n_hist = args.history or n_hist
+    params = getattr(FeatureParams(ignore_eos=True), feat)
+    if args.max_new_tokens:
+        params.max_new_tokens = args.max_new_tokens
+    if args.greedy:
+        params = SamplingParams.greedy(params.max_new_tokens, ignore_eos=True)
+    args.max_new_tokens = params.max_new_tokens
 
     def make_prompts(step: int) -> list[list[int]]:
-        hist = smart_reply_workload(args.batch, seed=rank * 100003 + step, history=args.history)
-        return [tok.encode(smart_reply_prompt(h)) for h in hist]
+        import random
+        rng = random.Random(dp_rank * 100003 + step)
+        return [tok.encode(build(channel_history(rng, n_hist), rng)) for _ in range(args.batch)]
 
     def serve(prompts):
         reqs = [eng.add_request(Request(p, params)) for p in prompts]
@@ -128,11 +156,13 @@ def main() -> None:
         sm = stats.clone()
         dist.all_reduce(sm, op=dist.ReduceOp.SUM)
         elapsed, p50 = float(mx[0]), float(mx[3])
-        gen, prompt_tokens = float(sm[1]), float(sm[2])
+        if tp == 1:  # DP replicas serve different requests; TP ranks serve the same ones
+            gen, prompt_tokens = float(sm[1]), float(sm[2])
     tps = gen / elapsed
     if rank == 0:
         out = {
-            "metric": METRIC,
+            "metric": METRIC if (args.workload, args.model) == ("smart_reply", "llama-3-8b") else
+            f"{args.workload} tokens/sec (whole node) + p50 latency, {cfg.name} TP={tp}",
             "value": round(tps, 1),
             "unit": "tokens/s",
             "n_gpus": world,
@@ -140,15 +170,17 @@ def main() -> None:
             "warmup": args.warmup,
             "ms_per_step": round(1000 * elapsed / args.steps, 2),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if tp > 1 else "weak",
             "vs_baseline": None,
             "dtype": "bf16",
-            "data": "synthetic chat logs (5-message smart-reply contexts), random-init weights",
-            "config": {"model": cfg.name, "global_batch": args.batch * world,
-                       "seq_len": args.max_new_tokens, "parallelism": f"dp{world}",
+            "data": f"synthetic chat logs ({n_hist}-message {args.workload} contexts), random-init weights",
+            "config": {"model": cfg.name, "global_batch": args.batch * (world // tp),
+                       "seq_len": args.max_new_tokens,
+                       "parallelism": f"tp{tp}" if tp > 1 else f"dp{world}",
                        "max_new_tokens": args.max_new_tokens,
-                       "avg_prompt_tokens": round(prompt_tokens / (args.batch * world * args.steps), 1),
-                       "sampling": "greedy" if args.greedy else "t=1.0,top_k=64,top_p=0.95",
+                       "avg_prompt_tokens": round(prompt_tokens / (args.batch * (world // tp) * args.steps), 1),
+                       "sampling": "greedy" if args.greedy else
+                       f"t={params.temperature},top_k={params.top_k},top_p={params.top_p}",
                        "graphs": not args.no_graphs},
             "p50_latency_ms": round(1000 * p50, 1),
             "total_tokens_per_s": round((gen + prompt_tokens) / elapsed, 1),

@@ -197,7 +197,9 @@ class TransformerLM:
     def _embed(self, ids: torch.Tensor) -> torch.Tensor:
         h = F.embedding(ids, self.embed)
         if self.cfg.embed_scale:
-            h = h * torch.tensor(math.sqrt(self.cfg.hidden_size), dtype=h.dtype, device=h.device)
+            # Gemma: x * sqrt(H) with the normaliser rounded to the activation
+            # dtype; a python scalar keeps the op graph-capturable (no H2D copy)
+            h = h * float(torch.tensor(math.sqrt(self.cfg.hidden_size), dtype=h.dtype))
         return h
 
     def _mlp(self, L: dict, x: torch.Tensor) -> torch.Tensor:

@@ -1,0 +1,83 @@
+"""Multi-process parallelism on CPU (gloo): EP all-to-all dispatch/combine and
+TP forward equivalence with world_size 2 (the same code runs on RCCL)."""
+import os
+import socket
+import sys
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _ep_worker(rank, world, port, q):
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from drtc_amd.parallel.expert_parallel import ep_moe_forward, moe_reference
+
+    g = torch.Generator().manual_seed(0)
+    E, H, I, k = 4, 64, 32, 2
+    router = (torch.randn(E, H, generator=g) * 0.3).to(torch.bfloat16)
+    gu = (torch.randn(E, 2 * I, H, generator=g) * 0.1).to(torch.bfloat16)
+    dn = (torch.randn(E, H, I, generator=g) * 0.1).to(torch.bfloat16)
+    x_all = torch.randn(world * 13, H, generator=g).to(torch.bfloat16)
+    x = x_all[rank * 13:(rank + 1) * 13]
+    el = E // world
+    y = ep_moe_forward(x, router, gu[rank * el:(rank + 1) * el], dn[rank * el:(rank + 1) * el], k)
+    ref = moe_reference(x_all, router, gu, dn, k)[rank * 13:(rank + 1) * 13]
+    q.put((rank, (y.float() - ref.float()).abs().max().item()))
+    dist.destroy_process_group()
+
+
+def _tp_worker(rank, world, port, q):
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from drtc_amd.models import TINY_GEMMA, TINY_LLAMA, TINY_MIXTRAL, TransformerLM
+    from drtc_amd.parallel.comm import ParallelContext
+
+    res = {}
+    for cfg in (TINY_LLAMA, TINY_GEMMA, TINY_MIXTRAL.replace(experts_per_token=4)):
+        pc = ParallelContext.from_world(tp=True, ep=cfg.is_moe)
+        m = TransformerLM(cfg, "cpu", pc=pc, seed=21)
+        out = m.forward_reference([list(range(3, 40))])[0]
+        full = TransformerLM(cfg, "cpu", seed=21).forward_reference([list(range(3, 40))])[0]
+        res[cfg.name] = (out.float() - full.float()).abs().max().item() / full.float().abs().max().item()
+    q.put((rank, res))
+    dist.destroy_process_group()
+
+
+def _run(fn, world=2):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=fn, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    out = [q.get(timeout=240) for _ in ps]
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return out
+
+
+def test_ep_all_to_all_matches_reference():
+    for rank, err in _run(_ep_worker):
+        assert err < 0.03, (rank, err)
+
+
+def test_tp_and_ep_model_forward_matches_single_process():
+    for rank, res in _run(_tp_worker):
+        for name, rel in res.items():
+            assert rel < 0.03, (rank, name, rel)
