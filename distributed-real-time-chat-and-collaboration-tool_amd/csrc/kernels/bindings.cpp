@@ -64,6 +64,13 @@ PYBIND11_MODULE(_hipk, m) {
               P<const int>(cu_seqlens), P<const int>(tile_seq),
               P<const int>(tile_q0), ntiles, scale, causal, S(st));
         });
+  m.def("moe", [](u64 out, u64 x, u64 logits, u64 w_gu, u64 w_dn, int T, int H, int I, int E,
+                  int k, int e_off, int e_local, int act, u64 ws, int64_t ws_bytes, u64 st) {
+    return drtc::launch_moe(P<void>(out), P<const void>(x), P<const void>(logits),
+                            P<const void>(w_gu), P<const void>(w_dn), T, H, I, E, k, e_off,
+                            e_local, act, P<void>(ws), ws_bytes, S(st));
+  });
+  m.def("moe_workspace_bytes", &drtc::moe_workspace_bytes);
   m.def("sample", [](u64 out_tokens, u64 logits, int B, int V, int ld,
                      u64 temperature, u64 top_k, u64 top_p, uint64_t seed,
                      u64 step, u64 st) {

@@ -41,6 +41,11 @@ int launch_sample(int* out_tokens, const void* logits, int B, int V, int ld,
                   const float* temperature, const int* top_k, const float* top_p,
                   uint64_t seed, const int64_t* step, hipStream_t st);
 
+int launch_moe(void* out, const void* x, const void* router_logits, const void* w_gu,
+               const void* w_dn, int T, int H, int I, int E, int k, int e_off, int e_local,
+               int act, void* workspace, int64_t ws_bytes, hipStream_t st);
+int64_t moe_workspace_bytes(int T, int H, int I, int e_local, int k);
+
 // Raise the dynamic-LDS ceiling of the kernels that need > 64 KiB (head_dim
 // 256).  Called once at import, before any graph capture.
 int configure_kernels();

@@ -1,0 +1,330 @@
+// Mixture-of-experts on MFMA (gfx950): routing, grouped GEMMs, combine.
+// Static launch shapes (device-side tile table), so the whole MoE layer is
+// hipGraph-capturable - the decode step of Mixtral replays with no host sync.
+//
+//   moe_align_kernel      top-k over the router logits (+ softmax over the
+//                         selected logits), counting sort of the (token, slot)
+//                         pairs by expert, per-expert 128-row tile table.
+//   moe_gate_up_kernel    grouped GEMM  H[p] = act(X[tok(p)] . Wg[e]^T) * (X[tok(p)] . Wu[e]^T)
+//                         with the gate|up activation fused in the epilogue: a
+//                         wave owns matching gate and up columns, so both MFMA
+//                         accumulators of an output element sit in one lane.
+//   moe_down_kernel       grouped GEMM  Z[p] = H[p] . Wd[e]^T
+//   moe_combine_kernel    out[t] = sum_j w[t,j] * Z[pos(t,j)]   (fp32, fixed order:
+//                         deterministic, no atomics)
+//
+// GEMM structure: 256-thread workgroup, 2x2 waves, 128-row tile; operands are
+// K-contiguous rows (activations gathered by token, weights [N][K]) loaded as
+// 16-B fragments straight into registers (register double buffer over the K
+// loop), 16 MFMA 16x16x32 per wave per k-step.
+#include "common.h"
+#include "launchers.h"
+
+namespace drtc {
+
+constexpr int kMoeBM = 128;   // rows per tile
+constexpr int kMoeMaxK = 8;   // top-k bound
+
+// ---------------------------------------------------------------- align
+__global__ __launch_bounds__(1024) void moe_align_kernel(
+    const bf16_t* __restrict__ logits, int T, int E, int k,
+    int* __restrict__ sorted_tok, float* __restrict__ sorted_w,
+    int* __restrict__ inv_pos, float* __restrict__ topk_w,
+    int* __restrict__ tile_expert, int* __restrict__ tile_row0, int* __restrict__ tile_rows,
+    int* __restrict__ n_tiles, int* __restrict__ local_range, int max_tiles, int e_off,
+    int e_local) {
+  __shared__ int cnt[256], off[257], fill[256], toff[257];
+  const int tid = threadIdx.x;
+  for (int e = tid; e < 256; e += 1024) { cnt[e] = 0; fill[e] = 0; }
+  __syncthreads();
+  for (int t = tid; t < T; t += 1024) {
+    const bf16_t* lr = logits + (int64_t)t * E;
+    // sorted top-8 list kept in registers (fully unrolled: no scratch)
+    float v[kMoeMaxK];
+    int id[kMoeMaxK];
+#pragma unroll
+    for (int j = 0; j < kMoeMaxK; ++j) { v[j] = -INFINITY; id[j] = 0x7fffffff; }
+    for (int e = 0; e < E; ++e) {
+      float x = bf2f(lr[e]);
+      int xi = e;
+#pragma unroll
+      for (int j = 0; j < kMoeMaxK; ++j) {
+        // order (value desc, id asc): a displaced entry carried down the list
+        // must not overtake an equal-valued entry with a higher id
+        if (x > v[j] || (x == v[j] && xi < id[j])) {
+          const float tv = v[j]; const int ti = id[j];
+          v[j] = x; id[j] = xi; x = tv; xi = ti;
+        }
+      }
+    }
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < kMoeMaxK; ++j) s += (j < k) ? __expf(v[j] - v[0]) : 0.f;
+#pragma unroll
+    for (int j = 0; j < kMoeMaxK; ++j) {
+      if (j < k) {
+        topk_w[t * k + j] = __expf(v[j] - v[0]) / s;
+        inv_pos[t * k + j] = id[j];  // expert id for now; position after the scatter
+        atomicAdd(&cnt[id[j]], 1);
+      }
+    }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    int o = 0, to = 0;
+    for (int e = 0; e < E; ++e) {  // tiles only for this rank's experts (EP)
+      const bool loc = e >= e_off && e < e_off + e_local;
+      off[e] = o;
+      toff[e] = to;
+      o += cnt[e];
+      to += loc ? (cnt[e] + kMoeBM - 1) / kMoeBM : 0;
+    }
+    off[E] = o;
+    toff[E] = to;
+    n_tiles[0] = to < max_tiles ? to : max_tiles;
+    local_range[0] = off[e_off];
+    local_range[1] = off[e_off + e_local];
+  }
+  __syncthreads();
+  for (int e = tid; e < E; e += 1024) {
+    const int nt = toff[e + 1] - toff[e];
+    for (int i = 0; i < nt; ++i) {
+      const int ti = toff[e] + i;
+      if (ti < max_tiles) {
+        tile_expert[ti] = e - e_off;  // local weight index
+        tile_row0[ti] = off[e] + i * kMoeBM;
+        tile_rows[ti] = min(kMoeBM, cnt[e] - i * kMoeBM);
+      }
+    }
+  }
+  for (int t = tid; t < T; t += 1024) {
+    for (int j = 0; j < k; ++j) {
+      const int e = inv_pos[t * k + j];
+      const int p = off[e] + atomicAdd(&fill[e], 1);
+      sorted_tok[p] = t;
+      sorted_w[p] = topk_w[t * k + j];
+      inv_pos[t * k + j] = p;
+    }
+  }
+}
+
+// ---------------------------------------------------------------- GEMMs
+// One grouped-GEMM kernel for both projections.  Tile 128 (pair rows) x 128
+// (weight rows) x BK 64; 4 waves in 2x2, each owning a 64x64 accumulator
+// (4x4 MFMA 16x16x32 tiles).  Both operands are K-contiguous rows, staged
+// global -> LDS with global_load_lds_dwordx4 (16 B per lane, lane-linear LDS
+// image; the gather of token rows is free because the source address is
+// per lane).  Bank conflicts of the ds_read_b128 fragment reads are removed
+// by an XOR swizzle of the 16-B chunk index with (row >> 1) & 7, applied to
+// the per-lane SOURCE address and to the read address (the two sides of the
+// same involution; cdna_hip_programming.md rule 21).  With 128-B rows two
+// rows share a 256-B bank row, so (row & 1, (row >> 1) & 7) picks 16
+// distinct 16-B slots for the 16 lanes of a read group: conflict-free.
+// Two LDS buffers (64 KiB, 2 workgroups per CU): tile k+1 streams in while
+// tile k feeds the MFMAs.
+//
+// MODE 0 (gate_up): B rows 0..63 = gate rows n0.., rows 64..127 = the
+//   matching up rows I+n0..; the epilogue writes act(gate) * up, 64 columns.
+// MODE 1 (down): B rows = output columns n0..n0+127.
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+typedef __attribute__((address_space(1))) void* gbl_ptr_t;
+
+constexpr int kBK = 64;
+constexpr int kTileElems = 128 * kBK;  // one operand tile (16 KiB)
+
+DRTC_DEVICE void glds16(const bf16_t* src, bf16_t* lds_base) {
+  __builtin_amdgcn_global_load_lds((gbl_ptr_t)src, (lds_ptr_t)lds_base, 16, 0, 0);
+}
+
+template <int MODE>
+__global__ __launch_bounds__(256, 2) void moe_gemm_kernel(
+    bf16_t* __restrict__ out, const bf16_t* __restrict__ a, const bf16_t* __restrict__ w,
+    const int* __restrict__ sorted_tok, const int* __restrict__ tile_expert,
+    const int* __restrict__ tile_row0, const int* __restrict__ tile_rows,
+    const int* __restrict__ n_tiles, int K, int w_rows, int I, int ldo, int max_tiles,
+    int act) {
+  __shared__ __attribute__((aligned(16))) bf16_t lds[4 * kTileElems];  // [buf][A|B][128][64]
+  // XCD-aware remap: contiguous chunks of the launch order share an XCD (L2),
+  // and tile (row block) varies fastest, so all row blocks of one weight
+  // panel run on the same XCD and re-read the panel from its L2.
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int xcd = orig & 7, q = nwg >> 3, rmd = nwg & 7;
+  const int wgid = (xcd < rmd ? xcd * (q + 1) : rmd * (q + 1) + (xcd - rmd) * q) + (orig >> 3);
+  const int tile = wgid % max_tiles, ct = wgid / max_tiles;
+  if (tile >= n_tiles[0]) return;
+  const int e = tile_expert[tile], r0 = tile_row0[tile], nr = tile_rows[tile];
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wv >> 1, wc = wv & 1, l16 = lane & 15, g = lane >> 4;
+
+  // staging sources: wave wv stages rows [32wv, 32wv+32) of both operands,
+  // 8 rows (8 lanes x 16 B each) per glds instruction
+  const bf16_t* asrc[4];
+  const bf16_t* bsrc[4];
+  const bf16_t* we = w + (int64_t)e * w_rows * K;
+  const int n0 = MODE == 0 ? 64 * ct : 128 * ct;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = 32 * wv + 8 * i + (lane >> 3);
+    const int d = (lane & 7) ^ ((r >> 1) & 7);  // source chunk for this LDS slot
+    const int rr = r < nr ? r : 0;
+    const int64_t arow = MODE == 0 ? (int64_t)sorted_tok[r0 + rr] : (int64_t)(r0 + rr);
+    asrc[i] = a + arow * K + 8 * d;
+    const int wrow = MODE == 0 ? (r < 64 ? n0 + r : I + n0 + r - 64) : n0 + r;
+    bsrc[i] = we + (int64_t)wrow * K + 8 * d;
+  }
+  auto stage = [&](int kt, int buf) {
+    bf16_t* A = lds + buf * 2 * kTileElems;
+    bf16_t* B = A + kTileElems;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      glds16(asrc[i] + kt * kBK, A + (32 * wv + 8 * i) * kBK);
+      glds16(bsrc[i] + kt * kBK, B + (32 * wv + 8 * i) * kBK);
+    }
+  };
+  // fragment read offsets (elements) within a tile, per k-substep s
+  const int rsw = (l16 >> 1) & 7;
+  const int off0 = l16 * kBK + ((0 + g) ^ rsw) * 8;
+  const int off1 = l16 * kBK + ((4 + g) ^ rsw) * 8;
+  int brow[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    brow[j] = MODE == 0 ? (j < 2 ? 32 * wc + 16 * j : 64 + 32 * wc + 16 * (j - 2))
+                        : 64 * wc + 16 * j;
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const int nk = K / kBK;
+  stage(0, 0);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) stage(kt + 1, cur ^ 1);
+    const bf16_t* A = lds + cur * 2 * kTileElems;
+    const bf16_t* B = A + kTileElems;
+    bf16x8 fa0[4], fa1[4], fb0[4], fb1[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      fa0[i] = *(const bf16x8*)(A + (64 * wr + 16 * i) * kBK + off0);
+      fa1[i] = *(const bf16x8*)(A + (64 * wr + 16 * i) * kBK + off1);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      fb0[j] = *(const bf16x8*)(B + brow[j] * kBK + off0);
+      fb1[j] = *(const bf16x8*)(B + brow[j] * kBK + off1);
+    }
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(fa0[i], fb0[j], acc[i][j]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(fa1[i], fb1[j], acc[i][j]);
+    __builtin_amdgcn_s_setprio(0);
+    __syncthreads();  // retires the glds of tile kt+1 (vmcnt) and the reads of tile kt
+  }
+
+  // epilogue: C lane map row 4g+r, col l16 of each 16x16 tile
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = 64 * wr + 16 * i + 4 * g + r;
+      if (row >= nr) continue;
+      bf16_t* orow = out + (int64_t)(r0 + row) * ldo;
+      if constexpr (MODE == 0) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const float gt = acc[i][j][r], up = acc[i][j + 2][r];
+          float av;
+          if (act == 0) {
+            av = gt / (1.f + __expf(-gt));
+          } else {
+            const float inner = 0.7978845608028654f * (gt + 0.044715f * gt * gt * gt);
+            av = 0.5f * gt * (1.f + tanhf(inner));
+          }
+          orow[n0 + 32 * wc + 16 * j + l16] = f2bf(av * up);
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) orow[n0 + 64 * wc + 16 * j + l16] = f2bf(acc[i][j][r]);
+      }
+    }
+}
+
+__global__ __launch_bounds__(256) void moe_combine_kernel(
+    bf16_t* __restrict__ out, const bf16_t* __restrict__ zbuf, const float* __restrict__ topk_w,
+    const int* __restrict__ inv_pos, const int* __restrict__ local_range, int T, int H, int k) {
+  const int t = blockIdx.x;
+  const int lo = local_range[0], hi = local_range[1];
+  for (int c = threadIdx.x * 8; c < H; c += 256 * 8) {
+    float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int j = 0; j < k; ++j) {
+      const int p = inv_pos[t * k + j];
+      if (p < lo || p >= hi) continue;  // pair routed to another EP rank
+      const float w = topk_w[t * k + j];
+      const bf16x8 z = load_bf16x8(zbuf + (int64_t)p * H + c);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) s[q] += w * bf2f(z[q]);
+    }
+    bf16x8 o;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) o[q] = f2bf(s[q]);
+    store_bf16x8(out + (int64_t)t * H + c, o);
+  }
+}
+
+int launch_moe(void* out, const void* x, const void* router_logits, const void* w_gu,
+               const void* w_dn, int T, int H, int I, int E, int k, int e_off, int e_local,
+               int act, void* workspace, int64_t ws_bytes, hipStream_t st) {
+  if (T == 0) return 0;
+  if (E > 256 || k > kMoeMaxK || k < 1 || k > E || H % 128 != 0 || I % 64 != 0 || H % kBK != 0 ||
+      e_off < 0 || e_local < 1 || e_off + e_local > E)
+    return -1;
+  const int P = T * k;
+  const int max_tiles = (P + kMoeBM - 1) / kMoeBM + e_local;
+  // workspace carve (all 256-B aligned)
+  auto align = [](int64_t v) { return (v + 255) & ~int64_t(255); };
+  char* p = (char*)workspace;
+  int64_t o = 0;
+  int* sorted_tok = (int*)(p + o); o = align(o + 4ll * P);
+  float* sorted_w = (float*)(p + o); o = align(o + 4ll * P);
+  int* inv_pos = (int*)(p + o); o = align(o + 4ll * P);
+  float* topk_w = (float*)(p + o); o = align(o + 4ll * P);
+  int* t_e = (int*)(p + o); o = align(o + 4ll * max_tiles);
+  int* t_r0 = (int*)(p + o); o = align(o + 4ll * max_tiles);
+  int* t_n = (int*)(p + o); o = align(o + 4ll * max_tiles);
+  int* n_tiles = (int*)(p + o); o = align(o + 4);
+  int* local_range = (int*)(p + o); o = align(o + 8);
+  bf16_t* hbuf = (bf16_t*)(p + o); o = align(o + 2ll * P * I);
+  bf16_t* zbuf = (bf16_t*)(p + o); o = align(o + 2ll * P * H);
+  if (o > ws_bytes) return -2;
+  hipLaunchKernelGGL(moe_align_kernel, dim3(1), dim3(1024), 0, st, (const bf16_t*)router_logits, T,
+                     E, k, sorted_tok, sorted_w, inv_pos, topk_w, t_e, t_r0, t_n, n_tiles, local_range,
+                     max_tiles, e_off, e_local);
+  hipLaunchKernelGGL(moe_gemm_kernel<0>, dim3((I / 64) * max_tiles), dim3(256), 0, st, hbuf,
+                     (const bf16_t*)x, (const bf16_t*)w_gu, sorted_tok, t_e, t_r0, t_n, n_tiles, H,
+                     2 * I, I, I, max_tiles, act);
+  hipLaunchKernelGGL(moe_gemm_kernel<1>, dim3((H / 128) * max_tiles), dim3(256), 0, st, zbuf,
+                     (const bf16_t*)hbuf, (const bf16_t*)w_dn, sorted_tok, t_e, t_r0, t_n, n_tiles,
+                     I, H, I, H, max_tiles, 0);
+  hipLaunchKernelGGL(moe_combine_kernel, dim3(T), dim3(256), 0, st, (bf16_t*)out, zbuf, topk_w,
+                     inv_pos, local_range, T, H, k);
+  return (int)hipGetLastError();
+}
+
+int64_t moe_workspace_bytes(int T, int H, int I, int e_local, int k) {
+  auto align = [](int64_t v) { return (v + 255) & ~int64_t(255); };
+  const int64_t P = (int64_t)T * k;
+  const int64_t mt = (P + kMoeBM - 1) / kMoeBM + e_local;
+  return 4 * align(4 * P) + 3 * align(4 * mt) + align(4) + align(8) + align(2 * P * I) +
+         align(2 * P * H);
+}
+
+}  // namespace drtc

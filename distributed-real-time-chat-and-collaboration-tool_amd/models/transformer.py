@@ -93,6 +93,14 @@ class TransformerLM:
         self.cos_sin = ops.build_rope_cache(cfg.max_position, cfg.head_dim, cfg.rope_theta,
                                             cfg.rope_scaling, device=self.device)
         self.qkv_dim = (self.sh.hq + 2 * self.sh.hkv) * cfg.head_dim
+        self.moe_ws = None
+        if cfg.is_moe and self.device.type == "cuda":
+            # one persistent scratch shared by prefill chunks and every decode
+            # graph (they replay serially on one stream)
+            from ..ops import moe as _moe_ops
+            self.moe_ws = _moe_ops.make_workspace(_moe_ops.MOE_CHUNK, cfg.hidden_size,
+                                                  self.sh.expert_inter, self.sh.n_local_experts,
+                                                  cfg.experts_per_token, self.device)
 
     # ------------------------------------------------------------ weights
     def _init_weights(self, seed: int, full_then_shard: bool) -> None:
@@ -213,27 +221,22 @@ class TransformerLM:
     def _moe(self, L: dict, x: torch.Tensor) -> torch.Tensor:
         """Top-k routed experts (Mixtral: softmax over the top-2 logits).
 
-        Eager (prefill): tokens are gathered per expert (sparse, exact FLOPs).
-        Under hipGraph capture (decode) shapes must be static, so every local
-        expert runs on the whole (small) batch and its output is weighted by
-        the dense routing matrix (zero for unrouted tokens) - same result,
-        no host synchronisation."""
+        GPU: the fused HIP MoE (ops/moe.py: device-side routing + grouped
+        MFMA GEMMs, static launch shapes -> the same code runs eagerly in
+        prefill and inside the decode hipGraphs).  CPU: per-expert gather
+        (reference semantics)."""
         cfg, sh = self.cfg, self.sh
+        if ops.on_gpu(x):
+            out = ops.fused_moe(x, F.linear(x, L["router"]), L["gate_up"], L["down"],
+                                cfg.experts_per_token, cfg.act, cfg.num_experts,
+                                sh.expert_offset, workspace=self.moe_ws)
+            if self.pc.ep_size > 1:
+                return self.pc.all_reduce_ep(out)
+            return self.pc.all_reduce_tp(out)
         logits = F.linear(x, L["router"]).float()
         topv, topi = logits.topk(cfg.experts_per_token, dim=-1)
         wts = torch.softmax(topv, dim=-1)
         out = torch.zeros(x.shape[0], x.shape[1], dtype=torch.float32, device=x.device)
-        if x.is_cuda and torch.cuda.is_current_stream_capturing():
-            dense = torch.zeros(x.shape[0], cfg.num_experts, dtype=torch.float32, device=x.device)
-            dense.scatter_(1, topi, wts)
-            for le in range(sh.n_local_experts):
-                e = sh.expert_offset + le
-                h = ops.act_glu(F.linear(x, L["gate_up"][le]), cfg.act)
-                out.add_(F.linear(h, L["down"][le]).float() * dense[:, e:e + 1])
-            out = out.to(x.dtype)
-            if self.pc.ep_size > 1:
-                return self.pc.all_reduce_ep(out)
-            return self.pc.all_reduce_tp(out)
         for le in range(sh.n_local_experts):
             e = sh.expert_offset + le
             tok, slot = torch.nonzero(topi == e, as_tuple=True)

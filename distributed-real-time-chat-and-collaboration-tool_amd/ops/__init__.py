@@ -6,16 +6,17 @@ reference of the same op (used by the CPU tests and as the GPU numerics
 oracle).  Plain projection GEMMs are ``torch.nn.functional.linear``
 (hipBLASLt on ROCm); everything around them is fused here.
 """
-from ._ext import reference_mode
+from ._ext import on_gpu, reference_mode
 from .activation import act_glu, act_glu_ref
 from .attention import (KV_BLOCK, DecodeWorkspace, decode_partitioning, paged_decode_attention,
                         paged_decode_ref, prefill_attention, prefill_attention_ref, prefill_tiles)
+from .moe import fused_moe, fused_moe_ref
 from .norm import rmsnorm, rmsnorm_ref
 from .rope import build_rope_cache, kv_write_v, kv_write_v_ref, rope_kv_, rope_kv_ref
 from .sampling import sample, sample_ref
 
 __all__ = [
-    "reference_mode",
+    "on_gpu", "reference_mode", "fused_moe", "fused_moe_ref",
     "act_glu", "act_glu_ref", "KV_BLOCK", "DecodeWorkspace", "decode_partitioning",
     "paged_decode_attention", "paged_decode_ref", "prefill_attention", "prefill_attention_ref",
     "prefill_tiles", "rmsnorm", "rmsnorm_ref", "build_rope_cache", "rope_kv_", "rope_kv_ref",

@@ -1,0 +1,106 @@
+"""Fused mixture-of-experts layer (router top-k -> grouped expert GEMMs -> combine).
+
+HIP kernels: csrc/kernels/moe.hip.  One call enqueues four kernels with
+static launch shapes (the per-expert tile table lives on the device), so the
+layer is hipGraph-capturable and the Mixtral decode step replays with no
+host synchronisation and exact sparse FLOPs (the earlier graph path ran every
+expert on every token).  SURVEY.md §2 K8.
+
+Routing semantics (Mixtral): top-k of the router logits, softmax over the
+selected k logits; ties pick the lower expert id.  With expert parallelism a
+rank holds experts [e_off, e_off + e_local) and returns only their
+contribution (the caller all-reduces over the EP group).
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from ._ext import check, hipk, on_gpu, stream_ptr
+from .activation import ACTS, act_glu_ref
+
+# Largest token chunk per kernel call: bounds the workspace (P = chunk * k
+# rows of [I] and [H] intermediates) while keeping >10k workgroups per GEMM.
+MOE_CHUNK = 8192
+
+
+def route_ref(router_logits: torch.Tensor, top_k: int):
+    """(expert ids [T, k], weights [T, k] fp32) with the kernel's tie rule."""
+    lg = router_logits.float()
+    v, i = torch.sort(lg, dim=-1, descending=True, stable=True)
+    return i[:, :top_k], torch.softmax(v[:, :top_k], dim=-1)
+
+
+def fused_moe_ref(x: torch.Tensor, router_logits: torch.Tensor, w_gu: torch.Tensor,
+                  w_dn: torch.Tensor, top_k: int, act: str = "silu", e_off: int = 0) -> torch.Tensor:
+    """fp32-accumulated PyTorch reference of :func:`fused_moe`."""
+    topi, wts = route_ref(router_logits, top_k)
+    out = torch.zeros(x.shape[0], x.shape[1], dtype=torch.float32, device=x.device)
+    for le in range(w_gu.shape[0]):
+        tok, slot = torch.nonzero(topi == e_off + le, as_tuple=True)
+        if tok.numel() == 0:
+            continue
+        xe = x.index_select(0, tok).float()
+        h = act_glu_ref(xe @ w_gu[le].float().t(), act).to(x.dtype).float()
+        ye = (h @ w_dn[le].float().t()).to(x.dtype).float()
+        out.index_add_(0, tok, ye * wts[tok, slot].unsqueeze(1))
+    return out.to(x.dtype)
+
+
+def workspace_bytes(tokens: int, hidden: int, inter: int, e_local: int, top_k: int) -> int:
+    return int(hipk().moe_workspace_bytes(tokens, hidden, inter, e_local, top_k))
+
+
+def make_workspace(tokens: int, hidden: int, inter: int, e_local: int, top_k: int,
+                   device) -> torch.Tensor:
+    """Persistent scratch for up to ``tokens`` tokens per call (allocate once,
+    before any graph capture)."""
+    n = workspace_bytes(min(tokens, MOE_CHUNK), hidden, inter, e_local, top_k)
+    return torch.empty(n, dtype=torch.uint8, device=device)
+
+
+def fused_moe(x: torch.Tensor, router_logits: torch.Tensor, w_gu: torch.Tensor,
+              w_dn: torch.Tensor, top_k: int, act: str = "silu", num_experts: int | None = None,
+              e_off: int = 0, workspace: torch.Tensor | None = None,
+              out: torch.Tensor | None = None) -> torch.Tensor:
+    """y[t] = sum_j w[t,j] * down_e(act(gate_e x_t) * up_e x_t) over the top-k experts.
+
+    x [T, H] bf16; router_logits [T, E] bf16; w_gu [E_local, 2I, H] ([gate | up]
+    rows); w_dn [E_local, H, I].
+    """
+    if not on_gpu(x):
+        r = fused_moe_ref(x, router_logits, w_gu, w_dn, top_k, act, e_off)
+        if out is not None:
+            out.copy_(r)
+            return out
+        return r
+    T, H = x.shape
+    E = num_experts if num_experts is not None else router_logits.shape[1]
+    e_local, two_i, h2 = w_gu.shape
+    inter = two_i // 2
+    assert x.dtype == torch.bfloat16 and x.is_contiguous()
+    assert router_logits.dtype == torch.bfloat16 and router_logits.is_contiguous()
+    assert router_logits.shape == (T, E) and h2 == H
+    assert w_gu.is_contiguous() and w_dn.is_contiguous() and w_dn.shape == (e_local, H, inter)
+    assert E <= 256 and 1 <= top_k <= min(8, E) and H % 128 == 0 and inter % 64 == 0
+    if out is None:
+        out = torch.empty_like(x)
+    assert out.is_contiguous() and out.shape == x.shape
+    chunk = min(T, MOE_CHUNK) if T else 1
+    need = workspace_bytes(chunk, H, inter, e_local, top_k)
+    if workspace is None or workspace.numel() < need:
+        assert not torch.cuda.is_current_stream_capturing(), \
+            "fused_moe under graph capture needs a preallocated workspace"
+        workspace = torch.empty(need, dtype=torch.uint8, device=x.device)
+    lib, st = hipk(), stream_ptr(x)
+    for t0 in range(0, T, MOE_CHUNK):
+        n = min(MOE_CHUNK, T - t0)
+        check(lib.moe(out[t0].data_ptr(), x[t0].data_ptr(), router_logits[t0].data_ptr(),
+                      w_gu.data_ptr(), w_dn.data_ptr(), n, H, inter, E, top_k, e_off, e_local,
+                      ACTS[act], workspace.data_ptr(), workspace.numel(), st), "moe")
+    return out
+
+
+def router_logits(x: torch.Tensor, router_w: torch.Tensor) -> torch.Tensor:
+    """bf16 router logits (the kernel up-converts)."""
+    return F.linear(x, router_w)

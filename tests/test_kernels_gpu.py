@@ -223,3 +223,60 @@ def test_sample_distribution(hipk):
     f = torch.bincount(out, minlength=V)[[10, 20, 30]].float() / 4096
     e = torch.softmax(torch.tensor([2.0, 1.0, 0.0]), 0)
     assert (f - e).abs().max() < 0.04, (f, e)
+
+
+def _moe_inputs(T, H, I, E, seed=0):
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    x = torch.randn(T, H, device=DEV, generator=g).to(torch.bfloat16)
+    lg = torch.randn(T, E, device=DEV, generator=g).to(torch.bfloat16)
+    wgu = (torch.randn(E, 2 * I, H, device=DEV, generator=g) / math.sqrt(H)).to(torch.bfloat16)
+    wdn = (torch.randn(E, H, I, device=DEV, generator=g) / math.sqrt(I)).to(torch.bfloat16)
+    return x, lg, wgu, wdn
+
+
+@pytest.mark.parametrize("T,H,I,E,k", [(1, 256, 128, 4, 2), (37, 256, 192, 4, 2),
+                                        (300, 4096, 1792, 8, 2), (1000, 512, 256, 16, 4),
+                                        (129, 256, 64, 8, 8)])
+@pytest.mark.parametrize("act", ["silu", "gelu_tanh"])
+def test_fused_moe(hipk, T, H, I, E, k, act):
+    x, lg, wgu, wdn = _moe_inputs(T, H, I, E)
+    y = ops.fused_moe(x, lg, wgu, wdn, k, act)
+    yr = ops.fused_moe_ref(x, lg, wgu, wdn, k, act)
+    _close(y, yr, 3e-2, 3e-2, "fused_moe")
+
+
+def test_fused_moe_expert_parallel_slices_sum(hipk):
+    """EP: per-rank contributions (expert slices) sum to the full layer."""
+    T, H, I, E, k = 200, 256, 128, 8, 2
+    x, lg, wgu, wdn = _moe_inputs(T, H, I, E, seed=3)
+    full = ops.fused_moe(x, lg, wgu, wdn, k).float()
+    parts = sum(ops.fused_moe(x, lg, wgu[r * 2:(r + 1) * 2].contiguous(),
+                              wdn[r * 2:(r + 1) * 2].contiguous(), k, num_experts=E,
+                              e_off=2 * r).float() for r in range(4))
+    _close(parts, full, 3e-2, 2e-2, "ep slices")
+    yr = ops.fused_moe_ref(x, lg, wgu[2:4], wdn[2:4], k, e_off=2)
+    y = ops.fused_moe(x, lg, wgu[2:4].contiguous(), wdn[2:4].contiguous(), k, num_experts=E,
+                      e_off=2)
+    _close(y, yr, 3e-2, 3e-2, "ep rank 1")
+
+
+def test_fused_moe_chunked_and_graph(hipk):
+    """> MOE_CHUNK tokens (chunked calls) and hipGraph capture/replay."""
+    from drtc_amd.ops import moe as moe_ops
+    T, H, I, E, k = moe_ops.MOE_CHUNK + 300, 256, 64, 4, 2
+    x, lg, wgu, wdn = _moe_inputs(T, H, I, E, seed=5)
+    _close(ops.fused_moe(x, lg, wgu, wdn, k), ops.fused_moe_ref(x, lg, wgu, wdn, k), 3e-2, 3e-2,
+           "chunked")
+    xs, ls = x[:64].clone(), lg[:64].clone()
+    ws = moe_ops.make_workspace(64, H, I, E, k, DEV)
+    out = torch.empty_like(xs)
+    ops.fused_moe(xs, ls, wgu, wdn, k, workspace=ws, out=out)
+    torch.cuda.synchronize()
+    gr = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(gr):
+        ops.fused_moe(xs, ls, wgu, wdn, k, workspace=ws, out=out)
+    xs.copy_(x[64:128])
+    ls.copy_(lg[64:128])
+    gr.replay()
+    torch.cuda.synchronize()
+    _close(out, ops.fused_moe_ref(x[64:128], lg[64:128], wgu, wdn, k), 3e-2, 3e-2, "graph")
