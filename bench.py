@@ -73,6 +73,8 @@ def main() -> None:
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--max-model-len", type=int, default=2048)
     ap.add_argument("--tp", type=int, default=1, help="tensor-parallel degree (= WORLD_SIZE)")
+    ap.add_argument("--custom-allreduce", action="store_true",
+                    help="TP: one-shot IPC all-reduce for decode-sized messages (else RCCL)")
     args = ap.parse_args()
 
     rank, world = init_distributed()
@@ -92,6 +94,8 @@ def main() -> None:
         assert tp == world, "--tp must equal WORLD_SIZE (one TP group per node)"
         from drtc_amd.parallel import ParallelContext
         pc = ParallelContext.from_world(tp=True, ep=cfg.is_moe)
+        if args.custom_allreduce:
+            pc.enable_custom_allreduce()
     else:
         pc = None
     dp_rank = 0 if tp > 1 else rank

@@ -5,6 +5,10 @@
 // .cuda_stream`; shape/dtype validation happens in the Python op wrappers
 // (drtc_amd/ops), which also check every launcher's return code.
 #include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <cstring>
+#include <vector>
 
 #include "launchers.h"
 
@@ -71,6 +75,38 @@ PYBIND11_MODULE(_hipk, m) {
                             e_local, act, P<void>(ws), ws_bytes, S(st));
   });
   m.def("moe_workspace_bytes", &drtc::moe_workspace_bytes);
+  m.def("custom_ar_buffer_bytes", &drtc::custom_ar_buffer_bytes);
+  m.def("custom_allreduce", [](u64 out, u64 in, int64_t n, const std::vector<u64>& bases, int rank,
+                               int64_t stage_elems, u64 st) {
+    drtc::ArPeers p{};
+    if (bases.size() > 8) return -1;
+    for (size_t i = 0; i < bases.size(); ++i) p.base[i] = P<char>(bases[i]);
+    return drtc::launch_custom_allreduce(P<void>(out), P<const void>(in), n, p, rank,
+                                         (int)bases.size(), stage_elems, S(st));
+  });
+  m.def("ar_alloc", [](int64_t bytes) {
+    void* p = nullptr;
+    const int rc = drtc::ar_alloc(&p, bytes);
+    if (rc) throw std::runtime_error("ar_alloc failed: " + std::to_string(rc));
+    return (u64)p;
+  });
+  m.def("ar_free", [](u64 p) { return drtc::ar_free(P<void>(p)); });
+  m.def("ar_ipc_get", [](u64 p) {
+    char h[64];
+    const int rc = drtc::ar_ipc_get(P<void>(p), h);
+    if (rc) throw std::runtime_error("hipIpcGetMemHandle failed: " + std::to_string(rc));
+    return py::bytes(h, 64);
+  });
+  m.def("ar_ipc_open", [](py::bytes handle) {
+    std::string h = handle;
+    if (h.size() != 64) throw std::runtime_error("bad IPC handle size");
+    void* p = nullptr;
+    const int rc = drtc::ar_ipc_open(h.data(), &p);
+    if (rc) throw std::runtime_error("hipIpcOpenMemHandle failed: " + std::to_string(rc));
+    return (u64)p;
+  });
+  m.def("ar_ipc_close", [](u64 p) { return drtc::ar_ipc_close(P<void>(p)); });
+  m.def("ar_error", [](u64 base) { return drtc::ar_error(P<void>(base)); });
   m.def("sample", [](u64 out_tokens, u64 logits, int B, int V, int ld,
                      u64 temperature, u64 top_k, u64 top_p, uint64_t seed,
                      u64 step, u64 st) {

@@ -46,6 +46,20 @@ int launch_moe(void* out, const void* x, const void* router_logits, const void* 
                int act, void* workspace, int64_t ws_bytes, hipStream_t st);
 int64_t moe_workspace_bytes(int T, int H, int I, int e_local, int k);
 
+// One-shot P2P all-reduce over IPC-mapped staging buffers (allreduce.hip).
+struct ArPeers {
+  char* base[8];
+};
+int64_t custom_ar_buffer_bytes(int64_t stage_elems);
+int launch_custom_allreduce(void* out, const void* in, int64_t n, const ArPeers& peers, int rank,
+                            int world, int64_t stage_elems, hipStream_t st);
+int ar_alloc(void** p, int64_t bytes);
+int ar_free(void* p);
+int ar_ipc_get(void* p, char* handle);  // 64-byte handle
+int ar_ipc_open(const char* handle, void** p);
+int ar_ipc_close(void* p);
+int ar_error(void* base);
+
 // Raise the dynamic-LDS ceiling of the kernels that need > 64 KiB (head_dim
 // 256).  Called once at import, before any graph capture.
 int configure_kernels();

@@ -43,7 +43,8 @@ def build_backend(args):
     if args.tp > 1:
         from ..parallel.tp_engine import TPEngineGroup
 
-        return TPEngineGroup(args.model, args.tp, engine_kw, tok)
+        return TPEngineGroup(args.model, args.tp, engine_kw, tok,
+                             custom_allreduce=args.custom_allreduce)
     n = args.gpus
     if n <= 1:
         import torch
@@ -79,6 +80,8 @@ def main(argv=None):
     ap.add_argument("--model", default="llama-3-8b")
     ap.add_argument("--gpus", type=int, default=1, help="data-parallel replicas (1 process/GPU)")
     ap.add_argument("--tp", type=int, default=1, help="tensor-parallel degree")
+    ap.add_argument("--custom-allreduce", action="store_true",
+                    help="one-shot IPC all-reduce for decode-sized TP messages (else RCCL)")
     ap.add_argument("--max-batch", type=int, default=256)
     ap.add_argument("--max-model-len", type=int, default=4096)
     ap.add_argument("--no-graphs", action="store_true")

@@ -48,6 +48,7 @@ class ParallelContext:
     ep_size: int = 1
     ep_rank: int = 0
     ep_group: object = None
+    custom_ar: object = None     # CustomAllReduce over the TP group (decode-sized messages)
 
     @staticmethod
     def single() -> "ParallelContext":
@@ -66,13 +67,28 @@ class ParallelContext:
             ctx.ep_size, ctx.ep_rank, ctx.ep_group = w, r, dist.group.WORLD
         return ctx
 
+    def enable_custom_allreduce(self, max_bytes: int = 4 << 20) -> None:
+        """Route small TP all-reduces through the one-shot IPC kernel
+        (parallel/custom_allreduce.py); larger ones stay on RCCL."""
+        if self.tp_size <= 1 or not torch.cuda.is_available():
+            return
+        from .custom_allreduce import CustomAllReduce
+        ranks = dist.get_process_group_ranks(self.tp_group)
+        cpu_group = dist.new_group(ranks=ranks, backend="gloo")
+        self.custom_ar = CustomAllReduce(cpu_group, max_bytes=max_bytes)
+
     def all_reduce_tp(self, x: torch.Tensor) -> torch.Tensor:
         if self.tp_size > 1:
+            if self.custom_ar is not None and self.custom_ar.can(x):
+                return self.custom_ar.all_reduce(x)
             dist.all_reduce(x, group=self.tp_group)
         return x
 
     def all_reduce_ep(self, x: torch.Tensor) -> torch.Tensor:
         if self.ep_size > 1:
+            if (self.custom_ar is not None and self.ep_group is self.tp_group
+                    and self.custom_ar.can(x)):
+                return self.custom_ar.all_reduce(x)
             dist.all_reduce(x, group=self.ep_group)
         return x
 

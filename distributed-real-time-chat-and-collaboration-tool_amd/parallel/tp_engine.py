@@ -31,7 +31,8 @@ def _free_port() -> int:
     return p
 
 
-def tp_worker(rank: int, world: int, port: int, model_name: str, engine_kw: dict, inq, outq):
+def tp_worker(rank: int, world: int, port: int, model_name: str, engine_kw: dict, inq, outq,
+              custom_ar: bool = False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
     import torch
@@ -46,6 +47,8 @@ def tp_worker(rank: int, world: int, port: int, model_name: str, engine_kw: dict
         cpu = dist.new_group(backend="gloo")
         dev = torch.device("cuda", rank) if torch.cuda.is_available() else torch.device("cpu")
         pc = ParallelContext.from_world(tp=True)
+        if custom_ar and dev.type == "cuda":
+            pc.enable_custom_allreduce()
         cfg = get_config(model_name)
         model = TransformerLM(cfg, dev, pc=pc, seed=1234)
         eng = LLMEngine(model, seed=0, **engine_kw)
@@ -89,13 +92,14 @@ class TPEngineGroup:
     """Front-end handle: generate() on a TP group of ``world`` GPUs."""
 
     def __init__(self, model_name: str, world: int, engine_kw: dict, tokenizer,
-                 start_timeout: float = 1800):
+                 start_timeout: float = 1800, custom_allreduce: bool = False):
         ctx = mp.get_context("spawn")
         self.inq, self.outq = ctx.Queue(), ctx.Queue()
         port = _free_port()
         self.procs = [ctx.Process(target=tp_worker, daemon=True,
                                   args=(r, world, port, model_name, engine_kw,
-                                        self.inq if r == 0 else None, self.outq if r == 0 else None))
+                                        self.inq if r == 0 else None, self.outq if r == 0 else None,
+                                        custom_allreduce))
                       for r in range(world)]
         for p in self.procs:
             p.start()
