@@ -73,9 +73,14 @@ def main() -> None:
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--max-model-len", type=int, default=2048)
     ap.add_argument("--tp", type=int, default=1, help="tensor-parallel degree (= WORLD_SIZE)")
+    ap.add_argument("--trace", default=None, metavar="PATH",
+                    help="record engine/graph spans (roctx + Chrome trace JSON at PATH)")
     ap.add_argument("--custom-allreduce", action="store_true",
                     help="TP: one-shot IPC all-reduce for decode-sized messages (else RCCL)")
     args = ap.parse_args()
+    if args.trace:
+        from drtc_amd.utils import tracing
+        tracing.enable(True)
 
     rank, world = init_distributed()
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -140,10 +145,11 @@ def main() -> None:
     if device.type == "cuda":
         torch.cuda.synchronize()
     t_start = time.perf_counter()
-    lat, gen = [], 0
+    lat, r_ttft, gen = [], [], 0
     for s in range(args.steps):
         reqs = serve(prompts[s])
         lat.extend(r.latency for r in reqs)
+        r_ttft.extend(r.ttft for r in reqs)
         gen += sum(len(r.output_ids) for r in reqs)
     if device.type == "cuda":
         torch.cuda.synchronize()
@@ -152,14 +158,17 @@ def main() -> None:
     elapsed = time.perf_counter() - t_start
 
     p50 = statistics.median(lat)
-    stats = torch.tensor([elapsed, float(gen), float(prompt_tokens), p50], dtype=torch.float64,
+    p99 = sorted(lat)[min(len(lat) - 1, int(round(0.99 * (len(lat) - 1))))]
+    ttft50 = statistics.median(r_ttft)
+    stats = torch.tensor([elapsed, float(gen), float(prompt_tokens), p50, p99, ttft50],
+                         dtype=torch.float64,
                          device=device)
     if world > 1:
         mx = stats.clone()
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
         sm = stats.clone()
         dist.all_reduce(sm, op=dist.ReduceOp.SUM)
-        elapsed, p50 = float(mx[0]), float(mx[3])
+        elapsed, p50, p99, ttft50 = float(mx[0]), float(mx[3]), float(mx[4]), float(mx[5])
         if tp == 1:  # DP replicas serve different requests; TP ranks serve the same ones
             gen, prompt_tokens = float(sm[1]), float(sm[2])
     tps = gen / elapsed
@@ -187,10 +196,16 @@ def main() -> None:
                        f"t={params.temperature},top_k={params.top_k},top_p={params.top_p}",
                        "graphs": not args.no_graphs},
             "p50_latency_ms": round(1000 * p50, 1),
+            "p99_latency_ms": round(1000 * p99, 1),
+            "p50_ttft_ms": round(1000 * ttft50, 1),
             "total_tokens_per_s": round((gen + prompt_tokens) / elapsed, 1),
             "engine_stats": dict(eng.stats),
         }
         print(json.dumps(out), flush=True)
+        if args.trace:
+            from drtc_amd.utils import tracing
+            n = tracing.dump_chrome_trace(args.trace)
+            log(rank, f"wrote {n} trace spans to {args.trace}")
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

@@ -15,6 +15,7 @@ import numpy as np
 import torch
 
 from .. import ops
+from ..utils import tracing
 from ..models.transformer import DecodeMeta, TransformerLM
 
 DEFAULT_BUCKETS = (1, 2, 4, 8, 16, 24, 32, 48, 64, 96, 128, 160, 192, 224, 256, 320, 384,
@@ -146,10 +147,11 @@ class DecodeRunner:
         if g is None and self.use_graphs:
             self.capture(Bb)
             g = self._graphs[Bb]
-        if g is not None:
-            g.replay()
-        else:
-            self._forward(Bb)
+        with tracing.span("decode.graph_replay" if g is not None else "decode.eager", bucket=Bb):
+            if g is not None:
+                g.replay()
+            else:
+                self._forward(Bb)
         if nb:
             self.h_out[:n].copy_(self.out[:n], non_blocking=True)
             torch.cuda.current_stream(self.device).synchronize()

@@ -26,6 +26,8 @@ import numpy as np
 import torch
 
 from .. import ops
+from ..utils import tracing
+from ..utils.metrics import METRICS
 from ..models.transformer import PrefillMeta, TransformerLM
 from .decode_runner import DEFAULT_BUCKETS, DecodeRunner
 from .kv_cache import PagedKVCache
@@ -115,9 +117,32 @@ class LLMEngine:
         with self.lock:
             batch = self._admit()
         if batch:
-            return self._run_prefill(batch)
-        if self.running:
-            return self._run_decode()
+            with tracing.span("engine.prefill", seqs=len(batch)):
+                done = self._run_prefill(batch)
+        elif self.running:
+            with tracing.span("engine.decode", batch=len(self.running)):
+                done = self._run_decode()
+        else:
+            return []
+        self._record(done)
+        return done
+
+    def _record(self, done: list[Request]) -> None:
+        """Serving metrics: TTFT / TPOT / end-to-end latency per finished
+        request, KV-cache occupancy and queue depths per step."""
+        M = METRICS
+        for r in done:
+            M.observe("engine.ttft_s", r.ttft)
+            M.observe("engine.e2e_s", r.finish_time - r.arrival_time)
+            if len(r.output_ids) > 1:
+                M.observe("engine.tpot_s", (r.finish_time - r.first_token_time)
+                          / (len(r.output_ids) - 1))
+            M.inc("engine.generated_tokens", len(r.output_ids))
+            M.inc("engine.finished")
+        used, free = self.alloc.num_used, self.alloc.num_free
+        M.set_gauge("engine.kv_used_frac", used / max(1, used + free))
+        M.set_gauge("engine.running", len(self.running))
+        M.set_gauge("engine.waiting", len(self.waiting))
         return []
 
     # ------------------------------------------------------------ admission
@@ -336,6 +361,9 @@ class EngineLoop:
         self.engine.add_request(req)
         self._wake.set()
         return req
+
+    def alive(self) -> bool:
+        return self.thread.is_alive() and self.error is None
 
     def _loop(self) -> None:
         try:

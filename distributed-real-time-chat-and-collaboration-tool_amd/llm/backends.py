@@ -93,8 +93,14 @@ class EngineBackend:
 
 
 # ------------------------------------------------------------- DP workers
-def _worker_main(rank: int, device: str, model_name: str, engine_kw: dict, inq, outq, seed: int):
-    """One engine replica per GPU (separate process: one process per GPU)."""
+def _worker_main(rank: int, device: str, model_name: str, engine_kw: dict, inq, outq, seed: int,
+                 hb_interval: float = 0.5):
+    """One engine replica per GPU (separate process: one process per GPU).
+
+    Besides results, the worker sends a heartbeat with its engine counters
+    every ``hb_interval`` s; the parent's health monitor evicts a replica
+    whose process died or whose heartbeats stopped (SURVEY §5 failure
+    detection: per-GPU replica eviction)."""
     import torch
 
     from ..engine.engine import EngineLoop, LLMEngine
@@ -115,11 +121,22 @@ def _worker_main(rank: int, device: str, model_name: str, engine_kw: dict, inq, 
     pending = {}
 
     def watcher():
+        last_hb = 0.0
         while True:
             for rid, r in list(pending.items()):
                 if r._done.is_set():
                     pending.pop(rid, None)
                     outq.put(("done", rid, (r.output_ids, r.finish_reason)))
+            if not loop.alive():  # engine fault: exit so the parent evicts/respawns us
+                log.error("engine loop of replica %d died: %r", rank, loop.error)
+                os._exit(3)
+            now = time.monotonic()
+            if now - last_hb >= hb_interval:
+                last_hb = now
+                st = dict(eng.stats)
+                st.update(running=len(eng.running), waiting=len(eng.waiting),
+                          pending=len(pending), alive=loop.alive())
+                outq.put(("hb", rank, st))
             time.sleep(0.001)
 
     threading.Thread(target=watcher, daemon=True).start()
@@ -139,40 +156,134 @@ def _worker_main(rank: int, device: str, model_name: str, engine_kw: dict, inq, 
 
 
 class WorkerPool:
-    """N engine processes; results come back on one queue."""
+    """N engine processes (one per GPU); results and heartbeats come back on
+    one queue.
 
-    def __init__(self, model_name: str, devices: list[str], engine_kw: dict, seed: int = 1234):
-        ctx = mp.get_context("spawn")
-        self.outq = ctx.Queue()
-        self.inqs = [ctx.Queue() for _ in devices]
-        self.procs = [ctx.Process(target=_worker_main, args=(i, d, model_name, engine_kw, q, self.outq, seed),
-                                  daemon=True) for i, (d, q) in enumerate(zip(devices, self.inqs))]
-        for p in self.procs:
-            p.start()
-        ready = 0
-        while ready < len(self.procs):
-            kind, rank, info = self.outq.get(timeout=1800)
-            if kind == "fatal":
-                raise GenerationError(f"engine worker {rank} failed: {info}")
-            ready += 1
+    Health: a monitor thread evicts a replica when its process exits or its
+    heartbeat is older than ``hb_timeout``; every request in flight on it is
+    failed with ``error: replica lost`` (the router re-dispatches those), and
+    with ``max_restarts > 0`` the replica is respawned on the same device and
+    rejoins the pool once its engine reports ready (elastic recovery)."""
+
+    LOST = "error: replica lost"
+
+    def __init__(self, model_name: str, devices: list[str], engine_kw: dict, seed: int = 1234,
+                 hb_interval: float = 0.5, hb_timeout: float = 30.0, max_restarts: int = 1,
+                 start_timeout: float = 1800):
+        self._ctx = mp.get_context("spawn")
+        self.model_name, self.devices, self.engine_kw, self.seed = model_name, devices, engine_kw, seed
+        self.hb_interval, self.hb_timeout, self.max_restarts = hb_interval, hb_timeout, max_restarts
+        n = len(devices)
+        self.outq = self._ctx.Queue()
+        self.inqs = [None] * n
+        self.procs = [None] * n
+        self.healthy = [False] * n
+        self.restarts = [0] * n
+        self.last_hb = [time.monotonic()] * n
+        self.worker_stats: list[dict] = [{} for _ in range(n)]
+        self.evictions: list[tuple[int, str]] = []
         self.futures: dict[str, tuple] = {}
-        self.load = [0] * len(self.procs)
+        self.load = [0] * n
         self._lock = threading.Lock()
         self._ids = itertools.count()
+        self._closed = False
+        for w in range(n):
+            self._spawn(w)
+        t_end = time.monotonic() + start_timeout
+        while not all(self.healthy):
+            kind, rank, info = self.outq.get(timeout=max(1.0, t_end - time.monotonic()))
+            if kind == "fatal":
+                self.close()
+                raise GenerationError(f"engine worker {rank} failed: {info}")
+            if kind == "ready":
+                self.healthy[rank] = True
+                self.last_hb[rank] = time.monotonic()
         threading.Thread(target=self._collect, daemon=True).start()
+        threading.Thread(target=self._monitor, daemon=True).start()
+
+    def _spawn(self, w: int) -> None:
+        self.inqs[w] = self._ctx.Queue()
+        self.procs[w] = self._ctx.Process(
+            target=_worker_main, daemon=True,
+            args=(w, self.devices[w], self.model_name, self.engine_kw, self.inqs[w], self.outq,
+                  self.seed, self.hb_interval))
+        self.procs[w].start()
 
     def _collect(self):
-        while True:
-            kind, rid, payload = self.outq.get()
+        while not self._closed:
+            try:
+                kind, rid, payload = self.outq.get(timeout=0.5)
+            except queue.Empty:
+                continue
+            except (EOFError, OSError):
+                return
+            if kind == "hb":
+                with self._lock:
+                    self.last_hb[rid] = time.monotonic()
+                    self.worker_stats[rid] = payload
+                continue
+            if kind == "ready":  # a respawned replica rejoins
+                with self._lock:
+                    self.healthy[rid] = True
+                    self.last_hb[rid] = time.monotonic()
+                log.info("engine replica %d back in service", rid)
+                continue
+            if kind == "fatal":
+                log.error("engine replica %s failed to start: %s", rid, payload)
+                continue
             if kind != "done":
                 continue
             with self._lock:
                 ev, slot, w = self.futures.get(rid, (None, None, None))
-                if ev is None:
+                if ev is None or slot:
                     continue
                 slot.append(payload)
                 self.load[w] -= 1
             ev.set()
+
+    def _monitor(self):
+        while not self._closed:
+            time.sleep(min(0.25, self.hb_interval))
+            now = time.monotonic()
+            for w, p in enumerate(self.procs):
+                if not self.healthy[w]:
+                    continue
+                if not p.is_alive():
+                    self.evict(w, f"process exited (code {p.exitcode})")
+                elif now - self.last_hb[w] > self.hb_timeout:
+                    self.evict(w, f"no heartbeat for {now - self.last_hb[w]:.1f}s")
+
+    def evict(self, w: int, reason: str) -> None:
+        """Take replica ``w`` out of service and fail its in-flight requests."""
+        failed = []
+        with self._lock:
+            if not self.healthy[w]:
+                return
+            self.healthy[w] = False
+            self.evictions.append((w, reason))
+            for rid, (ev, slot, ww) in self.futures.items():
+                if ww == w and not slot:
+                    slot.append(([], f"{self.LOST} ({reason})"))
+                    failed.append(ev)
+            self.load[w] = 0
+        log.error("evicting engine replica %d: %s", w, reason)
+        for ev in failed:
+            ev.set()
+        p = self.procs[w]
+        if p.is_alive():
+            p.kill()
+        p.join(timeout=5)
+        if not self._closed and self.restarts[w] < self.max_restarts:
+            self.restarts[w] += 1
+            log.info("respawning engine replica %d on %s", w, self.devices[w])
+            self._spawn(w)
+
+    def pick(self) -> int:
+        with self._lock:
+            live = [i for i in range(len(self.procs)) if self.healthy[i]]
+            if not live:
+                raise GenerationError("no healthy engine replica")
+            return min(live, key=lambda i: self.load[i])
 
     def submit(self, worker: int, ids, params):
         rid = f"w{worker}-{next(self._ids)}"
@@ -180,6 +291,11 @@ class WorkerPool:
         with self._lock:
             self.futures[rid] = (ev, slot, worker)
             self.load[worker] += 1
+            if not self.healthy[worker]:  # raced with an eviction
+                slot.append(([], f"{self.LOST} (not in service)"))
+                ev.set()
+                self.load[worker] -= 1
+                return rid, ev, slot
         self.inqs[worker].put((rid, ids, params))
         return rid, ev, slot
 
@@ -187,46 +303,69 @@ class WorkerPool:
         with self._lock:
             self.futures.pop(rid, None)
 
+    def health(self) -> list[dict]:
+        with self._lock:
+            now = time.monotonic()
+            return [dict(replica=w, device=self.devices[w], healthy=self.healthy[w],
+                         heartbeat_age_s=round(now - self.last_hb[w], 3), load=self.load[w],
+                         restarts=self.restarts[w], **self.worker_stats[w])
+                    for w in range(len(self.procs))]
+
     def close(self):
-        for q in self.inqs:
-            q.put(None)
+        self._closed = True
+        for w, q in enumerate(self.inqs):
+            if q is not None and self.procs[w] is not None and self.procs[w].is_alive():
+                q.put(None)
         for p in self.procs:
-            p.join(timeout=10)
+            if p is not None:
+                p.join(timeout=10)
+                if p.is_alive():
+                    p.kill()
 
 
 class ReplicaRouter:
-    """Least-outstanding routing over a WorkerPool (one replica per GPU)."""
+    """Least-outstanding routing over the healthy replicas of a WorkerPool
+    (one replica per GPU).  A request whose replica is evicted mid-flight is
+    re-dispatched once to another healthy replica."""
 
-    def __init__(self, pool: WorkerPool, tokenizer, max_model_len: int):
+    def __init__(self, pool: WorkerPool, tokenizer, max_model_len: int, max_redispatch: int = 1):
         self.pool = pool
         self.tok = tokenizer
         self.max_model_len = max_model_len
+        self.max_redispatch = max_redispatch
 
     def generate(self, prompts, params, timeout=None):
         if isinstance(params, SamplingParams):
             params = [params] * len(prompts)
-        handles = []
+        jobs = []
         for p, prm in zip(prompts, params):
             ids = self.tok.encode(p)
             limit = self.max_model_len - prm.max_new_tokens - 1
             if len(ids) > limit:
                 ids = ids[:1] + ids[len(ids) - limit + 1:]
-            w = min(range(len(self.pool.load)), key=lambda i: self.pool.load[i])
-            handles.append(self.pool.submit(w, ids, prm))
+            jobs.append([ids, prm, self.pool.submit(self.pool.pick(), ids, prm), 0])
         deadline = None if timeout is None else time.monotonic() + timeout
         outs = []
         try:
-            for rid, ev, slot in handles:
-                left = None if deadline is None else max(0.0, deadline - time.monotonic())
-                if not ev.wait(left):
-                    raise GenerationError("generation timed out")
-                ids, reason = slot[0]
-                if reason.startswith("error"):
-                    raise GenerationError(reason)
-                outs.append(self.tok.decode(ids))
+            for job in jobs:
+                while True:
+                    rid, ev, slot = job[2]
+                    left = None if deadline is None else max(0.0, deadline - time.monotonic())
+                    if not ev.wait(left):
+                        raise GenerationError("generation timed out")
+                    ids, reason = slot[0]
+                    if reason.startswith(WorkerPool.LOST) and job[3] < self.max_redispatch:
+                        self.pool.release(rid)
+                        job[3] += 1
+                        job[2] = self.pool.submit(self.pool.pick(), job[0], job[1])
+                        continue
+                    if reason.startswith("error"):
+                        raise GenerationError(reason)
+                    outs.append(self.tok.decode(ids))
+                    break
         finally:
-            for rid, _, _ in handles:
-                self.pool.release(rid)
+            for job in jobs:
+                self.pool.release(job[2][0])
         return outs
 
 

@@ -12,6 +12,7 @@ are identical to those of protoc-generated code for the same contract.
 """
 from __future__ import annotations
 
+import time
 import types
 from dataclasses import dataclass
 
@@ -172,12 +173,32 @@ def _unimplemented(request, context):
     raise NotImplementedError("Method not implemented!")
 
 
+def _instrumented(fn, label: str):
+    """Per-RPC latency histogram + request counter + trace span."""
+    from ..utils import tracing
+    from ..utils.metrics import METRICS
+
+    hist, cnt, span = f"rpc.{label}.latency_s", f"rpc.{label}.calls", f"rpc {label}"
+
+    def handler(request, context):
+        t = time.perf_counter()
+        try:
+            with tracing.span(span):
+                return fn(request, context)
+        finally:
+            METRICS.observe(hist, time.perf_counter() - t)
+            METRICS.inc(cnt)
+    return handler
+
+
 def add_servicer(server: grpc.Server, service: Service, impl) -> None:
     """Register ``impl``'s methods (by RPC name) on ``server``; missing
     methods answer UNIMPLEMENTED like a protoc base servicer."""
     handlers = {}
     for m in service.methods:
         fn = getattr(impl, m.name, None) or _unimplemented
+        if not m.server_streaming and fn is not _unimplemented:
+            fn = _instrumented(fn, f"{service.full_name}/{m.name}")
         mk = grpc.unary_stream_rpc_method_handler if m.server_streaming else grpc.unary_unary_rpc_method_handler
         handlers[m.name] = mk(fn, request_deserializer=m.request.FromString,
                               response_serializer=m.response.SerializeToString)

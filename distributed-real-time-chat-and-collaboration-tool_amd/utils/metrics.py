@@ -54,11 +54,16 @@ class Registry:
     def __init__(self):
         self._lock = threading.Lock()
         self.counters: dict[str, float] = defaultdict(float)
+        self.gauges: dict[str, float] = {}
         self.hists: dict[str, Histogram] = {}
 
     def inc(self, name: str, v: float = 1.0) -> None:
         with self._lock:
             self.counters[name] += v
+
+    def set_gauge(self, name: str, v: float) -> None:
+        with self._lock:
+            self.gauges[name] = v
 
     def observe(self, name: str, v: float) -> None:
         with self._lock:
@@ -77,12 +82,13 @@ class Registry:
 
     def snapshot(self) -> dict:
         with self._lock:
-            return {"counters": dict(self.counters),
+            return {"counters": dict(self.counters), "gauges": dict(self.gauges),
                     "histograms": {k: h.summary() for k, h in self.hists.items()}}
 
     def reset(self) -> None:
         with self._lock:
             self.counters.clear()
+            self.gauges.clear()
             self.hists.clear()
 
 

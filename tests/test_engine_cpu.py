@@ -137,3 +137,30 @@ def test_tokenizer_roundtrip_and_density():
     words = "should we review the project plan tomorrow after the meeting".split()
     assert len(tok.encode(" ".join(words), add_bos=False)) == len(words)
     assert len(tok.id_to_tok) == 128256
+
+
+def test_tracing_spans_and_serving_metrics(tmp_path):
+    import json
+
+    from drtc_amd.utils import tracing
+    from drtc_amd.utils.metrics import METRICS
+
+    METRICS.reset()
+    tracing.clear()
+    tracing.enable(True)
+    try:
+        eng = LLMEngine(TransformerLM(TINY_LLAMA, "cpu", seed=3), max_batch=4, max_model_len=256,
+                        num_blocks=64, use_graphs=False)
+        eng.generate([[1, 5, 6, 7], [1, 9]], SamplingParams.greedy(5, ignore_eos=True))
+    finally:
+        tracing.enable(False)
+    names = {e["name"] for e in tracing.events()}
+    assert {"engine.prefill", "engine.decode", "decode.eager"} <= names
+    n = tracing.dump_chrome_trace(str(tmp_path / "trace.json"))
+    data = json.load(open(tmp_path / "trace.json"))
+    assert n == len(data["traceEvents"]) > 0 and all(e["ph"] == "X" for e in data["traceEvents"])
+    snap = METRICS.snapshot()
+    h = snap["histograms"]
+    assert h["engine.ttft_s"]["count"] == 2 and h["engine.tpot_s"]["count"] == 2
+    assert snap["counters"]["engine.generated_tokens"] == 10
+    assert 0.0 <= snap["gauges"]["engine.kv_used_frac"] <= 1.0

@@ -208,3 +208,34 @@ def test_legacy_chat_service(tmp_path):
     from drtc_amd.utils.pickle_compat import safe_load
     d = safe_load(str(tmp_path / "server_data" / "users.pkl"))
     assert {"users", "users_by_email", "users_by_id"} <= set(d) and "dave" in d["users"]
+
+
+def test_replica_pool_evicts_dead_replica_and_respawns():
+    """DP failure detection: a killed engine process is evicted, its in-flight
+    requests are re-dispatched to a healthy replica, and it is respawned."""
+    import time
+
+    from drtc_amd.engine import ChatTokenizer, SamplingParams
+    from drtc_amd.llm.backends import ReplicaRouter, WorkerPool
+    from drtc_amd.models import TINY_LLAMA
+
+    kw = dict(max_batch=4, max_model_len=256, num_blocks=64, use_graphs=False)
+    pool = WorkerPool("tiny-llama", ["cpu", "cpu"], kw, hb_interval=0.2, hb_timeout=20,
+                      max_restarts=1)
+    try:
+        router = ReplicaRouter(pool, ChatTokenizer(TINY_LLAMA.vocab_size), 256)
+        prm = SamplingParams.greedy(4, ignore_eos=True)
+        assert len(router.generate(["hello there"] * 4, prm, timeout=60)) == 4
+        pool.procs[0].kill()
+        outs = router.generate(["after the crash"] * 4, prm, timeout=60)
+        assert len(outs) == 4
+        assert pool.evictions and pool.evictions[0][0] == 0
+        t0 = time.monotonic()
+        while not pool.healthy[0] and time.monotonic() - t0 < 60:
+            time.sleep(0.2)
+        assert pool.healthy[0] and pool.restarts[0] == 1
+        h = pool.health()
+        assert h[1]["healthy"] and "running" in h[1]
+        assert len(router.generate(["back again"] * 4, prm, timeout=60)) == 4
+    finally:
+        pool.close()
