@@ -1,0 +1,154 @@
+#!/usr/bin/env python3
+"""End-to-end service load driver (SURVEY §4.2 "Benchmarks").
+
+Drives smart-reply RPCs the way the product does:
+
+* ``--mode direct``: clients -> llm.LLMService/GetSmartReply (5 recent
+  messages per request, the reference's contract);
+* ``--mode raft``: clients -> raft.RaftNode/GetSmartReply on the leader of a
+  3-node local cluster (token check, last-5 channel messages from the
+  replicated state, node -> LLM proxy), i.e. the CLI's ``smart_reply`` path.
+
+The LLM service runs in-process on the in-tree engine (``--backend engine``,
+one GPU, random-init weights) or the scripted backend (CPU plumbing).
+Reports one JSON line: requests/s, generated tokens/s, p50/p99 latency.
+
+  python scripts/service_bench.py --model llama-3-8b --requests 2048 --concurrency 512
+  python scripts/service_bench.py --backend scripted --mode raft --requests 200
+"""
+import argparse
+import json
+import os
+import random
+import statistics
+import sys
+import tempfile
+import threading
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import grpc  # noqa: E402
+
+from drtc_amd.llm.server import serve as serve_llm  # noqa: E402
+from drtc_amd.llm.service import FeatureParams  # noqa: E402
+from drtc_amd.protos import LLM_SERVICE, llm_pb, make_stub, raft_pb  # noqa: E402
+from drtc_amd.utils.cluster import LocalCluster, free_port  # noqa: E402
+from drtc_amd.utils.metrics import METRICS  # noqa: E402
+from drtc_amd.utils.synthetic import channel_history  # noqa: E402
+
+
+def build_backend(args):
+    if args.backend == "scripted":
+        from drtc_amd.llm.backends import ScriptedBackend
+        return ScriptedBackend(), None
+    import torch
+
+    from drtc_amd.engine import ChatTokenizer, LLMEngine
+    from drtc_amd.llm.backends import EngineBackend
+    from drtc_amd.models import TransformerLM, get_config
+
+    cfg = get_config(args.model)
+    dev = "cuda" if torch.cuda.is_available() else "cpu"
+    model = TransformerLM(cfg, dev, seed=1234, full_then_shard=False)
+    eng = LLMEngine(model, max_batch=args.max_batch, max_model_len=2048,
+                    use_graphs=dev == "cuda")
+    eng.warmup(capture=True)
+    return EngineBackend(eng, ChatTokenizer(cfg.vocab_size, cfg.bos_token_id,
+                                            cfg.eos_token_id)), eng
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--backend", choices=("engine", "scripted"), default="engine")
+    ap.add_argument("--model", default="llama-3-8b")
+    ap.add_argument("--mode", choices=("direct", "raft"), default="direct")
+    ap.add_argument("--requests", type=int, default=1024)
+    ap.add_argument("--concurrency", type=int, default=256)
+    ap.add_argument("--max-batch", type=int, default=512)
+    args = ap.parse_args()
+
+    backend, eng = build_backend(args)
+    fp = FeatureParams(ignore_eos=True)  # full 48-token budget per reply (random weights)
+    port = free_port()
+    llm_srv = serve_llm(backend, port=port, bind="127.0.0.1", params=fp,
+                        workers=args.concurrency + 8)
+    rng = random.Random(0)
+    cluster = None
+    tmp = tempfile.TemporaryDirectory()
+    try:
+        if args.mode == "raft":
+            cluster = LocalCluster(3, data_root=tmp.name, llm_address=f"127.0.0.1:{port}",
+                                   grpc_workers=args.concurrency + 16).start()
+            leader = cluster.leader()
+            token = cluster.login(leader)
+            st = cluster.stub(leader)
+            for m in channel_history(rng, 5):
+                st.SendMessage(raft_pb.SendMessageRequest(token=token, channel_id="general",
+                                                          content=m.content))
+
+            def one(stub):
+                r = stub.GetSmartReply(raft_pb.SmartReplyRequest(token=token, channel_id="general"),
+                                       timeout=120)
+                assert r.success and len(r.suggestions) == 3
+            stubs = [cluster.stub(leader) for _ in range(8)]
+        else:
+            histories = [[llm_pb.Message(sender=m.sender, content=m.content)
+                          for m in channel_history(rng, 5)] for _ in range(64)]
+
+            def one(stub):
+                r = stub.GetSmartReply(llm_pb.SmartReplyRequest(
+                    recent_messages=histories[rng.randrange(len(histories))]), timeout=120)
+                assert len(r.suggestions) == 3
+            stubs = [make_stub(grpc.insecure_channel(f"127.0.0.1:{port}"), LLM_SERVICE)
+                     for _ in range(8)]
+
+        # warm-up (graph buckets, first-use GEMM kernels)
+        ths = [threading.Thread(target=one, args=(stubs[i % 8],)) for i in range(16)]
+        [t.start() for t in ths]
+        [t.join() for t in ths]
+        if eng is not None:
+            eng.stats.clear()
+        lat, lock, it = [], threading.Lock(), iter(range(args.requests))
+
+        def worker(k):
+            stub = stubs[k % len(stubs)]
+            while True:
+                with lock:
+                    if next(it, None) is None:
+                        return
+                t = time.perf_counter()
+                one(stub)
+                with lock:
+                    lat.append(time.perf_counter() - t)
+        t0 = time.perf_counter()
+        ths = [threading.Thread(target=worker, args=(k,)) for k in range(args.concurrency)]
+        [t.start() for t in ths]
+        [t.join() for t in ths]
+        dt = time.perf_counter() - t0
+        lat.sort()
+        gen_tokens = (len(lat) * fp.smart.max_new_tokens) if eng is not None else 0
+        out = {
+            "metric": f"service smart-reply ({args.mode}) requests/s + latency",
+            "backend": args.backend, "model": args.model if eng else None,
+            "requests": len(lat), "concurrency": args.concurrency, "seconds": round(dt, 3),
+            "requests_per_s": round(len(lat) / dt, 2),
+            "gen_tokens_per_s": round(gen_tokens / dt, 1) if gen_tokens else None,
+            "p50_latency_ms": round(1000 * statistics.median(lat), 1),
+            "p99_latency_ms": round(1000 * lat[min(len(lat) - 1, int(0.99 * (len(lat) - 1)))], 1),
+            "engine_stats": dict(eng.stats) if eng else None,
+            "rpc_metrics": {k: v for k, v in METRICS.snapshot()["histograms"].items()
+                            if "SmartReply" in k or k.startswith("engine.")},
+        }
+        print(json.dumps(out), flush=True)
+    finally:
+        if cluster is not None:
+            cluster.stop()
+        llm_srv.stop(0)
+        if hasattr(backend, "close"):
+            backend.close()
+        tmp.cleanup()
+
+
+if __name__ == "__main__":
+    main()
