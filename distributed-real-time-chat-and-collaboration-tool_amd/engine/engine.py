@@ -18,6 +18,7 @@ token bookkeeping).
 from __future__ import annotations
 
 import collections
+import itertools
 import math
 import threading
 import time
@@ -143,7 +144,6 @@ class LLMEngine:
         M.set_gauge("engine.kv_used_frac", used / max(1, used + free))
         M.set_gauge("engine.running", len(self.running))
         M.set_gauge("engine.waiting", len(self.waiting))
-        return []
 
     # ------------------------------------------------------------ admission
     def _admit(self) -> list[Request]:
@@ -211,11 +211,15 @@ class LLMEngine:
     # ------------------------------------------------------------ prefill
     def _run_prefill(self, batch: list[Request]) -> list[Request]:
         dev = self.device
+        # host metadata, vectorised over the batch (a 1024-prompt prefill is
+        # ~150k tokens: per-request numpy calls would idle the GPU for ~50 ms)
         seqs = [r.all_ids for r in batch]
-        lens = [len(s) for s in seqs]
-        cu = [0]
-        for n in lens:
-            cu.append(cu[-1] + n)
+        nseq = len(batch)
+        lens_a = np.fromiter((len(x) for x in seqs), dtype=np.int64, count=nseq)
+        lens = lens_a.tolist()
+        cu_a = np.zeros(nseq + 1, dtype=np.int64)
+        np.cumsum(lens_a, out=cu_a[1:])
+        cu = cu_a.tolist()
         T = cu[-1]
         # pad the token count to a coarse bucket: hipBLASLt picks (and caches)
         # its kernels per GEMM shape, so stable shapes avoid re-heuristics and
@@ -223,29 +227,30 @@ class LLMEngine:
         # position 0 and slot -1 (no cache write) and are never attended.
         Tp = _pad_tokens(T)
         ids = np.zeros(Tp, dtype=np.int32)
-        ids[:T] = np.concatenate([np.asarray(s, dtype=np.int32) for s in seqs])
+        ids[:T] = np.fromiter(itertools.chain.from_iterable(seqs), dtype=np.int32, count=T)
+        seq_of = np.repeat(np.arange(nseq), lens_a)
+        p_tok = np.arange(T, dtype=np.int64) - np.repeat(cu_a[:-1], lens_a)
         pos = np.zeros(Tp, dtype=np.int32)
-        pos[:T] = np.concatenate([np.arange(n, dtype=np.int32) for n in lens])
+        pos[:T] = p_tok
+        nblk = -(-lens_a // BS)
+        blk_tab = np.zeros((nseq, int(nblk.max())), dtype=np.int64)
+        for i, r in enumerate(batch):
+            blk_tab[i, :nblk[i]] = r.blocks[:nblk[i]]
         slots = np.full(Tp, -1, dtype=np.int64)
-        seg_tok, seg_len, seg_blk = [], [], []
-        for r, a, n in zip(batch, cu[:-1], lens):
-            blk = np.asarray(r.blocks, dtype=np.int64)
-            p = np.arange(n)
-            slots[a:a + n] = blk[p // BS] * BS + p % BS
-            nb = -(-n // BS)
-            seg_tok.append(a + BS * np.arange(nb))
-            seg_len.append(np.minimum(BS, n - BS * np.arange(nb)))
-            seg_blk.append(blk[:nb])
-        seg_tok = np.concatenate(seg_tok).astype(np.int32)
-        seg_len = np.concatenate(seg_len).astype(np.int32)
-        seg_blk = np.concatenate(seg_blk).astype(np.int32)
+        slots[:T] = blk_tab[seq_of, p_tok // BS] * BS + p_tok % BS
+        # one V-write segment per (sequence, cache block)
+        s_seq = np.repeat(np.arange(nseq), nblk)
+        s_j = np.arange(int(nblk.sum()), dtype=np.int64) - np.repeat(np.cumsum(nblk) - nblk, nblk)
+        seg_tok = (cu_a[s_seq] + BS * s_j).astype(np.int32)
+        seg_len = np.minimum(BS, lens_a[s_seq] - BS * s_j).astype(np.int32)
+        seg_blk = blk_tab[s_seq, s_j].astype(np.int32)
         last_idx = np.asarray(cu[1:], dtype=np.int64) - 1
         ts, tq = ops.prefill_tiles(cu)
         t_i32 = torch.from_numpy(np.concatenate([ids, pos, np.asarray(cu, np.int32),
                                                  np.asarray(ts, np.int32), np.asarray(tq, np.int32),
                                                  seg_tok, seg_len, seg_blk])).to(dev, non_blocking=True)
         t_i64 = torch.from_numpy(np.concatenate([slots, last_idx])).to(dev, non_blocking=True)
-        nseq, nt, ns = len(batch), len(ts), len(seg_tok)
+        nt, ns = len(ts), len(seg_tok)
         o = 0
         d_ids = t_i32[o:o + Tp]; o += Tp
         d_pos = t_i32[o:o + Tp]; o += Tp
@@ -255,12 +260,12 @@ class LLMEngine:
         d_segs = (t_i32[o:o + ns], t_i32[o + ns:o + 2 * ns], t_i32[o + 2 * ns:o + 3 * ns])
         meta = PrefillMeta(positions=d_pos, slots=t_i64[:Tp], cu_seqlens=d_cu, cu_host=cu,
                            tiles=(d_ts, d_tq), last_idx=t_i64[Tp:], v_segs=d_segs)
-        logits = self.model.forward_prefill(d_ids, meta, self.kv)
         temp = torch.tensor([r.params.temperature for r in batch], dtype=torch.float32, device=dev)
         topk = torch.tensor([r.params.top_k for r in batch], dtype=torch.int32, device=dev)
         topp = torch.tensor([r.params.top_p for r in batch], dtype=torch.float32, device=dev)
         self._prefill_step += 1
         step = torch.tensor([self._prefill_step + (1 << 40)], dtype=torch.int64, device=dev)
+        logits = self.model.forward_prefill(d_ids, meta, self.kv)
         toks = ops.sample(logits, temp, topk, topp, seed=self.seed, step=step).cpu().numpy()
         self.stats["prefill_steps"] += 1
         self.stats["prefill_tokens"] += T

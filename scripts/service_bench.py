@@ -109,7 +109,7 @@ def main():
         [t.join() for t in ths]
         if eng is not None:
             eng.stats.clear()
-        lat, lock, it = [], threading.Lock(), iter(range(args.requests))
+        lat, errors, lock, it = [], [], threading.Lock(), iter(range(args.requests))
 
         def worker(k):
             stub = stubs[k % len(stubs)]
@@ -118,7 +118,12 @@ def main():
                     if next(it, None) is None:
                         return
                 t = time.perf_counter()
-                one(stub)
+                try:
+                    one(stub)
+                except (grpc.RpcError, AssertionError) as e:
+                    with lock:
+                        errors.append(repr(e)[:200])
+                    continue
                 with lock:
                     lat.append(time.perf_counter() - t)
         t0 = time.perf_counter()
@@ -131,7 +136,7 @@ def main():
         out = {
             "metric": f"service smart-reply ({args.mode}) requests/s + latency",
             "backend": args.backend, "model": args.model if eng else None,
-            "requests": len(lat), "concurrency": args.concurrency, "seconds": round(dt, 3),
+            "requests": len(lat), "errors": len(errors), "concurrency": args.concurrency, "seconds": round(dt, 3),
             "requests_per_s": round(len(lat) / dt, 2),
             "gen_tokens_per_s": round(gen_tokens / dt, 1) if gen_tokens else None,
             "p50_latency_ms": round(1000 * statistics.median(lat), 1),
@@ -144,7 +149,7 @@ def main():
     finally:
         if cluster is not None:
             cluster.stop()
-        llm_srv.stop(0)
+        llm_srv.stop(0).wait(10)
         if hasattr(backend, "close"):
             backend.close()
         tmp.cleanup()
@@ -152,3 +157,9 @@ def main():
 
 if __name__ == "__main__":
     main()
+    sys.stdout.flush()
+    sys.stderr.flush()
+    # grpc's C++ core and the engine's graph pools are torn down by the OS:
+    # interpreter finalisation with live grpc completion-queue threads can
+    # std::terminate after the results are out.
+    os._exit(0)
