@@ -51,7 +51,7 @@ DRTC_DEVICE void load_kv_block(KVRegs<D>& r, const bf16_t* kb, const bf16_t* vb,
 }
 
 template <int D>
-__global__ __launch_bounds__(256, 2) void paged_decode_kernel(
+__global__ __launch_bounds__(256, D >= 256 ? 1 : 2) void paged_decode_kernel(
     bf16_t* __restrict__ out, float* __restrict__ part_o,
     float* __restrict__ part_ml, const bf16_t* __restrict__ q, int q_stride,
     const bf16_t* __restrict__ k_cache, const bf16_t* __restrict__ v_cache,
@@ -202,6 +202,156 @@ __global__ __launch_bounds__(256, 2) void paged_decode_kernel(
   }
 }
 
+// Variant 2: one WAVE per (sequence, kv head, partition) work item, four
+// independent items per workgroup, no cross-wave merge (no LDS, no barrier).
+// Short chat contexts (~6 cache blocks) make variant 1's per-workgroup fixed
+// costs - the 4-way LDS merge and the barrier that waits for the slowest
+// wave - a large share of each workgroup's life; here every wave streams its
+// item's blocks back to back (register double buffer), with the partition's
+// block-table slice preloaded into one VGPR (lane j = block j, readlane per
+// block) so the K/V loads of block j+1 never wait on a block-table load.
+template <int D>
+__global__ __launch_bounds__(256, D >= 256 ? 1 : 2) void paged_decode_wave_kernel(
+    bf16_t* __restrict__ out, float* __restrict__ part_o,
+    float* __restrict__ part_ml, const bf16_t* __restrict__ q, int q_stride,
+    const bf16_t* __restrict__ k_cache, const bf16_t* __restrict__ v_cache,
+    const int* __restrict__ block_tables, int bt_stride,
+    const int* __restrict__ context_lens, int B, int Hq, int Hkv, float scale_log2e,
+    int max_parts, int blocks_per_part) {
+  constexpr int NT = D / 16;
+  constexpr int KS = D / 32;
+  const int lane = threadIdx.x & 63;
+  const int item = blockIdx.x * 4 + wave_id_uniform();
+  const int BH = B * Hkv;
+  if (item >= BH * max_parts) return;
+  const int p = item / BH;  // partition slowest: idle items cluster in late workgroups
+  const int bh = item - p * BH;
+  const int b = bh / Hkv;
+  const int h = bh - b * Hkv;
+  const int G = Hq / Hkv;
+  const int col = lane & 15, g = lane >> 4;
+  const int ctx = context_lens[b];
+  if (ctx <= 0) {  // padded batch slot: deterministic zeros, no cache reads
+    if (p == 0) {
+      bf16x8 z;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) z[j] = f2bf(0.f);
+      for (int i = lane; i < G * D / 8; i += 64)
+        store_bf16x8(out + ((int64_t)b * Hq + h * G) * D + 8 * i, z);
+    }
+    return;
+  }
+  const int nblk = (ctx + kBS - 1) / kBS;
+  const int nparts = (nblk + blocks_per_part - 1) / blocks_per_part;
+  if (p >= nparts) return;
+  const int blk_begin = p * blocks_per_part;
+  const int blk_end = min(nblk, blk_begin + blocks_per_part);
+
+  bf16x8 qf[KS];
+  const bf16_t* qrow = q + (int64_t)b * q_stride + (int64_t)(h * G + col) * D;
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    if (col < G) qf[s] = load_bf16x8(qrow + 32 * s + 8 * g);
+    else for (int j = 0; j < 8; ++j) qf[s][j] = f2bf(0.f);
+  }
+  const int* bt = block_tables + (int64_t)b * bt_stride;
+  int chunk = blk_begin;  // block-table slice [chunk, chunk + 64) held in bt_reg
+  int bt_reg = (chunk + lane < blk_end) ? bt[chunk + lane] : 0;
+  auto phys_of = [&](int j) -> int64_t {
+    if (j - chunk >= 64) {
+      chunk += 64;
+      bt_reg = (chunk + lane < blk_end) ? bt[chunk + lane] : 0;
+    }
+    return (int64_t)__builtin_amdgcn_readlane(bt_reg, j - chunk);
+  };
+
+  f32x4 o[NT];
+#pragma unroll
+  for (int i = 0; i < NT; ++i) o[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  float m = kNegBig, lsum = 0.f;
+  const int64_t blk_elems = (int64_t)kBS * D;
+  KVRegs<D> cur, nxt;
+  {
+    const int64_t ph = phys_of(blk_begin);
+    load_kv_block<D>(cur, k_cache + (ph * Hkv + h) * blk_elems,
+                     v_cache + (ph * Hkv + h) * blk_elems, lane);
+  }
+  for (int blk = blk_begin; blk < blk_end; ++blk) {
+    const bool more = blk + 1 < blk_end;
+    if (more) {
+      const int64_t ph = phys_of(blk + 1);
+      load_kv_block<D>(nxt, k_cache + (ph * Hkv + h) * blk_elems,
+                       v_cache + (ph * Hkv + h) * blk_elems, lane);
+    }
+    f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      s0 = mfma16(cur.k0[s], qf[s], s0);
+      s1 = mfma16(cur.k1[s], qf[s], s1);
+    }
+    const int tok0 = blk * kBS + 4 * g;
+    float bmax = kNegBig;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      s0[r] = (tok0 + r < ctx) ? s0[r] * scale_log2e : kNegBig;
+      s1[r] = (tok0 + 16 + r < ctx) ? s1[r] * scale_log2e : kNegBig;
+      bmax = fmaxf(bmax, fmaxf(s0[r], s1[r]));
+    }
+    bmax = fmaxf(bmax, __shfl_xor(bmax, 16, 64));
+    bmax = fmaxf(bmax, __shfl_xor(bmax, 32, 64));
+    const float m_new = fmaxf(m, bmax);
+    const float alpha = fast_exp2(m - m_new);
+    m = m_new;
+    bf16x8 pf;
+    float psum = 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float p0 = fast_exp2(s0[r] - m_new);
+      const float p1 = fast_exp2(s1[r] - m_new);
+      psum += p0 + p1;
+      pf[r] = f2bf(p0);
+      pf[4 + r] = f2bf(p1);
+    }
+    lsum = lsum * alpha + psum;
+#pragma unroll
+    for (int i = 0; i < NT; ++i) {
+      o[i] *= alpha;
+      bf16x8 a;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        a[j] = cur.vlo[i][j];
+        a[4 + j] = cur.vhi[i][j];
+      }
+      o[i] = mfma16(a, pf, o[i]);
+    }
+    if (more) cur = nxt;
+  }
+  lsum += __shfl_xor(lsum, 16, 64);
+  lsum += __shfl_xor(lsum, 32, 64);
+  if (col >= G) return;
+  const int hq = h * G + col;
+  if (nparts == 1) {
+    const float inv = 1.f / lsum;
+    bf16_t* orow = out + ((int64_t)b * Hq + hq) * D + 4 * g;
+#pragma unroll
+    for (int i = 0; i < NT; ++i) {
+      bf16x4 v;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = f2bf(o[i][r] * inv);
+      *reinterpret_cast<bf16x4*>(orow + 16 * i) = v;
+    }
+  } else {
+    const int64_t pi = ((int64_t)b * Hq + hq) * max_parts + p;
+    float* po = part_o + pi * D + 4 * g;
+#pragma unroll
+    for (int i = 0; i < NT; ++i) *reinterpret_cast<f32x4*>(po + 16 * i) = o[i];
+    if (g == 0) {
+      part_ml[pi * 2 + 0] = m;
+      part_ml[pi * 2 + 1] = lsum;
+    }
+  }
+}
+
 // Merge the per-partition partials of sequences that span > 1 partition.
 __global__ __launch_bounds__(256) void decode_reduce_kernel(
     bf16_t* __restrict__ out, const float* __restrict__ part_o,
@@ -231,12 +381,34 @@ int launch_paged_decode(void* out, float* part_o, float* part_ml, const void* q,
                         int q_stride, const void* k_cache, const void* v_cache,
                         const int* block_tables, int bt_stride,
                         const int* context_lens, int B, int Hq, int Hkv, int D,
-                        float scale, int max_parts, int blocks_per_part,
+                        float scale, int max_parts, int blocks_per_part, int variant,
                         hipStream_t st) {
   if (B == 0) return 0;
   if (Hkv <= 0 || Hq % Hkv != 0 || Hq / Hkv > 16) return -1;
   if (max_parts > 1 && (!part_o || !part_ml)) return -2;
   const float sl2 = scale * kLog2e;
+  if (variant == 2) {
+    const dim3 wgrid((B * Hkv * max_parts + 3) / 4), wblock(256);
+    switch (D) {
+      case 64:
+        hipLaunchKernelGGL(paged_decode_wave_kernel<64>, wgrid, wblock, 0, st, (bf16_t*)out, part_o, part_ml, (const bf16_t*)q, q_stride, (const bf16_t*)k_cache, (const bf16_t*)v_cache, block_tables, bt_stride, context_lens, B, Hq, Hkv, sl2, max_parts, blocks_per_part);
+        break;
+      case 128:
+        hipLaunchKernelGGL(paged_decode_wave_kernel<128>, wgrid, wblock, 0, st, (bf16_t*)out, part_o, part_ml, (const bf16_t*)q, q_stride, (const bf16_t*)k_cache, (const bf16_t*)v_cache, block_tables, bt_stride, context_lens, B, Hq, Hkv, sl2, max_parts, blocks_per_part);
+        break;
+      case 256:
+        hipLaunchKernelGGL(paged_decode_wave_kernel<256>, wgrid, wblock, 0, st, (bf16_t*)out, part_o, part_ml, (const bf16_t*)q, q_stride, (const bf16_t*)k_cache, (const bf16_t*)v_cache, block_tables, bt_stride, context_lens, B, Hq, Hkv, sl2, max_parts, blocks_per_part);
+        break;
+      default:
+        return -1;
+    }
+    if (max_parts > 1)
+      hipLaunchKernelGGL(decode_reduce_kernel, dim3(B * Hq), dim3(256), 0, st,
+                         (bf16_t*)out, (const float*)part_o, (const float*)part_ml,
+                         context_lens, Hq, D, max_parts, blocks_per_part);
+    return (int)hipGetLastError();
+  }
+  if (variant != 1) return -3;
   dim3 grid(B * Hkv, max_parts), block(256);
   const size_t lds = (128 + 4 * (size_t)D * 16) * sizeof(float);
   switch (D) {

@@ -28,7 +28,7 @@ int launch_paged_decode(void* out, float* part_o, float* part_ml, const void* q,
                         int q_stride, const void* k_cache, const void* v_cache,
                         const int* block_tables, int bt_stride,
                         const int* context_lens, int B, int Hq, int Hkv, int D,
-                        float scale, int max_parts, int blocks_per_part,
+                        float scale, int max_parts, int blocks_per_part, int variant,
                         hipStream_t st);
 
 int launch_prefill_attn(void* out, int out_stride, const void* qkv,

@@ -5,6 +5,7 @@ HIP kernels: csrc/kernels/attention_prefill.hip, csrc/kernels/attention_decode.h
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 
@@ -88,13 +89,26 @@ def prefill_attention(qkv: torch.Tensor, cu_seqlens: torch.Tensor, Hq: int, Hkv:
 
 
 # ------------------------------------------------------------------ decode
-def decode_partitioning(batch: int, Hkv: int, max_blocks: int, target_wgs: int = 2048):
+# Decode kernel variant: 1 = workgroup per (seq, kv head, partition) with a
+# 4-wave LDS merge (default); 2 = one wave per (seq, kv head, partition), no
+# merge.  Measured on MI355X (scripts/decode_attn_bench.py, Llama-3-8B heads):
+# equal at batch 1024 (4.8 TB/s), v1 ahead at long contexts.
+DECODE_VARIANT = int(os.environ.get("DRTC_DECODE_VARIANT", "1"))
+
+
+def decode_partitioning(batch: int, Hkv: int, max_blocks: int, target_wgs: int = 256,
+                        variant: int | None = None):
     """Static (graph-capturable) split of the context into partitions.
 
-    Returns (blocks_per_part, max_parts): enough partitions to put roughly
-    ``target_wgs`` workgroups on the 256 CUs when the batch alone cannot."""
-    parts_wanted = max(1, math.ceil(target_wgs / max(1, batch * Hkv)))
-    bpp = max(4, math.ceil(max_blocks / parts_wanted))
+    Returns (blocks_per_part, max_parts).  Split-K only pays when the batch
+    cannot fill the chip by itself: the sweep in profiles/ shows one partition
+    per sequence winning from 512 (seq, kv head) workgroups up (e.g. batch 64 x
+    8 kv heads: 84 us unsplit vs 96 us in 4 parts at ~1.7k-token contexts), and
+    partitions shorter than ~8 blocks losing to the merge overhead (batch 8 at
+    4k tokens: 28 us with 32-block parts vs 40 us with 4-block parts)."""
+    per_wg = 4 if (variant or DECODE_VARIANT) == 2 else 1
+    parts_wanted = max(1, math.ceil(target_wgs * per_wg / max(1, batch * Hkv)))
+    bpp = max(8, math.ceil(max_blocks / parts_wanted))
     bpp = ((bpp + 3) // 4) * 4
     max_parts = max(1, math.ceil(max_blocks / bpp))
     return bpp, max_parts
@@ -136,7 +150,8 @@ def paged_decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torc
                            block_tables: torch.Tensor, context_lens: torch.Tensor,
                            scale: float, out: torch.Tensor | None = None,
                            blocks_per_part: int | None = None,
-                           workspace: DecodeWorkspace | None = None) -> torch.Tensor:
+                           workspace: DecodeWorkspace | None = None,
+                           variant: int | None = None) -> torch.Tensor:
     """One query token per sequence against the paged cache.
 
     q: [B, Hq, D] view (row stride may exceed Hq*D, e.g. the fused QKV row);
@@ -156,8 +171,9 @@ def paged_decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torc
     assert block_tables.dtype == torch.int32 and block_tables.stride(1) == 1
     assert context_lens.dtype == torch.int32 and context_lens.numel() >= B
     max_blocks = block_tables.shape[1]
+    variant = variant or DECODE_VARIANT
     if blocks_per_part is None or workspace is None:
-        blocks_per_part, max_parts = decode_partitioning(B, Hkv, max_blocks)
+        blocks_per_part, max_parts = decode_partitioning(B, Hkv, max_blocks, variant=variant)
         workspace = DecodeWorkspace(B, Hq, D, max_parts, q.device)
     if out is None:
         out = torch.empty((B, Hq, D), dtype=q.dtype, device=q.device)
@@ -166,6 +182,6 @@ def paged_decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torc
                               q.data_ptr(), q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
                               block_tables.data_ptr(), block_tables.stride(0),
                               context_lens.data_ptr(), B, Hq, Hkv, D, float(scale),
-                              workspace.max_parts, blocks_per_part, stream_ptr(q)),
+                              workspace.max_parts, blocks_per_part, variant, stream_ptr(q)),
           "paged_decode")
     return out

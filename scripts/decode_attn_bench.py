@@ -1,0 +1,80 @@
+#!/usr/bin/env python3
+"""Paged decode attention micro-benchmark: kernel variant 1 (workgroup per
+(seq, kv head) + LDS merge) vs 2 (wave per (seq, kv head)), Llama-3-8B
+geometry (Hq 32, Hkv 8, D 128) over several batch / context mixes.
+Reports us per call and effective HBM GB/s of K+V bytes read."""
+import math
+import random
+import sys
+
+import torch
+
+sys.path.insert(0, ".")
+from drtc_amd import ops  # noqa: E402
+
+
+def setup(B, ctxs, Hq=32, Hkv=8, D=128, seed=0):
+    bs = ops.KV_BLOCK
+    maxb = max(math.ceil(c / bs) for c in ctxs)
+    nb = sum(math.ceil(c / bs) for c in ctxs) + 1
+    kc = torch.randn(nb, Hkv, bs, D, device="cuda", dtype=torch.bfloat16)
+    vc = torch.randn(nb, Hkv, D, bs, device="cuda", dtype=torch.bfloat16)
+    perm = torch.randperm(nb - 1) + 1
+    bt = torch.zeros(B, maxb, dtype=torch.int32)
+    k = 0
+    for b, c in enumerate(ctxs):
+        n = math.ceil(c / bs)
+        bt[b, :n] = perm[k:k + n].to(torch.int32)
+        k += n
+    q = torch.randn(B, Hq, D, device="cuda", dtype=torch.bfloat16)
+    return q, kc, vc, bt.cuda(), torch.tensor(ctxs, dtype=torch.int32, device="cuda")
+
+
+def timeit(fn, iters=50):
+    for _ in range(5):
+        fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) * 1000 / iters
+
+
+def main():
+    rng = random.Random(0)
+    cases = [("B1024 ctx150-200", 1024, lambda: rng.randint(150, 200)),
+             ("B512 ctx150-200", 512, lambda: rng.randint(150, 200)),
+             ("B256 ctx600-1400", 256, lambda: rng.randint(600, 1400)),
+             ("B64 ctx1500-2000", 64, lambda: rng.randint(1500, 2000)),
+             ("B8 ctx4000", 8, lambda: 4000)]
+    for name, B, gen in cases:
+        ctxs = [gen() for _ in range(B)]
+        q, kc, vc, bt, cl = setup(B, ctxs)
+        kv_bytes = sum(ctxs) * 8 * 128 * 2 * 2
+        res = []
+        outs = []
+        maxb = bt.shape[1]
+        for v in (1, 2):
+            bpp0, _ = ops.decode_partitioning(B, 8, maxb, variant=v)
+            sweep = sorted({bpp0} | {max(4, -(-maxb // n)) for n in (1, 2, 4, 8, 16)})
+            for bpp in sweep:
+                mp = -(-maxb // bpp)
+                ws = ops.DecodeWorkspace(B, 32, 128, mp, "cuda")
+                out = torch.empty(B, 32, 128, device="cuda", dtype=torch.bfloat16)
+                us = timeit(lambda: ops.paged_decode_attention(
+                    q, kc, vc, bt, cl, 128 ** -0.5, out=out, blocks_per_part=bpp, workspace=ws,
+                    variant=v))
+                outs.append(out.float())
+                tag = "*" if bpp == bpp0 else " "
+                res.append(f"v{v}{tag}bpp{bpp:3d}/p{mp:2d} {us:7.1f}us {kv_bytes / us / 1e3:5.0f}GB/s")
+        diff = max((o - outs[0]).abs().max().item() for o in outs)
+        print(f"{name} (max diff {diff:.3g}; * = heuristic)", flush=True)
+        for r in res:
+            print("    " + r, flush=True)
+
+
+if __name__ == "__main__":
+    main()

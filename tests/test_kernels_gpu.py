@@ -112,20 +112,35 @@ def _paged_setup(B, Hq, Hkv, D, ctx_lens, nb_total=None, seed=0):
 @pytest.mark.parametrize("D,Hq,Hkv", [(128, 32, 8), (128, 64, 8), (256, 8, 1), (64, 4, 2),
                                       (128, 16, 16)])
 @pytest.mark.parametrize("ctx_lens", [[1, 31, 32, 33, 100, 257], [513, 1000, 2048], [5]])
-def test_paged_decode(hipk, D, Hq, Hkv, ctx_lens):
+@pytest.mark.parametrize("variant", [1, 2])
+def test_paged_decode(hipk, D, Hq, Hkv, ctx_lens, variant):
     B = len(ctx_lens)
     q, kc, vc, bt, cl = _paged_setup(B, Hq, Hkv, D, ctx_lens)
     scale = D ** -0.5
     ref = ops.paged_decode_ref(q, kc, vc, bt, cl, scale)
-    out = ops.paged_decode_attention(q, kc, vc, bt, cl, scale)
+    out = ops.paged_decode_attention(q, kc, vc, bt, cl, scale, variant=variant)
     _close(out, ref, 2e-2, 2e-2, "decode")
     # force a multi-partition split-K
     ws = ops.DecodeWorkspace(B, Hq, D, math.ceil(bt.shape[1] / 4), DEV)
-    out2 = ops.paged_decode_attention(q, kc, vc, bt, cl, scale, blocks_per_part=4, workspace=ws)
+    out2 = ops.paged_decode_attention(q, kc, vc, bt, cl, scale, blocks_per_part=4, workspace=ws,
+                                      variant=variant)
     _close(out2, ref, 2e-2, 2e-2, "decode split")
 
 
-def test_paged_decode_strided_q_and_padding(hipk):
+def test_paged_decode_wave_long_partition(hipk):
+    """Variant 2 with a partition longer than 64 blocks (block-table slice reload)."""
+    Hq, Hkv, D = 32, 8, 128
+    ctx = [4100, 2049, 70]
+    q, kc, vc, bt, cl = _paged_setup(3, Hq, Hkv, D, ctx)
+    ref = ops.paged_decode_ref(q, kc, vc, bt, cl, D ** -0.5)
+    ws = ops.DecodeWorkspace(3, Hq, D, 1, DEV)
+    out = ops.paged_decode_attention(q, kc, vc, bt, cl, D ** -0.5, blocks_per_part=bt.shape[1],
+                                     workspace=ws, variant=2)
+    _close(out, ref, 2e-2, 2e-2, "long partition")
+
+
+@pytest.mark.parametrize("variant", [1, 2])
+def test_paged_decode_strided_q_and_padding(hipk, variant):
     Hq, Hkv, D = 32, 8, 128
     ctx = [40, 0, 77]
     q, kc, vc, bt, cl = _paged_setup(3, Hq, Hkv, D, [40, 1, 77])
@@ -133,20 +148,21 @@ def test_paged_decode_strided_q_and_padding(hipk):
     big = torch.zeros(3, (Hq + 2 * Hkv) * D, device=DEV, dtype=torch.bfloat16)
     big[:, :Hq * D] = q.reshape(3, -1)
     qv = big.as_strided((3, Hq, D), (big.stride(0), D, 1))
-    out = ops.paged_decode_attention(qv, kc, vc, bt, cl, D ** -0.5)
+    out = ops.paged_decode_attention(qv, kc, vc, bt, cl, D ** -0.5, variant=variant)
     ref = ops.paged_decode_ref(q, kc, vc, bt, cl, D ** -0.5)
     _close(out, ref, 2e-2, 2e-2)
     assert out[1].abs().max().item() == 0.0
     assert ctx
 
 
-def test_paged_decode_spike(hipk):
+@pytest.mark.parametrize("variant", [1, 2])
+def test_paged_decode_spike(hipk, variant):
     """One key dominating forces the online-softmax rescale branch."""
     Hq, Hkv, D = 8, 2, 128
     q, kc, vc, bt, cl = _paged_setup(2, Hq, Hkv, D, [300, 700])
     kc[bt[0, 5].long(), :, 7, :] = q[0, 0].float().sign().to(torch.bfloat16) * 4
     ref = ops.paged_decode_ref(q, kc, vc, bt, cl, D ** -0.5)
-    out = ops.paged_decode_attention(q, kc, vc, bt, cl, D ** -0.5)
+    out = ops.paged_decode_attention(q, kc, vc, bt, cl, D ** -0.5, variant=variant)
     _close(out, ref, 2e-2, 2e-2)
 
 
