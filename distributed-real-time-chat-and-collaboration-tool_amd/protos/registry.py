@@ -137,15 +137,17 @@ def _service(ns, spec, sname) -> Service:
     return Service(f"{spec['package']}.{sname}", ms)
 
 
-_MAIN_POOL, _ = _pool_with([schema.RAFT, schema.LLM, schema.CHAT])
+_MAIN_POOL, _ = _pool_with([schema.RAFT, schema.RAFT_SNAPSHOT, schema.LLM, schema.CHAT])
 _TOY_POOL, _ = _pool_with([schema.CHAT_TOY])
 
 raft_pb = _namespace(_MAIN_POOL, schema.RAFT)
+raft_snap_pb = _namespace(_MAIN_POOL, schema.RAFT_SNAPSHOT)
 llm_pb = _namespace(_MAIN_POOL, schema.LLM)
 chat_pb = _namespace(_MAIN_POOL, schema.CHAT)
 chat_toy_pb = _namespace(_TOY_POOL, schema.CHAT_TOY)
 
 RAFT_SERVICE = _service(raft_pb, schema.RAFT, "RaftNode")
+RAFT_SNAPSHOT_SERVICE = _service(raft_snap_pb, schema.RAFT_SNAPSHOT, "RaftSnapshot")
 LLM_SERVICE = _service(llm_pb, schema.LLM, "LLMService")
 CHAT_SERVICE = _service(chat_pb, schema.CHAT, "ChatService")
 CHAT_TOY_SERVICE = _service(chat_toy_pb, schema.CHAT_TOY, "ChatService")

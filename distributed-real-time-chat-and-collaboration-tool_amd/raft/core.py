@@ -20,7 +20,13 @@ Behaviour vs the reference (server/raft_node.py:469-1194):
     ``RaftConfig.local_commit``;
   * AppendEntries batches are bounded in bytes (quirk Q12) and rejected
     followers are probed with exponential back-off instead of one entry
-    per round trip.
+    per round trip;
+  * log compaction (the reference has none, SURVEY §5 "Checkpoint"): the
+    runtime snapshots the state machine at an applied index and calls
+    ``compact``; entries up to it leave the log (``snap_index`` /
+    ``snap_term`` remember the boundary).  A follower whose next entry was
+    compacted away is sent the snapshot (``InstallSnapshot``, Raft §7)
+    instead of entries.
 """
 from __future__ import annotations
 
@@ -73,6 +79,21 @@ class AppendResp:
 
 
 @dataclass
+class SnapshotReq:
+    term: int
+    leader_id: int
+    last_index: int
+    last_term: int
+    data: bytes = b""   # filled in by the transport from the latest snapshot
+
+
+@dataclass
+class SnapshotResp:
+    term: int
+    success: bool
+
+
+@dataclass
 class RaftConfig:
     election_timeout: tuple = (1.5, 3.0)     # reference: (10.0, 15.0)
     heartbeat_interval: float = 0.05         # reference: 0.05 (raft_node.py:2356)
@@ -100,11 +121,16 @@ class _Inflight:
 
 
 class MemoryStorage:
-    """Volatile storage (tests); durable ones live in raft/storage.py."""
+    """Volatile storage (tests); durable ones live in raft/storage.py.
+
+    ``entries`` hold absolute indices ``snap_index + 1 ...``; ``snapshot`` is
+    the last installed/compacted state-machine image."""
 
     def __init__(self):
         self.entries: list[Entry] = []
-        self.state = {"current_term": 0, "voted_for": None, "commit_index": -1, "last_applied": -1}
+        self.state = {"current_term": 0, "voted_for": None, "commit_index": -1, "last_applied": -1,
+                      "snap_index": -1, "snap_term": 0}
+        self.snapshot: bytes | None = None
 
     def load(self):
         return self.state, self.entries
@@ -113,10 +139,26 @@ class MemoryStorage:
         self.entries.extend(entries)
 
     def truncate_from(self, index: int) -> None:
-        del self.entries[index:]
+        del self.entries[index - self.state["snap_index"] - 1:]
+
+    def compact(self, index: int, term: int, data: bytes | None = None) -> None:
+        del self.entries[:index - self.state["snap_index"]]
+        self.state["snap_index"], self.state["snap_term"] = index, term
+        if data is not None:
+            self.snapshot = data
+
+    def install_snapshot(self, index: int, term: int, data: bytes, keep: list[Entry]) -> None:
+        self.entries = list(keep)
+        self.state["snap_index"], self.state["snap_term"] = index, term
+        self.snapshot = data
+
+    def latest_snapshot(self):
+        if self.snapshot is None:
+            return None
+        return self.state["snap_index"], self.state["snap_term"], self.snapshot
 
     def save_state(self, state: dict) -> None:
-        self.state = dict(state)
+        self.state.update(state)
 
     def flush(self) -> None:
         pass
@@ -124,21 +166,28 @@ class MemoryStorage:
 
 class RaftCore:
     def __init__(self, node_id: int, peers, storage=None, apply_fn=None,
-                 config: RaftConfig | None = None, seed: int | None = None, now: float = 0.0):
+                 config: RaftConfig | None = None, seed: int | None = None, now: float = 0.0,
+                 restore_fn=None):
         self.id = node_id
         self.peers = sorted(int(p) for p in peers)
         self.cfg = config or RaftConfig()
         self.storage = storage if storage is not None else MemoryStorage()
         self.apply_fn = apply_fn or (lambda index, entry: None)
+        # restore_fn(data): replace the state machine with a snapshot image
+        self.restore_fn = restore_fn or (lambda data: None)
         self.rng = random.Random(seed if seed is not None else node_id * 7919 + 17)
         st, entries = self.storage.load()
-        self.log: list[Entry] = list(entries)
+        self.snap_index = int(st.get("snap_index", -1))
+        self.snap_term = int(st.get("snap_term", 0))
+        self.log: list[Entry] = list(entries)  # absolute indices snap_index+1 ...
         self.term = int(st.get("current_term", 0))
         self.voted_for = st.get("voted_for")
-        self.commit_index = min(int(st.get("commit_index", -1)), len(self.log) - 1)
+        self.commit_index = max(self.snap_index,
+                                min(int(st.get("commit_index", -1)), self.last_index))
         # the state machine is rebuilt by the runtime (snapshot + replay), so
         # apply restarts from the persisted last_applied
-        self.last_applied = min(int(st.get("last_applied", -1)), self.commit_index)
+        self.last_applied = max(self.snap_index,
+                                min(int(st.get("last_applied", -1)), self.commit_index))
         self.role = Role.FOLLOWER
         self.leader_id: int | None = None
         self.votes: set[int] = set()
@@ -160,10 +209,22 @@ class RaftCore:
 
     @property
     def last_index(self) -> int:
-        return len(self.log) - 1
+        return self.snap_index + len(self.log)
+
+    @property
+    def first_index(self) -> int:
+        """Oldest index still held as an entry."""
+        return self.snap_index + 1
+
+    def entry(self, i: int) -> Entry:
+        return self.log[i - self.snap_index - 1]
 
     def term_at(self, i: int) -> int:
-        return self.log[i].term if 0 <= i < len(self.log) else 0
+        if i == self.snap_index:
+            return self.snap_term
+        if self.snap_index < i <= self.last_index:
+            return self.log[i - self.snap_index - 1].term
+        return 0
 
     def _timeout(self) -> float:
         a, b = self.cfg.election_timeout
@@ -172,7 +233,8 @@ class RaftCore:
     def _persist(self) -> None:
         self.storage.save_state({"current_term": self.term, "voted_for": self.voted_for,
                                  "commit_index": self.commit_index,
-                                 "last_applied": self.last_applied})
+                                 "last_applied": self.last_applied,
+                                 "snap_index": self.snap_index, "snap_term": self.snap_term})
 
     def _become_follower(self, term: int, leader: int | None = None) -> None:
         changed = term != self.term
@@ -231,7 +293,7 @@ class RaftCore:
         self.leader_id = self.id
         self.inflight.clear()
         for p in self.peers:
-            self.next_index[p] = len(self.log)
+            self.next_index[p] = self.last_index + 1
             self.match_index[p] = -1
             self.backoff[p] = 1
             self.last_sent[p] = -1e9
@@ -278,11 +340,17 @@ class RaftCore:
         return self.last_index
 
     def _send_append(self, p: int) -> None:
-        ni = min(self.next_index.get(p, len(self.log)), len(self.log))
+        ni = min(self.next_index.get(p, self.last_index + 1), self.last_index + 1)
+        if ni <= self.snap_index:  # the entries it needs are compacted away
+            req = SnapshotReq(self.term, self.id, self.snap_index, self.snap_term)
+            self.inflight[p] = _Inflight(self.now, self.snap_index, 0, self.term)
+            self.last_sent[p] = self.now
+            self.outbox.append((p, "snapshot", req))
+            return
         prev = ni - 1
         batch, size = [], 0
-        for i in range(ni, len(self.log)):
-            e = self.log[i]
+        for i in range(ni, self.last_index + 1):
+            e = self.entry(i)
             sz = len(e.data) + len(e.command) + 16
             if batch and (size + sz > self.cfg.max_batch_bytes or len(batch) >= self.cfg.max_batch_entries):
                 break
@@ -301,28 +369,94 @@ class RaftCore:
         self.leader_id = req.leader_id
         self.election_deadline = self.now + self._timeout()
         prev = req.prev_log_index
-        if prev >= 0 and (prev >= len(self.log) or self.log[prev].term != req.prev_log_term):
+        new = list(req.entries)
+        if prev < self.snap_index:
+            # the prefix up to snap_index is committed (hence identical on
+            # every node): drop the part of the batch the snapshot covers
+            skip = self.snap_index - prev
+            if skip >= len(new):
+                return AppendResp(self.term, True)  # everything sent is in the snapshot
+            new = new[skip:]
+            prev = self.snap_index
+        elif prev >= 0 and (prev > self.last_index or self.term_at(prev) != req.prev_log_term):
             return AppendResp(self.term, False)
         # §5.3: skip entries already present, truncate only at a conflict
         idx = prev + 1
-        new = list(req.entries)
         k = 0
-        while k < len(new) and idx + k < len(self.log):
-            if self.log[idx + k].term != new[k].term:
+        while k < len(new) and idx + k <= self.last_index:
+            if self.term_at(idx + k) != new[k].term:
                 if idx + k <= self.commit_index and not self.cfg.local_commit:
                     # never happens under Raft's safety rules; with the
                     # reference's leader-local commit it can (quirk Q1)
                     raise AssertionError("leader tried to overwrite a committed entry")
-                del self.log[idx + k:]
+                del self.log[idx + k - self.snap_index - 1:]
                 self.storage.truncate_from(idx + k)
                 break
             k += 1
         if k < len(new):
             self._append_local(new[k:])
         if req.leader_commit > self.commit_index:
-            self.commit_index = min(req.leader_commit, prev + len(new))
+            self.commit_index = max(self.commit_index, min(req.leader_commit, prev + len(new)))
             self._apply()
         return AppendResp(self.term, True)
+
+    # ------------------------------------------------------------ snapshots
+    def on_install_snapshot(self, req: SnapshotReq) -> SnapshotResp:
+        """Raft §7 InstallSnapshot (whole image; the transport reassembles
+        chunks before calling this)."""
+        if req.term < self.term:
+            return SnapshotResp(self.term, False)
+        if req.term > self.term or self.role != Role.FOLLOWER:
+            self._become_follower(req.term, req.leader_id)
+        self.leader_id = req.leader_id
+        self.election_deadline = self.now + self._timeout()
+        if req.last_index <= self.commit_index:  # already have everything it covers
+            return SnapshotResp(self.term, True)
+        keep: list[Entry] = []
+        if self.snap_index < req.last_index <= self.last_index and \
+                self.term_at(req.last_index) == req.last_term:
+            keep = self.log[req.last_index - self.snap_index:]  # retain the matching suffix
+        self.log = list(keep)
+        self.snap_index, self.snap_term = req.last_index, req.last_term
+        self.storage.install_snapshot(req.last_index, req.last_term, req.data, keep)
+        self.restore_fn(req.data)
+        self.commit_index = max(self.commit_index, req.last_index)
+        self.last_applied = req.last_index
+        self._persist()
+        for cb in self.commit_listeners:
+            cb(self.last_applied)
+        return SnapshotResp(self.term, True)
+
+    def on_snapshot_reply(self, peer: int, req: SnapshotReq, resp: SnapshotResp | None) -> None:
+        inf = self.inflight.get(peer)
+        if inf is not None and inf.prev_index == req.last_index and inf.term == req.term:
+            del self.inflight[peer]
+        if resp is None:
+            return
+        if resp.term > self.term:
+            self._become_follower(resp.term)
+            self.election_deadline = self.now + self._timeout()
+            return
+        if self.role != Role.LEADER or req.term != self.term or not resp.success:
+            return
+        self.match_index[peer] = max(self.match_index.get(peer, -1), req.last_index)
+        self.next_index[peer] = max(self.next_index.get(peer, 0), req.last_index + 1)
+        self.backoff[peer] = 1
+        self._advance_commit()
+        if self.next_index[peer] <= self.last_index:
+            self._send_append(peer)
+
+    def compact(self, index: int, data: bytes | None = None) -> bool:
+        """Drop entries up to ``index`` (<= last_applied) after the runtime has
+        durably saved a state-machine snapshot taken at ``index``."""
+        if index <= self.snap_index or index > self.last_applied:
+            return False
+        term = self.term_at(index)
+        del self.log[:index - self.snap_index]
+        self.snap_index, self.snap_term = index, term
+        self.storage.compact(index, term, data)
+        self._persist()
+        return True
 
     def on_append_reply(self, peer: int, req: AppendReq, resp: AppendResp | None) -> None:
         inf = self.inflight.get(peer)
@@ -367,7 +501,7 @@ class RaftCore:
         applied = False
         while self.last_applied < self.commit_index:
             self.last_applied += 1
-            e = self.log[self.last_applied]
+            e = self.entry(self.last_applied)
             self.apply_fn(self.last_applied, e)
             applied = True
         if applied:
@@ -398,8 +532,8 @@ class RaftCore:
 
     def status(self) -> dict:
         return {"id": self.id, "role": self.role.value, "term": self.term,
-                "leader": self.leader_id, "log": len(self.log), "commit": self.commit_index,
-                "applied": self.last_applied}
+                "leader": self.leader_id, "log": self.last_index + 1, "commit": self.commit_index,
+                "applied": self.last_applied, "snap_index": self.snap_index}
 
 
 class NotLeaderError(Exception):

@@ -21,8 +21,9 @@ import time
 
 import grpc
 
-from ..protos import RAFT_SERVICE, make_stub, raft_pb
-from .core import NOOP, AppendReq, AppendResp, Entry, NotLeaderError, RaftConfig, RaftCore, VoteReq, VoteResp
+from ..protos import RAFT_SERVICE, RAFT_SNAPSHOT_SERVICE, make_stub, raft_pb, raft_snap_pb
+from .core import (NOOP, AppendReq, AppendResp, Entry, NotLeaderError, RaftConfig, RaftCore,
+                   SnapshotReq, SnapshotResp, VoteReq, VoteResp)
 from .state_machine import ChatState
 from .storage import data_dir, open_storage
 
@@ -59,7 +60,8 @@ class RaftRuntime:
     def __init__(self, node_id: int, port: int, peers: dict, data_root: str = ".",
                  storage: str = "native", config: RaftConfig | None = None,
                  state: ChatState | None = None, fsync: bool = False, tick: float = 0.01,
-                 persist_interval: float = 0.2, seed_defaults=None):
+                 persist_interval: float = 0.2, seed_defaults=None, snapshot_every: int = 0,
+                 snapshot_chunk: int = 4 << 20):
         self.id = node_id
         self.port = port
         self.peers = {int(k): v for k, v in peers.items() if int(k) != node_id}
@@ -73,19 +75,33 @@ class RaftRuntime:
         self.persist_interval = persist_interval
         self.waiters: dict[int, _Waiter] = {}
         self.apply_listeners = []
-        # app-state cache first (reference load order), defaults if empty
-        self.state.load(self.dir)
-        if not self.state.channels and seed_defaults is not None:
-            seed_defaults(self.state)
+        if snapshot_every and storage != "native":
+            raise ValueError("log compaction (snapshot_every) requires native storage")
+        self.snapshot_every = snapshot_every
+        self.snapshot_chunk = snapshot_chunk
+        self._snap_rx: dict = {}        # (term, leader, index) -> bytearray being received
+        self._snap_tx: set[int] = set()  # peers with a snapshot transfer in flight
+        snap = self.storage.latest_snapshot()
+        if snap is not None:
+            # a Raft snapshot is the authoritative baseline; the log after it
+            # is replayed below
+            self.state.restore_image(snap[2])
+        else:
+            # app-state cache first (reference load order), defaults if empty
+            self.state.load(self.dir)
+            if not self.state.channels and seed_defaults is not None:
+                seed_defaults(self.state)
         self.core = RaftCore(node_id, self.peers.keys(), self.storage, self._apply, config,
-                             now=time.monotonic())
-        # rebuild: replay every committed entry over the cached state (apply
-        # is idempotent), so a snapshot that lags the log loses nothing
+                             now=time.monotonic(), restore_fn=self._restore)
+        # rebuild: replay every committed entry after the snapshot over the
+        # cached state (apply is idempotent), so a cache that lags the log
+        # loses nothing
         with self.core_lock:
-            self.core.last_applied = -1
+            self.core.last_applied = self.core.snap_index
             self.core._apply()
         self.channels = {p: grpc.insecure_channel(a, options=GRPC_OPTS) for p, a in self.peers.items()}
         self.stubs = {p: make_stub(ch, RAFT_SERVICE) for p, ch in self.channels.items()}
+        self.snap_stubs = {p: make_stub(ch, RAFT_SNAPSHOT_SERVICE) for p, ch in self.channels.items()}
         self.running = False
         self._threads = []
 
@@ -116,6 +132,87 @@ class RaftRuntime:
                 self.core.tick(time.monotonic())
                 out = self.core.drain()
             self._send(out)
+            if self.snapshot_every:
+                self.maybe_compact()
+
+    # ------------------------------------------------------------ snapshots
+    def maybe_compact(self, force: bool = False) -> bool:
+        """Snapshot the state machine at the applied index and compact the log
+        once ``snapshot_every`` entries accumulated since the last snapshot.
+        Runs under core_lock, so the image is exactly the state at
+        last_applied (applies happen under the same lock)."""
+        with self.core_lock:
+            c = self.core
+            if c.last_applied <= c.snap_index:
+                return False
+            if not force and c.last_applied - c.snap_index < self.snapshot_every:
+                return False
+            with self.state_lock:
+                img = self.state.image()
+            return c.compact(c.last_applied, img)
+
+    def _restore(self, data: bytes) -> None:
+        with self.state_lock:
+            self.state.restore_image(data)
+
+    def _send_snapshot(self, peer: int, req: SnapshotReq) -> None:
+        """Stream the latest snapshot to ``peer`` in chunks (own thread)."""
+        resp = None
+        try:
+            snap = self.storage.latest_snapshot()
+            if snap is not None:
+                idx, term, data = snap
+                req = SnapshotReq(req.term, req.leader_id, idx, term)
+                stub = self.snap_stubs[peer]
+                n = len(data)
+                off = 0
+                while True:
+                    chunk = data[off:off + self.snapshot_chunk]
+                    done = off + len(chunk) >= n
+                    r = stub.InstallSnapshot(raft_snap_pb.InstallSnapshotRequest(
+                        term=req.term, leader_id=req.leader_id, last_included_index=idx,
+                        last_included_term=term, offset=off, data=chunk, done=done, total_size=n),
+                        timeout=max(self.core.cfg.rpc_timeout_append, 10.0))
+                    if done or not r.success or r.term > req.term:
+                        resp = SnapshotResp(r.term, r.success and done)
+                        break
+                    off += len(chunk)
+        except grpc.RpcError:
+            resp = None
+        finally:
+            with self.core_lock:
+                self._snap_tx.discard(peer)
+                self.core.now = time.monotonic()
+                self.core.on_snapshot_reply(peer, req, resp)
+                out = self.core.drain()
+            self._send(out)
+
+    def InstallSnapshot(self, request, context):
+        """raft.RaftSnapshot/InstallSnapshot: reassemble chunks, then hand the
+        whole image to the core."""
+        key = (request.term, request.leader_id, request.last_included_index)
+        with self.core_lock:
+            c = self.core
+            if request.term < c.term:
+                return raft_snap_pb.InstallSnapshotResponse(term=c.term, success=False)
+            c.now = time.monotonic()
+            c.election_deadline = c.now + c._timeout()  # the leader is alive
+            buf = self._snap_rx.get(key)
+            if request.offset == 0:
+                self._snap_rx = {key: bytearray()}  # a new transfer supersedes old ones
+                buf = self._snap_rx[key]
+            if buf is None or len(buf) != request.offset:
+                return raft_snap_pb.InstallSnapshotResponse(term=c.term, success=False)
+            buf += request.data
+            if not request.done:
+                return raft_snap_pb.InstallSnapshotResponse(term=c.term, success=True)
+            del self._snap_rx[key]
+            r = c.on_install_snapshot(SnapshotReq(request.term, request.leader_id,
+                                                  request.last_included_index,
+                                                  request.last_included_term, bytes(buf)))
+            out = c.drain()
+        self._send(out)
+        return raft_snap_pb.InstallSnapshotResponse(term=r.term, success=r.success)
 
     def _persist_loop(self) -> None:
         while self.running:
@@ -158,6 +255,14 @@ class RaftRuntime:
         for peer, kind, req in out:
             stub = self.stubs.get(peer)
             if stub is None:
+                continue
+            if kind == "snapshot":
+                with self.core_lock:
+                    if peer in self._snap_tx:
+                        continue
+                    self._snap_tx.add(peer)
+                threading.Thread(target=self._send_snapshot, args=(peer, req),
+                                 name=f"raft-snap-{self.id}->{peer}", daemon=True).start()
                 continue
             if kind == "vote":
                 pb = raft_pb.VoteRequest(term=req.term, candidate_id=req.candidate_id,
@@ -217,7 +322,8 @@ class RaftRuntime:
         with self.core_lock:
             c = self.core
             return {"is_leader": c.is_leader(), "leader_id": c.leader_id, "term": c.term,
-                    "state": c.role.value, "log": len(c.log), "commit": c.commit_index}
+                    "state": c.role.value, "log": c.last_index + 1, "commit": c.commit_index,
+                    "snap_index": c.snap_index}
 
     def propose(self, command: str, data: dict, timeout: float = 5.0) -> bool:
         """Replicate one command; True once committed and applied here."""

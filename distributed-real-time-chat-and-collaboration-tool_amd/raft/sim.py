@@ -7,6 +7,7 @@ reorder messages and partition the cluster.
 from __future__ import annotations
 
 import heapq
+import pickle
 import random
 
 from .core import AppendReq, MemoryStorage, RaftConfig, RaftCore, Role
@@ -34,13 +35,26 @@ class SimCluster:
         self.leaders_by_term: dict[int, set] = {}
 
     def _make(self, i, ids) -> None:
-        self.applied[i] = []
+        snap = self.storages[i].snapshot
+        # the simulated state machine is the list of applied entries; its
+        # snapshot image is that list (test-local data, produced here)
+        self.applied[i] = pickle.loads(snap) if snap else []
 
         def apply(idx, e, i=i):
             self.applied[i].append((idx, e))
 
+        def restore(data, i=i):
+            self.applied[i] = pickle.loads(data)
+
         self.nodes[i] = RaftCore(i, [p for p in ids if p != i], self.storages[i], apply, self.cfg,
-                                 seed=self.rng.randrange(1 << 30), now=self.now)
+                                 seed=self.rng.randrange(1 << 30), now=self.now,
+                                 restore_fn=restore)
+
+    def compact(self, i: int) -> bool:
+        """Snapshot node i's state machine at its applied index and compact."""
+        n = self.nodes[i]
+        data = pickle.dumps(self.applied[i])
+        return n.compact(n.last_applied, data)
 
     # ------------------------------------------------------------- faults
     def can_talk(self, a: int, b: int) -> bool:
@@ -56,7 +70,8 @@ class SimCluster:
     def restart(self, i: int) -> None:
         """Restart from durable storage (volatile state lost)."""
         self.down.discard(i)
-        # the simulated state machine is volatile: replay the whole log
+        # the simulated state machine is volatile: restore the snapshot and
+        # replay the log after it
         self.storages[i].state["last_applied"] = -1
         ids = sorted(self.nodes)
         self._make(i, ids)
@@ -71,6 +86,8 @@ class SimCluster:
             for dst, kind, req in n.drain():
                 if i in self.down:
                     continue
+                if kind == "snapshot":
+                    req.data = self.storages[i].snapshot
                 copies = 2 if self.rng.random() < self.dup else 1
                 for _ in range(copies):
                     if self.rng.random() < self.drop:
@@ -88,7 +105,12 @@ class SimCluster:
                     continue
                 node = self.nodes[dst]
                 node.now = self.now
-                resp = node.on_request_vote(req) if kind == "vote" else node.on_append_entries(req)
+                if kind == "vote":
+                    resp = node.on_request_vote(req)
+                elif kind == "snapshot":
+                    resp = node.on_install_snapshot(req)
+                else:
+                    resp = node.on_append_entries(req)
                 if self.rng.random() >= self.drop:
                     self._post(self.now + self.rng.uniform(*self.delay), ("resp", dst, src, kind, req, resp))
             else:
@@ -99,6 +121,8 @@ class SimCluster:
                 resp = item[5]
                 if kind == "vote":
                     node.on_vote_reply(src, req.term, resp)
+                elif kind == "snapshot":
+                    node.on_snapshot_reply(src, req, resp)
                 else:
                     node.on_append_reply(src, req, resp)
             self._flush_outboxes()

@@ -17,6 +17,7 @@ from __future__ import annotations
 import datetime as _dt
 import logging
 import os
+import pickle
 from collections import defaultdict
 
 from ..utils import pickle_compat
@@ -234,6 +235,25 @@ class ChatState:
         if os.path.exists(p):
             self.direct_messages = pickle_compat.safe_load(p)
         self.reindex()
+
+    # ------------------------------------------------- Raft snapshot image
+    def image(self) -> bytes:
+        """Whole replicated state as one blob for Raft snapshots (plain data,
+        pickle protocol 4; read back with the code-free SafeUnpickler).  Files
+        are included: the reference keeps uploads only in the log, so a
+        compacted log would otherwise lose them."""
+        return pickle.dumps({"users": self.users, "users_by_id": self.users_by_id,
+                             "channels": self.channels, "messages": self.channel_messages,
+                             "direct_messages": self.direct_messages, "files": self.files},
+                            protocol=pickle_compat.PROTOCOL)
+
+    def restore_image(self, data: bytes) -> None:
+        d = pickle_compat.safe_loads(data)
+        self.users, self.users_by_id = d["users"], d["users_by_id"]
+        self.channels, self.channel_messages = d["channels"], d["messages"]
+        self.direct_messages, self.files = d["direct_messages"], d["files"]
+        self.reindex()
+        self.dirty.update(self.FILES)
 
     def reindex(self) -> None:
         self._msg_ids = {m.get("id") for ms in self.channel_messages.values() for m in ms}

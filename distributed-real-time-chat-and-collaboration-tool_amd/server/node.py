@@ -17,7 +17,7 @@ from concurrent import futures
 
 import grpc
 
-from ..protos import RAFT_SERVICE, add_servicer
+from ..protos import RAFT_SERVICE, RAFT_SNAPSHOT_SERVICE, add_servicer
 from ..raft.core import RaftConfig
 from ..utils.logging_utils import setup_logging
 from .raft_service import ChatNode, NodeConfig
@@ -47,6 +47,7 @@ def serve(cfg: NodeConfig, block: bool = True, bind: str = "[::]"):
     node = ChatNode(cfg)
     server = grpc.server(futures.ThreadPoolExecutor(max_workers=cfg.grpc_workers), options=SERVER_OPTS)
     add_servicer(server, RAFT_SERVICE, node)
+    add_servicer(server, RAFT_SNAPSHOT_SERVICE, node.rt)  # log-compaction catch-up (Raft §7)
     port = server.add_insecure_port(f"{bind}:{cfg.port}")
     if port == 0:
         raise RuntimeError(f"cannot bind port {cfg.port}")
@@ -86,6 +87,9 @@ def main(argv=None) -> None:
     ap.add_argument("--token-mode", choices=("replicated", "reference"), default="replicated")
     ap.add_argument("--bcrypt-rounds", type=int, default=12)
     ap.add_argument("--fsync", action="store_true")
+    ap.add_argument("--snapshot-every", type=int, default=0,
+                    help="snapshot the state machine and compact the log every N entries "
+                         "(native storage; 0 = keep the whole log like the reference)")
     ap.add_argument("--log-level", default="INFO")
     a = ap.parse_args(argv)
     setup_logging(a.log_level)
@@ -94,7 +98,8 @@ def main(argv=None) -> None:
                      storage=a.storage, llm_address=a.llm or None,
                      raft=RaftConfig(election_timeout=(lo, hi), heartbeat_interval=a.heartbeat,
                                      local_commit=a.local_commit),
-                     token_mode=a.token_mode, bcrypt_rounds=a.bcrypt_rounds, fsync=a.fsync)
+                     token_mode=a.token_mode, bcrypt_rounds=a.bcrypt_rounds, fsync=a.fsync,
+                     snapshot_every=a.snapshot_every)
     print(f"\n{'=' * 60}\n  Raft Chat Node {a.node_id}\n  Port: {a.port}\n"
           f"  Features: Consensus + Full Chat Application + on-GPU AI\n{'=' * 60}\n", flush=True)
     serve(cfg)

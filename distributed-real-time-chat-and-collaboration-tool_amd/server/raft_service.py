@@ -64,6 +64,7 @@ class NodeConfig:
     advertise_host: str = "localhost"
     fsync: bool = False
     seed_defaults: bool = True
+    snapshot_every: int = 0                         # compact the log every N applied entries (0: never)
     llm_timeouts: dict = field(default_factory=lambda: {
         "smart": 20.0, "summary": 10.0, "answer": 10.0, "suggest": 20.0})
 
@@ -108,7 +109,8 @@ class ChatNode:
                 state.seed_defaults(lambda pw: auth.bcrypt_hashpw(pw, salt()))
 
         self.rt = RaftRuntime(cfg.node_id, cfg.port, cfg.peers, cfg.data_root, cfg.storage,
-                              cfg.raft, fsync=cfg.fsync, seed_defaults=seed)
+                              cfg.raft, fsync=cfg.fsync, seed_defaults=seed,
+                              snapshot_every=cfg.snapshot_every)
         self.state = self.rt.state
         self.llm = LLMClient(cfg.llm_address)
 

@@ -199,3 +199,37 @@ def test_storage_formats_and_migration(tmp_path):
     ns.export()
     assert len(pickle_compat.safe_load(os.path.join(d, "raft_log_port_50051.pkl"))) == 3
     ns.close()
+
+
+def test_native_storage_compaction_and_crash_recovery(tmp_path):
+    from drtc_amd.raft.core import Entry
+    from drtc_amd.raft.storage import NativeStorage
+
+    d = str(tmp_path / "n1")
+    st = NativeStorage(d, 50051)
+    st.load()
+    ents = [Entry(1 + i // 4, "SEND_MESSAGE", f"{i}".encode()) for i in range(20)]
+    st.append(ents)
+    st.compact(9, ents[9].term, b"image@9")
+    st.append([Entry(6, "SEND_MESSAGE", b"20")])
+    st.truncate_from(20)  # absolute index
+    st.append([Entry(6, "SEND_MESSAGE", b"20b")])
+    st.save_state({"current_term": 6, "voted_for": None, "commit_index": 15, "last_applied": 15})
+    st.close()
+    st2 = NativeStorage(d, 50051)
+    state, entries = st2.load()
+    assert state["snap_index"] == 9 and state["snap_term"] == ents[9].term
+    assert [e.data for e in entries] == [f"{i}".encode() for i in range(10, 20)] + [b"20b"]
+    assert st2.latest_snapshot() == (9, ents[9].term, b"image@9")
+    # crash after the snapshot file was written but before the log moved to
+    # its new segment: the covered prefix is skipped and the move completed
+    st2.snap.save(14, entries[4].term, b"image@14")
+    st2.close()
+    st3 = NativeStorage(d, 50051)
+    state, entries = st3.load()
+    assert state["snap_index"] == 14
+    assert [e.data for e in entries] == [f"{i}".encode() for i in range(15, 20)] + [b"20b"]
+    import os
+    segs = sorted(f for f in os.listdir(d) if f.endswith(".seg"))
+    assert segs == ["raft_log_port_50051.b15.seg"]
+    st3.close()

@@ -7,13 +7,17 @@ from drtc_amd.raft.sim import SimCluster
 
 
 def _check_log_matching(c: SimCluster):
+    """Absolute-index log matching over the entries both nodes still hold
+    (compaction drops committed prefixes)."""
     nodes = list(c.nodes.values())
     for a in nodes:
         for b in nodes:
-            n = min(len(a.log), len(b.log))
-            for i in range(n - 1, -1, -1):
-                if a.log[i].term == b.log[i].term:
-                    assert a.log[: i + 1] == b.log[: i + 1], "log matching violated"
+            lo = max(a.first_index, b.first_index)
+            hi = min(a.last_index, b.last_index)
+            for i in range(hi, lo - 1, -1):
+                if a.term_at(i) == b.term_at(i):
+                    assert all(a.entry(j) == b.entry(j) for j in range(lo, i + 1)), \
+                        "log matching violated"
                     break
 
 
@@ -174,3 +178,80 @@ def test_follower_catch_up_after_long_partition():
     c.partition = None
     c.run(3.0)
     assert len(c.committed_commands(lagger)) == 300
+
+
+# ------------------------------------------------------------ compaction
+def test_compaction_and_install_snapshot_to_lagging_follower():
+    c = SimCluster(3, seed=11)
+    l = c.wait_leader()
+    lag = next(i for i in c.nodes if i != l)
+    c.crash(lag)
+    for k in range(60):
+        c.propose("SEND_MESSAGE", str(k).encode())
+    c.run(1.0)
+    for i in c.nodes:
+        if i != lag:
+            assert c.compact(i)
+            assert c.nodes[i].snap_index >= 60 and len(c.nodes[i].log) == 0
+    for k in range(60, 70):
+        c.propose("SEND_MESSAGE", str(k).encode())
+    c.restart(lag)
+    c.run(2.0)
+    ref = c.committed_commands(l)
+    assert len(ref) == 70
+    assert c.committed_commands(lag) == ref  # caught up through InstallSnapshot
+    assert c.nodes[lag].snap_index >= 60
+    _check_log_matching(c)
+    _check_state_machine_safety(c)
+
+
+def test_restart_after_compaction_restores_snapshot_then_replays():
+    c = SimCluster(3, seed=12)
+    c.wait_leader()
+    for k in range(30):
+        c.propose("SEND_MESSAGE", str(k).encode())
+    c.run(1.0)
+    node = next(iter(c.nodes))
+    assert c.compact(node)
+    for k in range(30, 40):
+        c.propose("SEND_MESSAGE", str(k).encode())
+    c.run(1.0)
+    before = c.committed_commands(node)
+    c.crash(node)
+    c.restart(node)
+    c.run(1.0)
+    assert c.committed_commands(node)[:len(before)] == before
+    assert len(c.committed_commands(node)) == 40
+
+
+@pytest.mark.parametrize("seed", [21, 22, 23])
+def test_safety_with_periodic_compaction_under_faults(seed):
+    c = SimCluster(5, seed=seed, drop=0.1, dup=0.05)
+    c.wait_leader()
+    sent = 0
+    for rnd in range(12):
+        for _ in range(8):
+            try:
+                c.propose("SEND_MESSAGE", str(sent).encode())
+                sent += 1
+            except (RuntimeError, NotLeaderError):
+                pass
+        if rnd % 3 == 1:
+            victim = 1 + rnd % 5
+            c.crash(victim)
+        if rnd % 3 == 2:
+            for i in list(c.down):
+                c.restart(i)
+        for i in c.nodes:
+            if i not in c.down and c.nodes[i].last_applied - c.nodes[i].snap_index > 10:
+                c.compact(i)
+        c.run(0.5)
+    for i in list(c.down):
+        c.restart(i)
+    c.run(3.0)
+    _check_log_matching(c)
+    _check_state_machine_safety(c)
+    for t, ls in c.leaders_by_term.items():
+        assert len(ls) == 1
+    lens = {len(c.committed_commands(i)) for i in c.nodes}
+    assert len(lens) == 1  # everyone converged
