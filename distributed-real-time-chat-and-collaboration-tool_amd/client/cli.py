@@ -25,6 +25,7 @@ from datetime import datetime
 import grpc
 
 from ..protos import raft_pb
+from ..utils.config import parse_with_config
 from .connection import DEFAULT_CLUSTER, ClusterConnection, ClusterUnavailable
 
 BANNER = """
@@ -556,7 +557,7 @@ def main(argv=None):
     ap = argparse.ArgumentParser(description="drtc_amd chat client")
     ap.add_argument("--server", default=None, help="any node address (default: 3-node localhost cluster)")
     ap.add_argument("--nodes", default=None, help="comma-separated cluster addresses")
-    a = ap.parse_args(argv)
+    a = parse_with_config(ap, argv)
     nodes = a.nodes.split(",") if a.nodes else list(DEFAULT_CLUSTER)
     if a.server and a.server not in nodes:
         nodes.insert(0, a.server)

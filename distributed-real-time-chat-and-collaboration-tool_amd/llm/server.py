@@ -23,6 +23,7 @@ from concurrent import futures
 import grpc
 
 from ..protos import LLM_SERVICE, add_servicer
+from ..utils.config import parse_with_config
 from ..utils.logging_utils import setup_logging
 from .backends import ScriptedBackend
 from .service import FeatureParams, LLMServicer
@@ -87,7 +88,7 @@ def main(argv=None):
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--workers", type=int, default=64)
     ap.add_argument("--log-level", default="INFO")
-    args = ap.parse_args(argv)
+    args = parse_with_config(ap, argv)
     setup_logging(args.log_level)
     backend = build_backend(args)
     server = serve(backend, args.port, args.workers)

@@ -31,6 +31,7 @@ import grpc
 
 from ..protos import CHAT_SERVICE, add_servicer, chat_pb
 from ..utils import auth, pickle_compat
+from ..utils.config import parse_with_config
 
 log = logging.getLogger(__name__)
 
@@ -620,7 +621,7 @@ def main(argv=None):
     ap.add_argument("--port", type=int, default=50050)
     ap.add_argument("--node_id", type=int, default=1)
     ap.add_argument("--data-dir", default="server_data")
-    a = ap.parse_args(argv)
+    a = parse_with_config(ap, argv)
     logging.basicConfig(level=logging.INFO)
     serve(a.port, a.data_dir, node_id=a.node_id)
 

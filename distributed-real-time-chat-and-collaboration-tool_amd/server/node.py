@@ -19,6 +19,7 @@ import grpc
 
 from ..protos import RAFT_SERVICE, RAFT_SNAPSHOT_SERVICE, add_servicer
 from ..raft.core import RaftConfig
+from ..utils.config import parse_with_config
 from ..utils.logging_utils import setup_logging
 from .raft_service import ChatNode, NodeConfig
 
@@ -91,7 +92,7 @@ def main(argv=None) -> None:
                     help="snapshot the state machine and compact the log every N entries "
                          "(native storage; 0 = keep the whole log like the reference)")
     ap.add_argument("--log-level", default="INFO")
-    a = ap.parse_args(argv)
+    a = parse_with_config(ap, argv)
     setup_logging(a.log_level)
     lo, hi = (10.0, 15.0) if a.reference_timing else tuple(float(x) for x in a.election_timeout.split(","))
     cfg = NodeConfig(node_id=a.node_id, port=a.port, peers=parse_peers(a.peers), data_root=a.data_root,

@@ -233,3 +233,27 @@ def test_native_storage_compaction_and_crash_recovery(tmp_path):
     segs = sorted(f for f in os.listdir(d) if f.endswith(".seg"))
     assert segs == ["raft_log_port_50051.b15.seg"]
     st3.close()
+
+
+def test_config_file_layer(tmp_path):
+    import argparse
+
+    import pytest as _pytest
+
+    from drtc_amd.utils.config import parse_with_config
+
+    def parser():
+        ap = argparse.ArgumentParser()
+        ap.add_argument("--node-id", type=int, required=True)
+        ap.add_argument("--port", type=int, default=50051)
+        ap.add_argument("--snapshot-every", type=int, default=0)
+        return ap
+
+    y = tmp_path / "n.yaml"
+    y.write_text("node_id: 2\nport: 50052\nsnapshot_every: 100\n")
+    a = parse_with_config(parser(), ["--config", str(y), "--port", "6000"])
+    assert (a.node_id, a.port, a.snapshot_every) == (2, 6000, 100)  # CLI beats file
+    j = tmp_path / "n.json"
+    j.write_text('{"node_id": 3, "bogus": 1}')
+    with _pytest.raises(SystemExit):
+        parse_with_config(parser(), ["--config", str(j)])
