@@ -379,4 +379,4 @@ def visible_gpus() -> int:
 
 
 __all__ = ["EngineBackend", "ReplicaRouter", "ScriptedBackend", "WorkerPool", "GenerationError",
-           "visible_gpus", "queue", "os"]
+           "visible_gpus"]

@@ -26,7 +26,7 @@ from ..protos import LLM_SERVICE, add_servicer
 from ..utils.config import parse_with_config
 from ..utils.logging_utils import setup_logging
 from .backends import ScriptedBackend
-from .service import FeatureParams, LLMServicer
+from .service import LLMServicer
 
 log = logging.getLogger("drtc_amd.llm.server")
 

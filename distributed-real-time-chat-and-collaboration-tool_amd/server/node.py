@@ -12,7 +12,6 @@ import argparse
 import logging
 import signal
 import threading
-import time
 from concurrent import futures
 
 import grpc

@@ -74,8 +74,7 @@ def main():
                      "TFLOPs": round(2 * M * n * k / t / 1e12, 1)}
                 res.append(r)
                 print(json.dumps(r), flush=True)
-        if mode == "tunable":
-            torch.cuda.tunable.write_file()
+        if mode == "tunable":  # results are flushed to set_filename()'s file at exit
             torch.cuda.tunable.enable(False)
     os.makedirs("gpurun_out", exist_ok=True)
     with open("gpurun_out/gemm_bench.json", "w") as f:

@@ -1,6 +1,5 @@
 """Multi-node integration over real gRPC on localhost (in-process nodes)."""
 import io
-import os
 import time
 
 import pytest
@@ -10,7 +9,6 @@ from drtc_amd.client.connection import ClusterConnection
 from drtc_amd.llm.backends import ScriptedBackend
 from drtc_amd.llm.server import serve as serve_llm
 from drtc_amd.protos import raft_pb
-from drtc_amd.raft.core import RaftConfig
 from drtc_amd.utils.cluster import LocalCluster, free_port
 
 

@@ -10,7 +10,7 @@ import pytest
 
 from drtc_amd.engine import ChatTokenizer, LLMEngine
 from drtc_amd.llm import prompts as P
-from drtc_amd.llm.backends import EngineBackend, ScriptedBackend
+from drtc_amd.llm.backends import EngineBackend
 from drtc_amd.llm.server import serve as serve_llm
 from drtc_amd.models import TINY_LLAMA, TransformerLM
 from drtc_amd.protos import CHAT_SERVICE, LLM_SERVICE, chat_pb, llm_pb, make_stub

@@ -1,7 +1,6 @@
 """End-to-end GPU checks: model forward on the HIP path vs the PyTorch
 reference path, and hipGraph decode vs eager decode."""
 import pytest
-import torch
 
 from drtc_amd import ops
 from drtc_amd.engine import LLMEngine, SamplingParams

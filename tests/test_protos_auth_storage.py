@@ -64,7 +64,6 @@ def test_jwt_pyjwt_byte_format():
     h, p, s = tok.split(".")
     assert h == "eyJhbGciOiJIUzI1NiIsInR5cCI6IkpXVCJ9"  # {"alg":"HS256","typ":"JWT"}
     import base64
-    import json
     body = base64.urlsafe_b64decode(p + "=" * (-len(p) % 4))
     assert body == b'{"user_id":"alice","username":"alice","exp":1893456000}'
     assert "=" not in tok
