@@ -69,10 +69,11 @@ PYBIND11_MODULE(_hipk, m) {
               P<const int>(tile_q0), ntiles, scale, causal, S(st));
         });
   m.def("moe", [](u64 out, u64 x, u64 logits, u64 w_gu, u64 w_dn, int T, int H, int I, int E,
-                  int k, int e_off, int e_local, int act, u64 ws, int64_t ws_bytes, u64 st) {
+                  int k, int e_off, int e_local, int act, u64 ws, int64_t ws_bytes, int variant,
+                  u64 st) {
     return drtc::launch_moe(P<void>(out), P<const void>(x), P<const void>(logits),
                             P<const void>(w_gu), P<const void>(w_dn), T, H, I, E, k, e_off,
-                            e_local, act, P<void>(ws), ws_bytes, S(st));
+                            e_local, act, P<void>(ws), ws_bytes, variant, S(st));
   });
   m.def("moe_workspace_bytes", &drtc::moe_workspace_bytes);
   m.def("custom_ar_buffer_bytes", &drtc::custom_ar_buffer_bytes);

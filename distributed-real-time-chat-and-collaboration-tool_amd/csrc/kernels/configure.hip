@@ -5,6 +5,8 @@ namespace drtc {
 int configure_kernels() {
   int e = configure_decode();
   if (e) return e;
-  return configure_prefill();
+  e = configure_prefill();
+  if (e) return e;
+  return configure_moe();
 }
 }  // namespace drtc

@@ -43,7 +43,7 @@ int launch_sample(int* out_tokens, const void* logits, int B, int V, int ld,
 
 int launch_moe(void* out, const void* x, const void* router_logits, const void* w_gu,
                const void* w_dn, int T, int H, int I, int E, int k, int e_off, int e_local,
-               int act, void* workspace, int64_t ws_bytes, hipStream_t st);
+               int act, void* workspace, int64_t ws_bytes, int variant, hipStream_t st);
 int64_t moe_workspace_bytes(int T, int H, int I, int e_local, int k);
 
 // One-shot P2P all-reduce over IPC-mapped staging buffers (allreduce.hip).
@@ -65,5 +65,6 @@ int ar_error(void* base);
 int configure_kernels();
 int configure_decode();
 int configure_prefill();
+int configure_moe();
 
 }  // namespace drtc

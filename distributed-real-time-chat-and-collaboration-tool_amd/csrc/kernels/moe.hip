@@ -32,7 +32,7 @@ __global__ __launch_bounds__(1024) void moe_align_kernel(
     int* __restrict__ inv_pos, float* __restrict__ topk_w,
     int* __restrict__ tile_expert, int* __restrict__ tile_row0, int* __restrict__ tile_rows,
     int* __restrict__ n_tiles, int* __restrict__ local_range, int max_tiles, int e_off,
-    int e_local) {
+    int e_local, int bm) {
   __shared__ int cnt[256], off[257], fill[256], toff[257];
   const int tid = threadIdx.x;
   for (int e = tid; e < 256; e += 1024) { cnt[e] = 0; fill[e] = 0; }
@@ -77,7 +77,7 @@ __global__ __launch_bounds__(1024) void moe_align_kernel(
       off[e] = o;
       toff[e] = to;
       o += cnt[e];
-      to += loc ? (cnt[e] + kMoeBM - 1) / kMoeBM : 0;
+      to += loc ? (cnt[e] + bm - 1) / bm : 0;
     }
     off[E] = o;
     toff[E] = to;
@@ -92,8 +92,8 @@ __global__ __launch_bounds__(1024) void moe_align_kernel(
       const int ti = toff[e] + i;
       if (ti < max_tiles) {
         tile_expert[ti] = e - e_off;  // local weight index
-        tile_row0[ti] = off[e] + i * kMoeBM;
-        tile_rows[ti] = min(kMoeBM, cnt[e] - i * kMoeBM);
+        tile_row0[ti] = off[e] + i * bm;
+        tile_rows[ti] = min(bm, cnt[e] - i * bm);
       }
     }
   }
@@ -206,17 +206,17 @@ __global__ __launch_bounds__(256, 2) void moe_gemm_kernel(
     if (kt + 1 < nk) stage(kt + 1, cur ^ 1);
     const bf16_t* A = lds + cur * 2 * kTileElems;
     const bf16_t* B = A + kTileElems;
+    // k-substep 0 fragments first: its 16 MFMAs wait only for the first 8
+    // LDS reads (lgkmcnt counts in order), substep 1's reads overlap them
     bf16x8 fa0[4], fa1[4], fb0[4], fb1[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      fa0[i] = *(const bf16x8*)(A + (64 * wr + 16 * i) * kBK + off0);
-      fa1[i] = *(const bf16x8*)(A + (64 * wr + 16 * i) * kBK + off1);
-    }
+    for (int i = 0; i < 4; ++i) fa0[i] = *(const bf16x8*)(A + (64 * wr + 16 * i) * kBK + off0);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      fb0[j] = *(const bf16x8*)(B + brow[j] * kBK + off0);
-      fb1[j] = *(const bf16x8*)(B + brow[j] * kBK + off1);
-    }
+    for (int j = 0; j < 4; ++j) fb0[j] = *(const bf16x8*)(B + brow[j] * kBK + off0);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) fa1[i] = *(const bf16x8*)(A + (64 * wr + 16 * i) * kBK + off1);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) fb1[j] = *(const bf16x8*)(B + brow[j] * kBK + off1);
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -231,6 +231,150 @@ __global__ __launch_bounds__(256, 2) void moe_gemm_kernel(
   }
 
   // epilogue: C lane map row 4g+r, col l16 of each 16x16 tile
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = 64 * wr + 16 * i + 4 * g + r;
+      if (row >= nr) continue;
+      bf16_t* orow = out + (int64_t)(r0 + row) * ldo;
+      if constexpr (MODE == 0) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const float gt = acc[i][j][r], up = acc[i][j + 2][r];
+          float av;
+          if (act == 0) {
+            av = gt / (1.f + __expf(-gt));
+          } else {
+            const float inner = 0.7978845608028654f * (gt + 0.044715f * gt * gt * gt);
+            av = 0.5f * gt * (1.f + tanhf(inner));
+          }
+          orow[n0 + 32 * wc + 16 * j + l16] = f2bf(av * up);
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) orow[n0 + 64 * wc + 16 * j + l16] = f2bf(acc[i][j][r]);
+      }
+    }
+}
+
+// ------------------------------------------------------ pipelined GEMM
+// Same operand/epilogue contract as moe_gemm_kernel, restructured for the
+// glds-pipelined regime (cdna_hip_programming.md §5 "Pipelining across
+// barriers"): THREE LDS stages, two k-tiles in flight.  Each k-step waits
+// with a COUNTED vmcnt (the youngest tile may stay in flight), passes a raw
+// s_barrier (no vmcnt(0) drain, unlike __syncthreads with an LDS-DMA
+// outstanding), then issues the tile two steps ahead into the stage freed
+// by the previous step.  BM = 256 doubles the MFMA work per staged byte
+// (8 waves, 4x2, each 64x64) - the prefill shape; BM = 128 keeps 4 waves.
+// All LDS is one dynamic array (a second __shared__ object can make hipcc
+// drain vmcnt before every ds_read: §5 trap 4a).
+template <int BM>
+struct PipeCfg {
+  static constexpr int BN = 128;
+  static constexpr int WM = BM / 64, WN = 2, NW = WM * WN, NT = NW * 64;
+  static constexpr int ROWS = BM + BN;          // staged rows per k-tile
+  static constexpr int GPW = ROWS / (8 * NW);   // glds per wave per stage
+  static constexpr int STAGE = ROWS * kBK;      // elements per stage
+  static constexpr int LDS_BYTES = 3 * STAGE * 2;
+};
+
+template <int N>
+DRTC_DEVICE void wait_vmcnt() {
+  // gfx9 s_waitcnt immediate: vmcnt[3:0] | expcnt[6:4]=7 | lgkmcnt[11:8]=15 | vmcnt_hi[15:14]
+  constexpr int imm = (N & 0xF) | (0x7 << 4) | (0xF << 8) | ((N >> 4) << 14);
+  __builtin_amdgcn_s_waitcnt(imm);
+}
+
+template <int BM, int MODE>
+__global__ __launch_bounds__(PipeCfg<BM>::NT, 1) void moe_gemm_pipe_kernel(
+    bf16_t* __restrict__ out, const bf16_t* __restrict__ a, const bf16_t* __restrict__ w,
+    const int* __restrict__ sorted_tok, const int* __restrict__ tile_expert,
+    const int* __restrict__ tile_row0, const int* __restrict__ tile_rows,
+    const int* __restrict__ n_tiles, int K, int w_rows, int I, int ldo, int max_tiles,
+    int act) {
+  using C = PipeCfg<BM>;
+  extern __shared__ __attribute__((aligned(16))) bf16_t plds[];  // [3][ROWS][64]
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int xcd = orig & 7, q = nwg >> 3, rmd = nwg & 7;
+  const int wgid = (xcd < rmd ? xcd * (q + 1) : rmd * (q + 1) + (xcd - rmd) * q) + (orig >> 3);
+  const int tile = wgid % max_tiles, ct = wgid / max_tiles;
+  if (tile >= n_tiles[0]) return;
+  const int e = tile_expert[tile], r0 = tile_row0[tile], nr = tile_rows[tile];
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wv / C::WN, wc = wv % C::WN, l16 = lane & 15, g = lane >> 4;
+
+  const bf16_t* src[C::GPW];
+  const bf16_t* we = w + (int64_t)e * w_rows * K;
+  const int n0 = MODE == 0 ? (C::BN / 2) * ct : C::BN * ct;
+#pragma unroll
+  for (int i = 0; i < C::GPW; ++i) {
+    const int r = (C::GPW * 8) * wv + 8 * i + (lane >> 3);  // staged row (A rows, then B rows)
+    const int d = (lane & 7) ^ ((r >> 1) & 7);
+    if (r < BM) {
+      const int rr = r < nr ? r : 0;
+      const int64_t arow = MODE == 0 ? (int64_t)sorted_tok[r0 + rr] : (int64_t)(r0 + rr);
+      src[i] = a + arow * K + 8 * d;
+    } else {
+      const int br = r - BM;
+      const int wrow = MODE == 0 ? (br < C::BN / 2 ? n0 + br : I + n0 + br - C::BN / 2) : n0 + br;
+      src[i] = we + (int64_t)wrow * K + 8 * d;
+    }
+  }
+  auto stage = [&](int kt, int buf) {
+    bf16_t* base = plds + buf * C::STAGE + (C::GPW * 8) * wv * kBK;
+#pragma unroll
+    for (int i = 0; i < C::GPW; ++i) glds16(src[i] + kt * kBK, base + 8 * i * kBK);
+  };
+  const int rsw = (l16 >> 1) & 7;
+  const int off0 = l16 * kBK + ((0 + g) ^ rsw) * 8;
+  const int off1 = l16 * kBK + ((4 + g) ^ rsw) * 8;
+  int brow[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    brow[j] = BM + (MODE == 0 ? (j < 2 ? 32 * wc + 16 * j : C::BN / 2 + 32 * wc + 16 * (j - 2))
+                              : 64 * wc + 16 * j);
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const int nk = K / kBK;
+  stage(0, 0);
+  if (nk > 1) stage(1, 1);
+  int cur = 0;
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + 1 < nk) wait_vmcnt<C::GPW>();  // tile kt landed; tile kt+1 may still fly
+    else wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (kt + 2 < nk) stage(kt + 2, cur == 0 ? 2 : cur - 1);  // the stage read in step kt-1
+    const bf16_t* A = plds + cur * C::STAGE;
+    bf16x8 fa0[4], fa1[4], fb0[4], fb1[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) fa0[i] = *(const bf16x8*)(A + (64 * wr + 16 * i) * kBK + off0);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) fb0[j] = *(const bf16x8*)(A + brow[j] * kBK + off0);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) fa1[i] = *(const bf16x8*)(A + (64 * wr + 16 * i) * kBK + off1);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) fb1[j] = *(const bf16x8*)(A + brow[j] * kBK + off1);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(fa0[i], fb0[j], acc[i][j]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(fa1[i], fb1[j], acc[i][j]);
+    __builtin_amdgcn_s_setprio(0);
+    cur = cur == 2 ? 0 : cur + 1;
+  }
+
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -282,13 +426,21 @@ __global__ __launch_bounds__(256) void moe_combine_kernel(
 
 int launch_moe(void* out, const void* x, const void* router_logits, const void* w_gu,
                const void* w_dn, int T, int H, int I, int E, int k, int e_off, int e_local,
-               int act, void* workspace, int64_t ws_bytes, hipStream_t st) {
+               int act, void* workspace, int64_t ws_bytes, int variant, hipStream_t st) {
   if (T == 0) return 0;
   if (E > 256 || k > kMoeMaxK || k < 1 || k > E || H % 128 != 0 || I % 64 != 0 || H % kBK != 0 ||
       e_off < 0 || e_local < 1 || e_off + e_local > E)
     return -1;
   const int P = T * k;
-  const int max_tiles = (P + kMoeBM - 1) / kMoeBM + e_local;
+  // GEMM structure: 0 = 128-row 2-barrier (small tiles, decode), 1 = 128-row
+  // 3-stage pipeline, 2 = 256-row 3-stage pipeline; -1 = pick by rows/expert
+  // measured (scripts/moe_bench.py, Mixtral shapes): the 128-row pipeline wins
+  // below ~100 rows per expert (decode: 5.3 TB/s of expert weights at T=256),
+  // the 256-row one from there up (ties the two-barrier kernel at 8k tokens)
+  if (variant < 0) variant = (P / e_local >= 96) ? 2 : 1;
+  if (variant > 2) return -1;
+  const int bm = variant == 2 ? 256 : 128;
+  const int max_tiles = (P + bm - 1) / bm + e_local;
   // workspace carve (all 256-B aligned)
   auto align = [](int64_t v) { return (v + 255) & ~int64_t(255); };
   char* p = (char*)workspace;
@@ -307,16 +459,48 @@ int launch_moe(void* out, const void* x, const void* router_logits, const void* 
   if (o > ws_bytes) return -2;
   hipLaunchKernelGGL(moe_align_kernel, dim3(1), dim3(1024), 0, st, (const bf16_t*)router_logits, T,
                      E, k, sorted_tok, sorted_w, inv_pos, topk_w, t_e, t_r0, t_n, n_tiles, local_range,
-                     max_tiles, e_off, e_local);
-  hipLaunchKernelGGL(moe_gemm_kernel<0>, dim3((I / 64) * max_tiles), dim3(256), 0, st, hbuf,
-                     (const bf16_t*)x, (const bf16_t*)w_gu, sorted_tok, t_e, t_r0, t_n, n_tiles, H,
-                     2 * I, I, I, max_tiles, act);
-  hipLaunchKernelGGL(moe_gemm_kernel<1>, dim3((H / 128) * max_tiles), dim3(256), 0, st, zbuf,
-                     (const bf16_t*)hbuf, (const bf16_t*)w_dn, sorted_tok, t_e, t_r0, t_n, n_tiles,
-                     I, H, I, H, max_tiles, 0);
+                     max_tiles, e_off, e_local, bm);
+  const dim3 g_gu((I / 64) * max_tiles), g_dn((H / 128) * max_tiles);
+  if (variant == 0) {
+    hipLaunchKernelGGL(moe_gemm_kernel<0>, g_gu, dim3(256), 0, st, hbuf, (const bf16_t*)x,
+                       (const bf16_t*)w_gu, sorted_tok, t_e, t_r0, t_n, n_tiles, H, 2 * I, I, I,
+                       max_tiles, act);
+    hipLaunchKernelGGL(moe_gemm_kernel<1>, g_dn, dim3(256), 0, st, zbuf, (const bf16_t*)hbuf,
+                       (const bf16_t*)w_dn, sorted_tok, t_e, t_r0, t_n, n_tiles, I, H, I, H,
+                       max_tiles, 0);
+  } else if (variant == 1) {
+    using Cf = PipeCfg<128>;
+    hipLaunchKernelGGL((moe_gemm_pipe_kernel<128, 0>), g_gu, dim3(Cf::NT), Cf::LDS_BYTES, st, hbuf,
+                       (const bf16_t*)x, (const bf16_t*)w_gu, sorted_tok, t_e, t_r0, t_n, n_tiles, H,
+                       2 * I, I, I, max_tiles, act);
+    hipLaunchKernelGGL((moe_gemm_pipe_kernel<128, 1>), g_dn, dim3(Cf::NT), Cf::LDS_BYTES, st, zbuf,
+                       (const bf16_t*)hbuf, (const bf16_t*)w_dn, sorted_tok, t_e, t_r0, t_n,
+                       n_tiles, I, H, I, H, max_tiles, 0);
+  } else {
+    using Cf = PipeCfg<256>;
+    hipLaunchKernelGGL((moe_gemm_pipe_kernel<256, 0>), g_gu, dim3(Cf::NT), Cf::LDS_BYTES, st, hbuf,
+                       (const bf16_t*)x, (const bf16_t*)w_gu, sorted_tok, t_e, t_r0, t_n, n_tiles, H,
+                       2 * I, I, I, max_tiles, act);
+    hipLaunchKernelGGL((moe_gemm_pipe_kernel<256, 1>), g_dn, dim3(Cf::NT), Cf::LDS_BYTES, st, zbuf,
+                       (const bf16_t*)hbuf, (const bf16_t*)w_dn, sorted_tok, t_e, t_r0, t_n,
+                       n_tiles, I, H, I, H, max_tiles, 0);
+  }
   hipLaunchKernelGGL(moe_combine_kernel, dim3(T), dim3(256), 0, st, (bf16_t*)out, zbuf, topk_w,
                      inv_pos, local_range, T, H, k);
   return (int)hipGetLastError();
+}
+
+int configure_moe() {
+  int e = 0;
+  e |= (int)hipFuncSetAttribute((const void*)moe_gemm_pipe_kernel<128, 0>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, PipeCfg<128>::LDS_BYTES);
+  e |= (int)hipFuncSetAttribute((const void*)moe_gemm_pipe_kernel<128, 1>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, PipeCfg<128>::LDS_BYTES);
+  e |= (int)hipFuncSetAttribute((const void*)moe_gemm_pipe_kernel<256, 0>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, PipeCfg<256>::LDS_BYTES);
+  e |= (int)hipFuncSetAttribute((const void*)moe_gemm_pipe_kernel<256, 1>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, PipeCfg<256>::LDS_BYTES);
+  return e;
 }
 
 int64_t moe_workspace_bytes(int T, int H, int I, int e_local, int k) {

@@ -13,6 +13,8 @@ contribution (the caller all-reduces over the EP group).
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn.functional as F
 
@@ -22,6 +24,11 @@ from .activation import ACTS, act_glu_ref
 # Largest token chunk per kernel call: bounds the workspace (P = chunk * k
 # rows of [I] and [H] intermediates) while keeping >10k workgroups per GEMM.
 MOE_CHUNK = 8192
+
+# Grouped-GEMM structure (csrc/kernels/moe.hip): 0 = 128-row two-barrier,
+# 1 = 128-row 3-stage pipeline, 2 = 256-row 3-stage pipeline, -1 = by rows
+# per expert.
+MOE_GEMM_VARIANT = int(os.environ.get("DRTC_MOE_VARIANT", "-1"))
 
 
 def route_ref(router_logits: torch.Tensor, top_k: int):
@@ -62,7 +69,7 @@ def make_workspace(tokens: int, hidden: int, inter: int, e_local: int, top_k: in
 def fused_moe(x: torch.Tensor, router_logits: torch.Tensor, w_gu: torch.Tensor,
               w_dn: torch.Tensor, top_k: int, act: str = "silu", num_experts: int | None = None,
               e_off: int = 0, workspace: torch.Tensor | None = None,
-              out: torch.Tensor | None = None) -> torch.Tensor:
+              out: torch.Tensor | None = None, variant: int | None = None) -> torch.Tensor:
     """y[t] = sum_j w[t,j] * down_e(act(gate_e x_t) * up_e x_t) over the top-k experts.
 
     x [T, H] bf16; router_logits [T, E] bf16; w_gu [E_local, 2I, H] ([gate | up]
@@ -97,7 +104,8 @@ def fused_moe(x: torch.Tensor, router_logits: torch.Tensor, w_gu: torch.Tensor,
         n = min(MOE_CHUNK, T - t0)
         check(lib.moe(out[t0].data_ptr(), x[t0].data_ptr(), router_logits[t0].data_ptr(),
                       w_gu.data_ptr(), w_dn.data_ptr(), n, H, inter, E, top_k, e_off, e_local,
-                      ACTS[act], workspace.data_ptr(), workspace.numel(), st), "moe")
+                      ACTS[act], workspace.data_ptr(), workspace.numel(),
+                      MOE_GEMM_VARIANT if variant is None else variant, st), "moe")
     return out
 
 

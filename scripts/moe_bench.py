@@ -37,6 +37,10 @@ def main():
         x = (torch.rand(T, H, device=dev, generator=g) * 2 - 1).to(torch.bfloat16)
         lg = torch.randn(T, E, device=dev, generator=g).to(torch.bfloat16)
         out = torch.empty_like(x)
+        t_v = []
+        for v in (0, 1, 2):
+            t_v.append(timeit(lambda: ops.fused_moe(x, lg, wgu, wdn, k, workspace=ws, out=out,
+                                                    variant=v)))
         t_f = timeit(lambda: ops.fused_moe(x, lg, wgu, wdn, k, workspace=ws, out=out))
         topi, wts = moe_ops.route_ref(lg, k)
 
@@ -49,8 +53,9 @@ def main():
             return o
         t_b = timeit(blaslt, 5)
         flops = 2 * T * k * 3 * H * I
-        print(f"T={T:5d}  fused {t_f:7.3f} ms {flops / t_f / 1e9:7.1f} TF/s "
-              f"{wbytes / t_f / 1e6:7.0f} GB/s | per-expert hipBLASLt {t_b:7.3f} ms "
+        vs = " ".join(f"v{v}:{flops / t / 1e9:6.0f}" for v, t in enumerate(t_v))
+        print(f"T={T:5d}  fused(auto) {t_f:7.3f} ms {flops / t_f / 1e9:7.1f} TF/s "
+              f"{wbytes / t_f / 1e6:7.0f} GB/s [{vs} TF/s] | per-expert hipBLASLt {t_b:7.3f} ms "
               f"{flops / t_b / 1e9:7.1f} TF/s", flush=True)
 
 

@@ -254,9 +254,10 @@ def _moe_inputs(T, H, I, E, seed=0):
                                         (300, 4096, 1792, 8, 2), (1000, 512, 256, 16, 4),
                                         (129, 256, 64, 8, 8)])
 @pytest.mark.parametrize("act", ["silu", "gelu_tanh"])
-def test_fused_moe(hipk, T, H, I, E, k, act):
+@pytest.mark.parametrize("variant", [0, 1, 2])
+def test_fused_moe(hipk, T, H, I, E, k, act, variant):
     x, lg, wgu, wdn = _moe_inputs(T, H, I, E)
-    y = ops.fused_moe(x, lg, wgu, wdn, k, act)
+    y = ops.fused_moe(x, lg, wgu, wdn, k, act, variant=variant)
     yr = ops.fused_moe_ref(x, lg, wgu, wdn, k, act)
     _close(y, yr, 3e-2, 3e-2, "fused_moe")
 
