@@ -74,6 +74,13 @@ class LLMEngine:
         self.temp = np.zeros(max_batch, dtype=np.float32)
         self.topk = np.zeros(max_batch, dtype=np.int32)
         self.topp = np.ones(max_batch, dtype=np.float32)
+        # per-slot finish bookkeeping, so a decode step checks 1024 sequences
+        # with a few numpy ops instead of a Python call per request
+        self.gen = np.zeros(max_batch, dtype=np.int32)        # tokens generated so far
+        self.max_new = np.zeros(max_batch, dtype=np.int32)
+        self.eos_stop = np.zeros(max_batch, dtype=bool)       # stop on EOS (not ignore_eos)
+        self.nblk = np.zeros(max_batch, dtype=np.int32)       # cache blocks held
+        self.stop_ids: dict[int, tuple] = {}                  # slot -> custom stop ids
         self.running: list[Request] = []
         self.waiting: collections.deque[Request] = collections.deque()
         self.lock = threading.Lock()
@@ -181,6 +188,12 @@ class LLMEngine:
         self.temp[s] = r.params.temperature
         self.topk[s] = r.params.top_k
         self.topp[s] = r.params.top_p
+        self.gen[s] = len(r.output_ids)
+        self.max_new[s] = r.params.max_new_tokens
+        self.eos_stop[s] = not r.params.ignore_eos
+        self.nblk[s] = len(r.blocks)
+        if r.params.stop_token_ids and not r.params.ignore_eos:
+            self.stop_ids[s] = tuple(r.params.stop_token_ids)
         return s
 
     def _release_slot(self, r: Request) -> None:
@@ -190,8 +203,16 @@ class LLMEngine:
             m = self.running[last]
             self.running[s] = m
             m.slot = s
-            for arr in (self.bt, self.ctx, self.last, self.temp, self.topk, self.topp):
+            for arr in (self.bt, self.ctx, self.last, self.temp, self.topk, self.topp, self.gen,
+                        self.max_new, self.eos_stop, self.nblk):
                 arr[s] = arr[last]
+            moved = self.stop_ids.pop(last, None)
+            if moved is not None:
+                self.stop_ids[s] = moved
+            else:
+                self.stop_ids.pop(s, None)
+        else:
+            self.stop_ids.pop(s, None)
         self.running.pop()
         r.slot = -1
         if r.blocks:
@@ -277,6 +298,7 @@ class LLMEngine:
             self.ctx[s] = n
             self.last[s] = tok
             r.output_ids.append(tok)
+            self.gen[s] = len(r.output_ids)
             if not r.first_token_time:
                 r.first_token_time = now
             reason = self._finish_check(r, tok)
@@ -292,7 +314,7 @@ class LLMEngine:
         newest requests when the cache is exhausted."""
         n = len(self.running)
         pos = self.ctx[:n]
-        need = (pos % BS == 0) & (pos // BS >= np.array([len(r.blocks) for r in self.running]))
+        need = (pos % BS == 0) & (pos // BS >= self.nblk[:n])
         for s in np.nonzero(need)[0].tolist():
             if s >= len(self.running):
                 continue
@@ -307,6 +329,7 @@ class LLMEngine:
             b = self.alloc.allocate_one()
             r.blocks.append(b)
             self.bt[r.slot, len(r.blocks) - 1] = b
+            self.nblk[r.slot] = len(r.blocks)
 
     def _preempt(self, r: Request) -> None:
         self._pressure = True
@@ -331,13 +354,18 @@ class LLMEngine:
         self.stats["decode_tokens"] += n
         self.ctx[:n] += 1
         self.last[:n] = toks
-        finished = []
+        self.gen[:n] += 1
         reqs = list(self.running)
         for r, tok in zip(reqs, toks.tolist()):
             r.output_ids.append(tok)
-            reason = self._finish_check(r, tok)
-            if reason:
-                finished.append((r, reason))
+        # finish conditions for the whole batch at once (see _finish_check)
+        stop = self.eos_stop[:n] & (toks == self.cfg.eos_token_id)
+        for s_, ids in self.stop_ids.items():
+            if s_ < n and int(toks[s_]) in ids:
+                stop[s_] = True
+        length = (self.gen[:n] >= self.max_new[:n]) | (self.ctx[:n] + 1 >= self.max_model_len)
+        done_idx = np.nonzero(stop | length)[0].tolist()
+        finished = [(reqs[i], "stop" if stop[i] else "length") for i in done_idx]
         for r, reason in finished:
             self._release_slot(r)
             r.mark_finished(reason)
