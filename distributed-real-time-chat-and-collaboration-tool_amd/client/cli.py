@@ -533,6 +533,30 @@ class ChatShell(cmd.Cmd):
             self.say(f"  - {p}")
 
     # ----------------------------------------------------------- help/exit
+    HELP_GROUPS = (
+        ("Account", ("signup", "login <username>", "logout")),
+        ("Channels", ("channels", "create_channel <name> [description]", "switch <channel>",
+                      "join <channel>", "send <message>", "history [n]", "members",
+                      "add_user <username>  (channel admins)",
+                      "remove_user <username>  (channel admins)")),
+        ("Direct messages", ("dm <username>", "conversations", "back")),
+        ("Files", ("upload <path> [description]", "download <file_id> [name]", "files")),
+        ("AI", ("smart_reply [k]", "summarize [n]", "ask <question>", "suggest [text|k]")),
+        ("Cluster", ("users", "status", "reconnect")),
+        ("Other", ("clear", "help", "help_all", "exit / quit / Ctrl-D")),
+    )
+
+    def do_help(self, arg):
+        """Show the command overview (help <command> for one command)"""
+        if arg:
+            return super().do_help(arg)
+        self.say("\n" + "=" * 60 + "\nCOMMANDS\n" + "=" * 60)
+        for title, cmds in self.HELP_GROUPS:
+            self.say(f" {title}:")
+            for c in cmds:
+                self.say(f"   {c}")
+        self.say(" 'help_all' lists every command with a one-line description.")
+
     def do_help_all(self, arg):
         """Show every command with its usage"""
         for name in sorted(n[3:] for n in self.get_names() if n.startswith("do_")):

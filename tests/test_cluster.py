@@ -165,9 +165,10 @@ def test_cli_session(cluster, tmp_path):
                  "send in proj", "members", "add_user bob", "switch general", "history 5", "users",
                  f"upload {f}", "files", "smart_reply", "summarize 3", "suggest lets", "ask what?",
                  "dm bob", "send hi bob", "back", "conversations", "status", "switch general",
-                 "help_all"]:
+                 "help_all", "help", "help send"]:
         sh.onecmd(line)
     text = out.getvalue()
+    assert "Direct messages:" in text and "smart_reply [k]" in text
     assert "You -> #general: hi team" in text and "#proj" in text
     assert "Added bob to #proj" in text
     assert "Uploaded notes.txt" in text and "notes.txt" in text
