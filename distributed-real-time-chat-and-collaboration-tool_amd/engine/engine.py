@@ -10,6 +10,11 @@ Scheduling (one iteration = one ``step()``):
   * on KV exhaustion the most recently admitted request is preempted
     (blocks freed, re-queued at the front for recomputation).
 
+Replaces the reference's hosted model call
+(``genai.GenerativeModel('gemini-2.5-flash').generate_content``,
+llm_server/llm_server.py:33,167,231,287,403): the four LLM features now
+generate on the node's own GPU, batched across concurrent RPCs.
+
 Running requests occupy dense "slots" 0..n-1 whose block-table rows live in
 a persistent numpy array, so building a decode step's metadata is a handful
 of vectorised numpy ops (no per-request Python loops on the hot path except

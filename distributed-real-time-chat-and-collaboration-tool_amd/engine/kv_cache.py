@@ -6,7 +6,9 @@ One contiguous allocation per engine, carved into per-layer views:
 The block count is derived from the free HBM left after the weights
 (``torch.cuda.mem_get_info``) times ``kv_fraction``; on a 288 GB MI355X with
 Llama-3-8B that is ~1.5 M cached tokens.  Blocks are handed out by the
-native :class:`BlockAllocator` (C++ free list, see csrc/runtime).
+native :class:`BlockAllocator` (C++ free list, see csrc/runtime).  No
+reference counterpart: the reference keeps no model state (hosted Gemini,
+llm_server/llm_server.py:33); SURVEY §7.1 "paged KV allocator sized from free HBM".
 """
 from __future__ import annotations
 

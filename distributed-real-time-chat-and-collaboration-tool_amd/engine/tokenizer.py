@@ -9,7 +9,9 @@ ids up to ``vocab_size`` (128,256 for Llama-3, 32,000 for Mixtral, 256,000
 for Gemma).  Text is pre-split GPT-style into `` ?word | ?punct | space``
 pieces; each piece is one token when in the vocabulary, else its UTF-8 bytes.
 Token counts of chat text therefore track a BPE tokenizer's (~1 token per
-word), which is what matters for prefill/decode shapes.
+word), which is what matters for prefill/decode shapes.  (The reference
+sends raw prompt text to a hosted API, llm_server/llm_server.py:167; the
+prompt strings themselves are the reference's, see llm/prompts.py.)
 """
 from __future__ import annotations
 

@@ -7,7 +7,9 @@
 * ``ScriptedBackend`` - deterministic, format-correct text for CPU tests and
   the "LLM disabled" plumbing configuration (no model at all).
 
-All expose ``generate(prompts, params, timeout) -> list[str]``.
+All expose ``generate(prompts, params, timeout) -> list[str]`` - the role of
+``self.model.generate_content`` in the reference's LLMServicer
+(llm_server/llm_server.py:23-145, 167).
 """
 from __future__ import annotations
 

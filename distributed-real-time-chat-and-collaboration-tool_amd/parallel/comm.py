@@ -5,6 +5,8 @@ with the same code path.  A :class:`ParallelContext` carries the tensor-
 parallel (TP) and expert-parallel (EP) groups a model shard needs; the
 data-parallel (DP) dimension is replica-level (one engine per GPU, requests
 routed by the LLM service) and needs no collective on the hot path.
+The reference has no collectives at all (gRPC only); these
+are the X1-X3 rows of SURVEY §2.3.
 """
 from __future__ import annotations
 
