@@ -64,12 +64,27 @@ __global__ __launch_bounds__(256, D >= 256 ? 1 : 2) void paged_decode_kernel(
   const int h = blockIdx.x - b * Hkv;
   const int p = blockIdx.y;
   const int G = Hq / Hkv;
-  const int ctx = context_lens[b];
-  const int nblk = (ctx + kBS - 1) / kBS;
-  const int nparts = (nblk + blocks_per_part - 1) / blocks_per_part;
   const int lane = threadIdx.x & 63;
   const int w = wave_id_uniform();
   const int col = lane & 15, g = lane >> 4;
+  const int blk_begin = p * blocks_per_part;
+  // Issue every load that does not depend on the context length first: the
+  // block-table entries of this wave's first two blocks (clamped into the
+  // row: speculative, used only if the blocks exist) and Q.  The critical
+  // path becomes max(ctx, table) -> K/V instead of ctx -> table -> K/V.
+  const int* bt = block_tables + (int64_t)b * bt_stride;
+  const int ph_a = bt[min(blk_begin + w, bt_stride - 1)];
+  const int ph_b = bt[min(blk_begin + w + 4, bt_stride - 1)];
+  bf16x8 qf[KS];  // Q^T B-operand fragments (zero for padding columns col >= G)
+  const bf16_t* qrow = q + (int64_t)b * q_stride + (int64_t)(h * G + col) * D;
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    if (col < G) qf[s] = load_bf16x8(qrow + 32 * s + 8 * g);
+    else for (int j = 0; j < 8; ++j) qf[s][j] = f2bf(0.f);
+  }
+  const int ctx = context_lens[b];
+  const int nblk = (ctx + kBS - 1) / kBS;
+  const int nparts = (nblk + blocks_per_part - 1) / blocks_per_part;
 
   if (ctx <= 0) {  // padded batch slot: deterministic zeros, no cache reads
     if (p == 0)
@@ -79,38 +94,29 @@ __global__ __launch_bounds__(256, D >= 256 ? 1 : 2) void paged_decode_kernel(
   }
   if (p >= nparts) return;
 
-  const int blk_begin = p * blocks_per_part;
   const int blk_end = min(nblk, blk_begin + blocks_per_part);
-
-  // Q^T B-operand fragments (zero for padding columns col >= G).
-  bf16x8 qf[KS];
-  const bf16_t* qrow = q + (int64_t)b * q_stride + (int64_t)(h * G + col) * D;
-#pragma unroll
-  for (int s = 0; s < KS; ++s) {
-    if (col < G) qf[s] = load_bf16x8(qrow + 32 * s + 8 * g);
-    else for (int j = 0; j < 8; ++j) qf[s][j] = f2bf(0.f);
-  }
 
   f32x4 o[NT];
 #pragma unroll
   for (int i = 0; i < NT; ++i) o[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
   float m = kNegBig, lsum = 0.f;
 
-  const int* bt = block_tables + (int64_t)b * bt_stride;
   const int64_t blk_elems = (int64_t)kBS * D;
   KVRegs<D> cur, nxt;
   int blk = blk_begin + w;
+  int ph_next = ph_b;  // table entry of block blk + 4, loaded one step ahead
   if (blk < blk_end) {
-    const int64_t phys = bt[blk];
+    const int64_t phys = ph_a;
     load_kv_block<D>(cur, k_cache + (phys * Hkv + h) * blk_elems,
                      v_cache + (phys * Hkv + h) * blk_elems, lane);
   }
   for (; blk < blk_end; blk += 4) {
     const int nb = blk + 4;
     if (nb < blk_end) {  // register double-buffer: next block in flight
-      const int64_t phys = bt[nb];
+      const int64_t phys = ph_next;
       load_kv_block<D>(nxt, k_cache + (phys * Hkv + h) * blk_elems,
                        v_cache + (phys * Hkv + h) * blk_elems, lane);
+      ph_next = bt[min(nb + 4, bt_stride - 1)];
     }
     f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
