@@ -202,6 +202,9 @@ def main() -> None:
             "engine_stats": dict(eng.stats),
         }
         print(json.dumps(out), flush=True)
+        if eng.runner.gpu_ms:
+            g = sorted(eng.runner.gpu_ms)
+            log(rank, f"decode graph GPU time: median {g[len(g) // 2]:.3f} ms over {len(g)} steps")
         if args.trace:
             from drtc_amd.utils import tracing
             n = tracing.dump_chrome_trace(args.trace)

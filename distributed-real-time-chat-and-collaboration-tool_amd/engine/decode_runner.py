@@ -10,6 +10,7 @@ the sampled token ids.
 from __future__ import annotations
 
 import bisect
+import os
 
 import numpy as np
 import torch
@@ -61,6 +62,10 @@ class DecodeRunner:
         self._metas = {}
         self._graphs = {}
         self._pool = None
+        # DRTC_TIME_DECODE=1: GPU time of every replay (hipEvents), for host-
+        # overhead accounting (decode wall time - GPU time)
+        self.time_gpu = os.environ.get("DRTC_TIME_DECODE") == "1"
+        self.gpu_ms: list[float] = []
 
     # ------------------------------------------------------------------
     def bucket(self, n: int) -> int:
@@ -147,13 +152,22 @@ class DecodeRunner:
         if g is None and self.use_graphs:
             self.capture(Bb)
             g = self._graphs[Bb]
+        timing = nb and self.time_gpu
+        if timing:
+            ev0 = torch.cuda.Event(enable_timing=True)
+            ev1 = torch.cuda.Event(enable_timing=True)
+            ev0.record()
         with tracing.span("decode.graph_replay" if g is not None else "decode.eager", bucket=Bb):
             if g is not None:
                 g.replay()
             else:
                 self._forward(Bb)
+        if timing:
+            ev1.record()
         if nb:
             self.h_out[:n].copy_(self.out[:n], non_blocking=True)
             torch.cuda.current_stream(self.device).synchronize()
+            if timing:
+                self.gpu_ms.append(ev0.elapsed_time(ev1))
             return self.h_out[:n].numpy().copy()
         return self.out[:n].numpy().copy()
