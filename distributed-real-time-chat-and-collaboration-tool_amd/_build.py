@@ -34,6 +34,13 @@ def _pybind_includes() -> list[str]:
     return [f"-I{pybind11.get_include()}", f"-I{sysconfig.get_paths()['include']}"]
 
 
+def _torch_lib() -> str:
+    import importlib.util
+
+    spec = importlib.util.find_spec("torch")
+    return os.path.join(os.path.dirname(spec.origin), "lib")
+
+
 def _newer(target: str, deps: list[str]) -> bool:
     if not os.path.exists(target):
         return True
@@ -68,14 +75,18 @@ def _build_module(name: str, sources: list[str], headers: list[str], compiler: s
 
 def build_hip(jobs: int = 8) -> str:
     kdir = os.path.join(CSRC, "kernels")
-    sources = sorted(glob.glob(os.path.join(kdir, "*.hip"))) + [os.path.join(kdir, "bindings.cpp")]
+    sources = sorted(glob.glob(os.path.join(kdir, "*.hip")) + glob.glob(os.path.join(kdir, "*.cpp")))
     headers = sorted(glob.glob(os.path.join(kdir, "*.h")))
     cflags = [
         f"--offload-arch={ARCH}", "-O3", "-fPIC", "-std=c++17", "-ffp-contract=fast",
         "-Wno-unused-result", f"-I{kdir}", *_pybind_includes(),
     ]
+    # hipBLASLt: link the copy PyTorch ships (it is already loaded when torch
+    # is imported first, and the soname resolves to it), headers from /opt/rocm
+    tlib = _torch_lib()
     return _build_module("_hipk", sources, headers, HIPCC, cflags,
-                         [f"--offload-arch={ARCH}", "-fPIC"], jobs)
+                         [f"--offload-arch={ARCH}", "-fPIC", f"-L{tlib}", "-l:libhipblaslt.so",
+                          f"-Wl,-rpath,{tlib}"], jobs)
 
 
 def build_native(jobs: int = 8) -> str:

@@ -108,6 +108,18 @@ PYBIND11_MODULE(_hipk, m) {
   });
   m.def("ar_ipc_close", [](u64 p) { return drtc::ar_ipc_close(P<void>(p)); });
   m.def("ar_error", [](u64 base) { return drtc::ar_error(P<void>(base)); });
+  m.def("lt_version", &drtc::lt_version);
+  m.def("lt_gemm", [](u64 y, u64 x, u64 w, int64_t M, int64_t N, int64_t K, int64_t ldx,
+                      int64_t ldy, u64 st) {
+    return drtc::lt_gemm(P<void>(y), P<const void>(x), P<const void>(w), M, N, K, ldx, ldy, S(st));
+  });
+  m.def("lt_set_algo", &drtc::lt_set_algo);
+  m.def("lt_tune", [](u64 y, u64 x, u64 w, int64_t M, int64_t N, int64_t K, int64_t ldx,
+                      int64_t ldy, int iters, int max_candidates, u64 st) {
+    py::gil_scoped_release nogil;
+    return drtc::lt_tune(P<void>(y), P<const void>(x), P<const void>(w), M, N, K, ldx, ldy,
+                         iters, max_candidates, S(st));
+  });
   m.def("sample", [](u64 out_tokens, u64 logits, int B, int V, int ld,
                      u64 temperature, u64 top_k, u64 top_p, uint64_t seed,
                      u64 step, u64 st) {

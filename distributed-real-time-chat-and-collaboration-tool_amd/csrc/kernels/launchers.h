@@ -6,6 +6,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <utility>
+#include <vector>
+
 namespace drtc {
 
 int launch_rmsnorm(void* out, void* residual, const void* x, const void* w,
@@ -59,6 +62,16 @@ int ar_ipc_get(void* p, char* handle);  // 64-byte handle
 int ar_ipc_open(const char* handle, void** p);
 int ar_ipc_close(void* p);
 int ar_error(void* base);
+
+// Tuned hipBLASLt projection GEMM y[M,N] = x[M,K] @ W[N,K]^T, bf16 (gemm_lt.cpp).
+int lt_version();
+int lt_gemm(void* y, const void* x, const void* w, int64_t M, int64_t N, int64_t K, int64_t ldx,
+            int64_t ldy, hipStream_t st);
+int lt_set_algo(int64_t M, int64_t N, int64_t K, int64_t ldx, int64_t ldy, int algo_index);
+// (solution index, us per call) pairs; index -1 = hipBLASLt's heuristic pick
+std::vector<std::pair<int, float>> lt_tune(void* y, const void* x, const void* w, int64_t M,
+                                           int64_t N, int64_t K, int64_t ldx, int64_t ldy,
+                                           int iters, int max_candidates, hipStream_t st);
 
 // Raise the dynamic-LDS ceiling of the kernels that need > 64 KiB (head_dim
 // 256).  Called once at import, before any graph capture.

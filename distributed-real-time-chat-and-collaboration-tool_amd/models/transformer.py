@@ -2,7 +2,8 @@
 
 MI355X-first layout decisions
   * fused projections: one QKV GEMM and one gate|up GEMM per layer
-    (hipBLASLt via ``F.linear``); everything between the GEMMs is a fused HIP
+    (hipBLASLt via ``ops.linear``: per-shape tuned solutions for the decode
+    buckets); everything between the GEMMs is a fused HIP
     kernel: add+RMSNorm, RoPE + paged-KV write (in place on the QKV output),
     MFMA attention reading q/k/v straight out of the QKV buffer, act*up;
   * tensor parallel over RCCL: heads / intermediate columns sharded, one
@@ -213,9 +214,9 @@ class TransformerLM:
     def _mlp(self, L: dict, x: torch.Tensor) -> torch.Tensor:
         if self.cfg.is_moe:
             return self._moe(L, x)
-        gu = F.linear(x, L["gate_up"])
+        gu = ops.linear(x, L["gate_up"])
         a = ops.act_glu(gu, self.cfg.act)
-        y = F.linear(a, L["down"])
+        y = ops.linear(a, L["down"])
         return self.pc.all_reduce_tp(y)
 
     def _moe(self, L: dict, x: torch.Tensor) -> torch.Tensor:
@@ -265,7 +266,7 @@ class TransformerLM:
         return x
 
     def _logits(self, x: torch.Tensor) -> torch.Tensor:
-        logits = F.linear(x, self.lm_head)
+        logits = ops.linear(x, self.lm_head)
         return self.pc.all_gather_tp_lastdim(logits)
 
     def forward_prefill(self, ids: torch.Tensor, meta: PrefillMeta, kv_caches) -> torch.Tensor:
@@ -274,7 +275,7 @@ class TransformerLM:
         D = cfg.head_dim
 
         def attn(i, L, x):
-            qkv = F.linear(x, L["qkv"])
+            qkv = ops.linear(x, L["qkv"])
             kc, vc = kv_caches[i] if kv_caches is not None else (None, None)
             blockwise_v = kc is not None and meta.v_segs is not None
             ops.rope_kv_(qkv, meta.positions, meta.slots if kc is not None else None,
@@ -284,7 +285,7 @@ class TransformerLM:
                 ops.kv_write_v(vc, qkv, meta.v_segs, sh.hq, sh.hkv, D)
             a = ops.prefill_attention(qkv, meta.cu_seqlens, sh.hq, sh.hkv, D, cfg.attn_scale,
                                       True, tiles=meta.tiles, cu_host=meta.cu_host)
-            return self.pc.all_reduce_tp(F.linear(a, L["o"]))
+            return self.pc.all_reduce_tp(ops.linear(a, L["o"]))
 
         x = self._layers(self._embed(ids), attn)
         return self._logits(x.index_select(0, meta.last_idx))
@@ -297,7 +298,7 @@ class TransformerLM:
         B = ids.shape[0]
 
         def attn(i, L, x):
-            qkv = F.linear(x, L["qkv"])
+            qkv = ops.linear(x, L["qkv"])
             kc, vc = kv_caches[i]
             ops.rope_kv_(qkv, meta.positions, meta.slots, self.cos_sin, sh.hq, sh.hkv, D,
                          kc, vc, ops.KV_BLOCK)
@@ -306,7 +307,7 @@ class TransformerLM:
                                            cfg.attn_scale, out=attn_out,
                                            blocks_per_part=meta.blocks_per_part,
                                            workspace=meta.workspace)
-            return self.pc.all_reduce_tp(F.linear(a.view(B, sh.hq * D), L["o"]))
+            return self.pc.all_reduce_tp(ops.linear(a.view(B, sh.hq * D), L["o"]))
 
         x = self._layers(self._embed(ids), attn)
         return self._logits(x)

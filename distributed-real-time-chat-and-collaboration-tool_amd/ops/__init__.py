@@ -3,20 +3,23 @@
 Each op dispatches on the tensor's device: GPU tensors run the hand-written
 CDNA4 HIP kernel (``csrc/kernels``), CPU tensors run the fp32 PyTorch
 reference of the same op (used by the CPU tests and as the GPU numerics
-oracle).  Plain projection GEMMs are ``torch.nn.functional.linear``
-(hipBLASLt on ROCm); everything around them is fused here.
+oracle).  Projection GEMMs are hipBLASLt: ``linear`` replays a measured per-shape
+solution for the decode shapes in the tuning table (``ops/gemm.py``) and
+falls back to ``torch.nn.functional.linear`` elsewhere; everything around
+them is fused here.
 """
 from ._ext import on_gpu, reference_mode
 from .activation import act_glu, act_glu_ref
 from .attention import (KV_BLOCK, DecodeWorkspace, decode_partitioning, paged_decode_attention,
                         paged_decode_ref, prefill_attention, prefill_attention_ref, prefill_tiles)
+from .gemm import linear
 from .moe import fused_moe, fused_moe_ref
 from .norm import rmsnorm, rmsnorm_ref
 from .rope import build_rope_cache, kv_write_v, kv_write_v_ref, rope_kv_, rope_kv_ref
 from .sampling import sample, sample_ref
 
 __all__ = [
-    "on_gpu", "reference_mode", "fused_moe", "fused_moe_ref",
+    "on_gpu", "reference_mode", "linear", "fused_moe", "fused_moe_ref",
     "act_glu", "act_glu_ref", "KV_BLOCK", "DecodeWorkspace", "decode_partitioning",
     "paged_decode_attention", "paged_decode_ref", "prefill_attention", "prefill_attention_ref",
     "prefill_tiles", "rmsnorm", "rmsnorm_ref", "build_rope_cache", "rope_kv_", "rope_kv_ref",

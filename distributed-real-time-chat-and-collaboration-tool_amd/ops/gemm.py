@@ -1,0 +1,133 @@
+"""Projection GEMMs with measured per-shape hipBLASLt solutions.
+
+``linear(x, w)`` computes ``x @ w.T`` (bf16, fp32 accumulate).  For the
+shapes listed in the tuning table (``ops/tuned/gemm_<arch>.json``: the
+decode GEMMs of each model at every hipGraph batch bucket) it calls
+hipBLASLt directly through ``csrc/kernels/gemm_lt.cpp`` with the solution
+that measured fastest on MI355X; every other shape (prefill, CPU) goes
+through ``torch.nn.functional.linear``.
+
+Why a table: a decode GEMM has a small fixed M (the batch bucket) and
+model-fixed N/K, where hipBLASLt's heuristic pick can be far from the best
+listed solution - e.g. Llama-3-70B ``down`` at M=256: 312 us heuristic vs
+178 us tuned (profiles/r1g_gemm_tuning.md).  Tables are produced by
+``scripts/tune_gemms.py`` on the GPU and keyed by the hipBLASLt version
+(solution indices are only valid for the library that listed them).
+"""
+from __future__ import annotations
+
+import json
+import os
+import threading
+
+import torch
+import torch.nn.functional as F
+
+from ._ext import check, hipk, on_gpu, stream_ptr
+
+TUNED_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuned")
+_lock = threading.Lock()
+_table: dict[tuple[int, int, int, int], int] | None = None  # (M, N, K, ldx) -> solution index
+_enabled = os.environ.get("DRTC_TUNED_GEMM", "1") != "0"
+
+
+def table_path(arch: str = "gfx950") -> str:
+    return os.path.join(TUNED_DIR, f"gemm_{arch}.json")
+
+
+def _key_str(M: int, N: int, K: int, ldx: int) -> str:
+    return f"{M},{N},{K},{ldx}"
+
+
+def load_table(path: str | None = None) -> dict:
+    """Read the tuning file: {str(hipblaslt_version): {"M,N,K,ldx": {...}}}."""
+    path = path or table_path()
+    if not os.path.exists(path):
+        return {}
+    with open(path) as f:
+        return json.load(f)
+
+
+def _activate() -> dict:
+    """Register every entry for the running hipBLASLt version with the native
+    plan cache (creates descriptors + workspace: must run outside capture)."""
+    global _table
+    if _table is not None:
+        return _table
+    with _lock:
+        if _table is not None:
+            return _table
+        tab: dict[tuple[int, int, int, int], int] = {}
+        if _enabled and torch.cuda.is_available():
+            h = hipk()
+            ver = str(h.lt_version())
+            for ks, e in load_table().get(ver, {}).items():
+                M, N, K, ldx = (int(v) for v in ks.split(","))
+                if h.lt_set_algo(M, N, K, ldx, N, int(e["algo"])) == 0:
+                    tab[(M, N, K, ldx)] = int(e["algo"])
+        _table = tab
+    return _table
+
+
+def reset() -> None:
+    """Forget the activated table (tests / after re-tuning)."""
+    global _table
+    with _lock:
+        _table = None
+
+
+def set_enabled(on: bool) -> None:
+    global _enabled
+    _enabled = bool(on)
+    reset()
+
+
+def linear(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """y = x @ w.T for x [M, K] (row stride ldx), w [N, K] contiguous."""
+    if (on_gpu(x) and _enabled and x.dim() == 2 and x.dtype == torch.bfloat16
+            and w.dtype == torch.bfloat16 and x.stride(1) == 1 and w.is_contiguous()):
+        M, K = x.shape
+        N = w.shape[0]
+        if (M, N, K, x.stride(0)) in _activate():
+            y = torch.empty((M, N), dtype=x.dtype, device=x.device)
+            check(hipk().lt_gemm(y.data_ptr(), x.data_ptr(), w.data_ptr(), M, N, K, x.stride(0),
+                                 N, stream_ptr(x)), "lt_gemm")
+            return y
+    return F.linear(x, w)
+
+
+def tune(M: int, N: int, K: int, device, iters: int = 20, max_candidates: int = 12) -> dict:
+    """Measure every hipBLASLt solution for y[M,N] = x[M,K] @ W[N,K]^T on
+    random operands; returns {"algo", "us", "heuristic_us", "candidates"}."""
+    g = torch.Generator(device=device).manual_seed(M * 7 + N * 13 + K)
+    x = torch.randn(M, K, device=device, dtype=torch.bfloat16, generator=g)
+    w = torch.randn(N, K, device=device, dtype=torch.bfloat16, generator=g) * 0.02
+    y = torch.empty(M, N, device=device, dtype=torch.bfloat16)
+    torch.cuda.synchronize(device)
+    res = hipk().lt_tune(y.data_ptr(), x.data_ptr(), w.data_ptr(), M, N, K, K, N, iters,
+                         max_candidates, torch.cuda.current_stream(device).cuda_stream)
+    if not res:
+        raise RuntimeError(f"lt_tune found no solution for M={M} N={N} K={K}")
+    heur = next((us for i, us in res if i == -1), float("inf"))
+    best_i, best_us = min(((i, us) for i, us in res if i >= 0), key=lambda t: t[1],
+                          default=(-1, heur))
+    return {"algo": best_i, "us": round(best_us, 2), "heuristic_us": round(heur, 2),
+            "candidates": len(res) - 1}
+
+
+def save_entries(entries: dict[str, dict], path: str | None = None) -> str:
+    """Merge ``entries`` ("M,N,K,ldx" -> tune() result) into the table of the
+    running hipBLASLt version."""
+    path = path or table_path()
+    data = load_table(path)
+    ver = str(hipk().lt_version())
+    data.setdefault(ver, {}).update(entries)
+    os.makedirs(os.path.dirname(path), exist_ok=True)
+    with open(path, "w") as f:
+        json.dump(data, f, indent=1, sort_keys=True)
+    reset()
+    return path
+
+
+__all__ = ["linear", "tune", "save_entries", "load_table", "reset", "set_enabled", "table_path",
+           "_key_str"]

@@ -21,6 +21,10 @@ SHAPES = {  # name: (N, K)
     "qkv": (6144, 4096), "o": (4096, 4096), "gate_up": (28672, 4096), "down": (4096, 14336),
     "lm_head": (128256, 4096),
 }
+SHAPES_70B = {  # Llama-3-70B (TP=1): hidden 8192, inter 28672, GQA 64/8
+    "qkv": (10240, 8192), "o": (8192, 8192), "gate_up": (57344, 8192), "down": (8192, 28672),
+    "lm_head": (128256, 8192),
+}
 
 
 def bench(fn, iters=50):
@@ -43,10 +47,13 @@ def main():
     ap.add_argument("--ms", default="64,128,256,512,1024,16384")
     ap.add_argument("--tunable-file", default="gpurun_out/tunableop_results.csv")
     ap.add_argument("--modes", default="default,rocblas,tunable")
+    ap.add_argument("--model", default="8b", choices=["8b", "70b"])
     a = ap.parse_args()
     dev = torch.device("cuda")
     res = []
-    W = {k: torch.randn(n, kk, device=dev, dtype=torch.bfloat16) * 0.02 for k, (n, kk) in SHAPES.items()}
+    shapes = SHAPES_70B if a.model == "70b" else SHAPES
+    W = {k: torch.randn(n, kk, device=dev, dtype=torch.bfloat16) * 0.02 for k, (n, kk) in shapes.items()}
+    H, inter = shapes["o"][0], shapes["down"][1]
     for mode in a.modes.split(","):
         if mode == "rocblas":
             torch.backends.cuda.preferred_blas_library("cublas")
@@ -58,8 +65,8 @@ def main():
             torch.cuda.tunable.set_max_tuning_duration(200)
             torch.cuda.tunable.set_filename(a.tunable_file)
         for M in [int(x) for x in a.ms.split(",")]:
-            x = torch.randn(M, 4096, device=dev, dtype=torch.bfloat16)
-            xd = torch.randn(M, 14336, device=dev, dtype=torch.bfloat16)
+            x = torch.randn(M, H, device=dev, dtype=torch.bfloat16)
+            xd = torch.randn(M, inter, device=dev, dtype=torch.bfloat16)
             for name, w in W.items():
                 if name == "lm_head" and M > 1024:
                     continue
@@ -67,7 +74,10 @@ def main():
                 if mode == "tunable":
                     F.linear(inp, w)  # tune outside the graph
                     torch.cuda.synchronize()
-                t = bench(lambda: F.linear(inp, w))
+                if mode == "transposed":  # out^T = W @ x^T (library sees M'=N, N'=M)
+                    t = bench(lambda: torch.mm(w, inp.t()).t().contiguous())
+                else:
+                    t = bench(lambda: F.linear(inp, w))
                 n, k = w.shape
                 r = {"mode": mode, "M": M, "gemm": name, "us": round(t * 1e6, 1),
                      "TBps_weights": round(n * k * 2 / t / 1e12, 2),

@@ -297,3 +297,33 @@ def test_fused_moe_chunked_and_graph(hipk):
     gr.replay()
     torch.cuda.synchronize()
     _close(out, ops.fused_moe_ref(x[64:128], lg[64:128], wgu, wdn, k), 3e-2, 3e-2, "graph")
+
+
+@pytest.mark.parametrize("M,N,K", [(64, 512, 256), (256, 1280, 1024), (1, 4096, 512)])
+def test_tuned_linear(hipk, M, N, K):
+    """Tuned hipBLASLt GEMM (csrc/kernels/gemm_lt.cpp): the measured-best
+    solution, replayed through ops.linear and inside a hipGraph, matches an
+    fp32 x @ w.T."""
+    from drtc_amd.ops import gemm
+
+    torch.manual_seed(1)
+    r = gemm.tune(M, N, K, torch.device(DEV), iters=3, max_candidates=4)
+    assert r["algo"] >= 0 and r["us"] > 0 and r["candidates"] >= 1, r
+    assert hipk.lt_set_algo(M, N, K, K, N, r["algo"]) == 0
+    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=DEV) * 0.05).to(torch.bfloat16)
+    ref = x.float() @ w.float().t()
+    saved = gemm._table
+    try:
+        gemm._table = {(M, N, K, K): r["algo"]}
+        y = ops.linear(x, w)
+        _close(y, ref, 2e-2, 2e-2, "tuned linear")
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            yg = ops.linear(x, w)
+        x.copy_(torch.randn(M, K, device=DEV).to(torch.bfloat16))
+        g.replay()
+        torch.cuda.synchronize()
+        _close(yg, x.float() @ w.float().t(), 2e-2, 2e-2, "tuned linear (graph)")
+    finally:
+        gemm._table = saved
