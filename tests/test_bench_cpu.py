@@ -1,0 +1,52 @@
+"""bench.py's driver contract on CPU (gloo): one JSON line from rank 0 with the
+whole-job value, max-over-ranks timing and DP global batch."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ARGS = ["--steps", "1", "--warmup", "0", "--model", "tiny-llama", "--batch", "4",
+        "--max-new-tokens", "4", "--max-model-len", "1024"]
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _json_line(out: str) -> dict:
+    lines = [ln for ln in out.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out
+    return json.loads(lines[0])
+
+
+def _check(r: dict, n: int) -> None:
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+              "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config"):
+        assert k in r, k
+    assert r["n_gpus"] == n and r["steps"] == 1 and r["warmup"] == 0
+    assert r["value"] > 0 and r["higher_is_better"] is True and r["scaling"] == "weak"
+    assert r["config"]["global_batch"] == 4 * n
+    assert r["config"]["parallelism"] == f"dp{n}"
+    # value is the whole-job aggregate: generated tokens of every rank / max time
+    assert abs(r["value"] - 4 * n * 4 / (r["ms_per_step"] / 1000)) / r["value"] < 0.05
+
+
+def test_bench_single_process():
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *ARGS], cwd=ROOT,
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-2000:]
+    _check(_json_line(p.stdout), 1)
+
+
+def test_bench_two_ranks_gloo():
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(ROOT, "bench.py"), "--gpus", "2", *ARGS]
+    p = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-2000:]
+    _check(_json_line(p.stdout), 2)
