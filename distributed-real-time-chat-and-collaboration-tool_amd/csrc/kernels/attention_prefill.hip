@@ -167,6 +167,220 @@ __global__ __launch_bounds__(256) void prefill_attn_kernel(
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// v2: GQA-grouped, double-buffered, transposed-read V.
+//
+// One workgroup = one 64-row query tile x GH query heads that share a KV head
+// (4 waves per head, 16 rows per wave): each K/V tile is fetched from HBM and
+// staged in LDS ONCE for the GH heads instead of once per head.  Staging is
+// split issue-early / write-late (the next tile's global loads are in flight
+// during this tile's MFMAs; double-buffered LDS, one barrier per tile).  V is
+// staged row-major exactly as loaded (16-B ds_write) and read as the P.V
+// A-operand with ds_read_b64_tr_b16 (CDNA4 hardware transpose: lanes 4q+p of a
+// 16-lane group address row q / columns 4p..4p+3, lane i receives column i).
+// Row paddings: K rows D+8 (conflict-free ds_read_b128), V rows D+16 (the 8
+// rows of one tr-read half land on distinct bank octets).
+template <int D, int GH>
+struct PrefillV2Lds {
+  static constexpr int KROW = D + 8;
+  static constexpr int VROW = D + 16;
+  static constexpr int K_ELEMS = kKT * KROW;
+  static constexpr int V_ELEMS = kKT * VROW;
+  static constexpr int BUF = K_ELEMS + V_ELEMS;  // one stage
+  static constexpr size_t BYTES = (size_t)2 * BUF * 2;
+};
+
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+
+DRTC_DEVICE bf16x4 lds_read_tr16(const bf16_t* p) {
+  s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) s16x4*)(p));
+  return __builtin_bit_cast(bf16x4, v);
+}
+
+template <int D, int GH>
+__global__ __launch_bounds__(256 * GH) void prefill_attn_v2_kernel(
+    bf16_t* __restrict__ out, int out_stride, const bf16_t* __restrict__ qkv,
+    int qkv_stride, int Hq, int Hkv, const int* __restrict__ cu_seqlens,
+    const int* __restrict__ tile_seq, const int* __restrict__ tile_q0,
+    float scale_log2e, int causal) {
+  using L = PrefillV2Lds<D, GH>;
+  constexpr int NTHR = 256 * GH;
+  constexpr int KS = D / 32;
+  constexpr int NT = D / 16;
+  constexpr int VPR = D / 8;                 // 16-B vectors per K/V row
+  constexpr int NV = kKT * VPR / NTHR;       // vectors per thread per operand
+  static_assert(NV >= 1 && (kKT * VPR) % NTHR == 0, "staging split");
+  extern __shared__ __attribute__((aligned(16))) bf16_t lds[];
+
+  const int tile = blockIdx.x;
+  const int G = Hq / Hkv;
+  const int groups = G / GH;
+  const int hk = blockIdx.y / groups;
+  const int hq0 = hk * G + (blockIdx.y - hk * groups) * GH;
+  const int w = wave_id_uniform();
+  const int hq = hq0 + (w >> 2);
+  const int seq = tile_seq[tile];
+  const int q0 = tile_q0[tile];
+  const int s_begin = cu_seqlens[seq];
+  const int seqlen = cu_seqlens[seq + 1] - s_begin;
+  const int lane = threadIdx.x & 63;
+  const int col = lane & 15, g = lane >> 4;
+  const int qrow = q0 + 16 * (w & 3) + col;
+  const int k_off = (Hq + hk) * D;
+  const int v_off = (Hq + Hkv + hk) * D;
+  const int kv_end = causal ? min(seqlen, q0 + kQT) : seqlen;
+  const int ntiles = (kv_end + kKT - 1) / kKT;
+
+  bf16x8 kr[NV], vr[NV];
+  auto issue = [&](int k0) {
+#pragma unroll
+    for (int n = 0; n < NV; ++n) {
+      const int v = threadIdx.x + n * NTHR;
+      const int key = v / VPR;
+      const int c = (v - key * VPR) * 8;
+      if (k0 + key < seqlen) {
+        const bf16_t* rp = qkv + (int64_t)(s_begin + k0 + key) * qkv_stride;
+        kr[n] = load_bf16x8(rp + k_off + c);
+        vr[n] = load_bf16x8(rp + v_off + c);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { kr[n][j] = f2bf(0.f); vr[n][j] = f2bf(0.f); }
+      }
+    }
+  };
+  auto commit = [&](bf16_t* kb) {
+#pragma unroll
+    for (int n = 0; n < NV; ++n) {
+      const int v = threadIdx.x + n * NTHR;
+      const int key = v / VPR;
+      const int c = (v - key * VPR) * 8;
+      store_bf16x8(kb + key * L::KROW + c, kr[n]);
+      store_bf16x8(kb + L::K_ELEMS + key * L::VROW + c, vr[n]);
+    }
+  };
+
+  issue(0);
+  bf16x8 qf[KS];
+  {
+    const bf16_t* qp = qkv + (int64_t)(s_begin + qrow) * qkv_stride + hq * D;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      if (qrow < seqlen) qf[s] = load_bf16x8(qp + 32 * s + 8 * g);
+      else for (int j = 0; j < 8; ++j) qf[s][j] = f2bf(0.f);
+    }
+  }
+  f32x4 o[NT];
+#pragma unroll
+  for (int i = 0; i < NT; ++i) o[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  float m = kNegBig, lsum = 0.f;
+  // tr-read lane address within a 16-lane group: row q = (lane&15)>>2, cols 4p
+  const int tr_off = ((col >> 2) + 4 * g) * L::VROW + 4 * (col & 3);
+
+  for (int kt = 0; kt < ntiles; ++kt) {
+    bf16_t* kb = lds + (kt & 1) * L::BUF;
+    const bf16_t* vb = kb + L::K_ELEMS;
+    commit(kb);
+    __syncthreads();
+    if (kt + 1 < ntiles) issue((kt + 1) * kKT);
+    const int k0 = kt * kKT;
+
+    f32x4 sc[4];
+#pragma unroll
+    for (int st = 0; st < 4; ++st) {
+      sc[st] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        bf16x8 a = load_bf16x8(kb + (16 * st + col) * L::KROW + 32 * s + 8 * g);
+        sc[st] = mfma16(a, qf[s], sc[st]);
+      }
+    }
+    float bmax = kNegBig;
+#pragma unroll
+    for (int st = 0; st < 4; ++st)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = k0 + 16 * st + 4 * g + r;
+        const bool ok = key < seqlen && (!causal || key <= qrow);
+        sc[st][r] = ok ? sc[st][r] * scale_log2e : kNegBig;
+        bmax = fmaxf(bmax, sc[st][r]);
+      }
+    bmax = fmaxf(bmax, __shfl_xor(bmax, 16, 64));
+    bmax = fmaxf(bmax, __shfl_xor(bmax, 32, 64));
+    const float m_new = fmaxf(m, bmax);
+    const float alpha = fast_exp2(m - m_new);
+    m = m_new;
+    bf16x8 pf[2];
+    float psum = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float pa = fast_exp2(sc[2 * ks][r] - m_new);
+        const float pb = fast_exp2(sc[2 * ks + 1][r] - m_new);
+        psum += pa + pb;
+        pf[ks][r] = f2bf(pa);
+        pf[ks][4 + r] = f2bf(pb);
+      }
+    lsum = lsum * alpha + psum;
+#pragma unroll
+    for (int i = 0; i < NT; ++i) {
+      o[i] *= alpha;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const bf16x4 lo = lds_read_tr16(vb + tr_off + 32 * ks * L::VROW + 16 * i);
+        const bf16x4 hi = lds_read_tr16(vb + tr_off + (32 * ks + 16) * L::VROW + 16 * i);
+        bf16x8 a;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { a[j] = lo[j]; a[4 + j] = hi[j]; }
+        o[i] = mfma16(a, pf[ks], o[i]);
+      }
+    }
+  }
+  lsum += __shfl_xor(lsum, 16, 64);
+  lsum += __shfl_xor(lsum, 32, 64);
+  if (qrow < seqlen) {
+    const float inv = 1.f / lsum;
+    bf16_t* op = out + (int64_t)(s_begin + qrow) * out_stride + hq * D + 4 * g;
+#pragma unroll
+    for (int i = 0; i < NT; ++i) {
+      bf16x4 v;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = f2bf(o[i][r] * inv);
+      *reinterpret_cast<bf16x4*>(op + 16 * i) = v;
+    }
+  }
+}
+
+template <int D, int GH>
+static void launch_v2(dim3 grid, hipStream_t st, bf16_t* out, int out_stride, const bf16_t* qkv,
+                      int qkv_stride, int Hq, int Hkv, const int* cu, const int* ts,
+                      const int* tq, float sl2, int causal) {
+  constexpr size_t lds_bytes = PrefillV2Lds<D, GH>::BYTES;
+  prefill_attn_v2_kernel<D, GH><<<grid, dim3(256 * GH), lds_bytes, st>>>(
+      out, out_stride, qkv, qkv_stride, Hq, Hkv, cu, ts, tq, sl2, causal);
+}
+
+template <int D>
+static int launch_v2_gh(int GH, int ntiles, int Hq, int Hkv, hipStream_t st, bf16_t* out,
+                        int out_stride, const bf16_t* qkv, int qkv_stride, const int* cu,
+                        const int* ts, const int* tq, float sl2, int causal) {
+  dim3 grid(ntiles, Hq / GH);
+  switch (GH) {
+    case 1: launch_v2<D, 1>(grid, st, out, out_stride, qkv, qkv_stride, Hq, Hkv, cu, ts, tq, sl2, causal); break;
+    case 2: launch_v2<D, 2>(grid, st, out, out_stride, qkv, qkv_stride, Hq, Hkv, cu, ts, tq, sl2, causal); break;
+    case 4:
+      if constexpr (D == 128) {
+        launch_v2<D, 4>(grid, st, out, out_stride, qkv, qkv_stride, Hq, Hkv, cu, ts, tq, sl2, causal);
+        break;
+      }
+      return -1;
+    default: return -1;
+  }
+  return 0;
+}
+
 int launch_prefill_attn(void* out, int out_stride, const void* qkv,
                         int qkv_stride, int Hq, int Hkv, int D,
                         const int* cu_seqlens, const int* tile_seq,
@@ -175,6 +389,26 @@ int launch_prefill_attn(void* out, int out_stride, const void* qkv,
   if (ntiles == 0) return 0;
   if (Hkv <= 0 || Hq % Hkv != 0) return -1;
   const float sl2 = scale * kLog2e;
+  static const int v1 = getenv("DRTC_PREFILL_ATTN_V1") != nullptr;
+  if (!v1) {
+    const int G = Hq / Hkv;
+    // heads per workgroup: 4 for D=128 (1024 threads), 2 for D=64 (one
+    // 16-B K and V vector per thread) and D=256 (VGPR budget)
+    const int gh_max = D == 128 ? 4 : 2;
+    const int GH = gh_max <= G ? gh_max : (G >= 2 ? 2 : 1);
+    if (G % GH != 0) return -1;
+    const bf16_t* q = (const bf16_t*)qkv;
+    bf16_t* o = (bf16_t*)out;
+    int rc;
+    switch (D) {
+      case 64: rc = launch_v2_gh<64>(GH, ntiles, Hq, Hkv, st, o, out_stride, q, qkv_stride, cu_seqlens, tile_seq, tile_q0, sl2, causal); break;
+      case 128: rc = launch_v2_gh<128>(GH, ntiles, Hq, Hkv, st, o, out_stride, q, qkv_stride, cu_seqlens, tile_seq, tile_q0, sl2, causal); break;
+      case 256: rc = launch_v2_gh<256>(GH, ntiles, Hq, Hkv, st, o, out_stride, q, qkv_stride, cu_seqlens, tile_seq, tile_q0, sl2, causal); break;
+      default: return -1;
+    }
+    if (rc) return rc;
+    return (int)hipGetLastError();
+  }
   dim3 grid(ntiles, Hq), block(256);
   switch (D) {
     case 64:
@@ -192,10 +426,25 @@ int launch_prefill_attn(void* out, int out_stride, const void* qkv,
   return (int)hipGetLastError();
 }
 
-int configure_prefill() {
-  return (int)hipFuncSetAttribute((const void*)prefill_attn_kernel<256>,
+template <int D, int GH>
+static int set_lds() {
+  return (int)hipFuncSetAttribute((const void*)prefill_attn_v2_kernel<D, GH>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)PrefillLds<256>::BYTES);
+                                  (int)PrefillV2Lds<D, GH>::BYTES);
+}
+
+int configure_prefill() {
+  int e = (int)hipFuncSetAttribute((const void*)prefill_attn_kernel<256>,
+                                   hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)PrefillLds<256>::BYTES);
+  if (!e) e = set_lds<64, 1>();
+  if (!e) e = set_lds<64, 2>();
+  if (!e) e = set_lds<128, 1>();
+  if (!e) e = set_lds<128, 2>();
+  if (!e) e = set_lds<128, 4>();
+  if (!e) e = set_lds<256, 1>();
+  if (!e) e = set_lds<256, 2>();
+  return e;
 }
 
 }  // namespace drtc

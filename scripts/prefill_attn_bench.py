@@ -1,0 +1,63 @@
+#!/usr/bin/env python3
+"""Time the packed varlen prefill attention kernel on chat-shaped batches.
+
+Prints one JSON line per shape: us per call and effective TFLOP/s (causal
+FLOPs = 4 * sum(n^2)/2 * Hq * D).  Run with DRTC_PREFILL_ATTN_V1=1 in the
+environment to time the previous per-head kernel for an A/B comparison.
+"""
+import json
+import os
+import random
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+from drtc_amd import ops  # noqa: E402
+
+SHAPES = [  # (name, nseq, mean len, Hq, Hkv, D)
+    ("llama8b_smart_reply", 1024, 148, 32, 8, 128),
+    ("llama8b_summarize", 512, 432, 32, 8, 128),
+    ("llama8b_long", 16, 4096, 32, 8, 128),
+    ("gemma2b_smart_reply", 1024, 148, 8, 1, 256),
+    ("llama70b_ask", 256, 136, 64, 8, 128),
+]
+
+
+def main():
+    dev = torch.device("cuda")
+    rng = random.Random(0)
+    variant = "v1" if os.environ.get("DRTC_PREFILL_ATTN_V1") else "v2"
+    for name, nseq, mean, Hq, Hkv, D in SHAPES:
+        lens = [max(8, int(rng.gauss(mean, mean * 0.1))) for _ in range(nseq)]
+        cu = [0]
+        for n in lens:
+            cu.append(cu[-1] + n)
+        T = cu[-1]
+        qkv = torch.randn(T, (Hq + 2 * Hkv) * D, device=dev).to(torch.bfloat16)
+        cu_d = torch.tensor(cu, dtype=torch.int32, device=dev)
+        ts, tq = ops.prefill_tiles(cu)
+        tiles = (torch.tensor(ts, dtype=torch.int32, device=dev),
+                 torch.tensor(tq, dtype=torch.int32, device=dev))
+        out = torch.empty(T, Hq * D, device=dev, dtype=torch.bfloat16)
+        f = lambda: ops.prefill_attention(qkv, cu_d, Hq, Hkv, D, D ** -0.5, True, tiles=tiles,
+                                          cu_host=cu, out=out)
+        for _ in range(3):
+            f()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        it = 20
+        e0.record()
+        for _ in range(it):
+            f()
+        e1.record()
+        torch.cuda.synchronize()
+        us = 1000 * e0.elapsed_time(e1) / it
+        flops = 4 * sum(n * (n + 1) / 2 for n in lens) * Hq * D
+        print(json.dumps({"variant": variant, "shape": name, "tokens": T, "us": round(us, 1),
+                          "TFLOPs": round(flops / us / 1e6, 1)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
