@@ -166,7 +166,7 @@ def test_paged_decode_spike(hipk, variant):
     _close(out, ref, 2e-2, 2e-2)
 
 
-@pytest.mark.parametrize("D,Hq,Hkv", [(128, 32, 8), (256, 8, 1), (64, 4, 4)])
+@pytest.mark.parametrize("D,Hq,Hkv", [(128, 32, 8), (256, 8, 1), (64, 4, 4), (64, 8, 2), (128, 64, 8), (256, 4, 4)])
 @pytest.mark.parametrize("lens", [[1], [7, 64, 65, 200], [513, 3]])
 def test_prefill_attention(hipk, D, Hq, Hkv, lens):
     torch.manual_seed(2)
