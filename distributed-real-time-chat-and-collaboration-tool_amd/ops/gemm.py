@@ -10,7 +10,7 @@ through ``torch.nn.functional.linear``.
 Why a table: a decode GEMM has a small fixed M (the batch bucket) and
 model-fixed N/K, where hipBLASLt's heuristic pick can be far from the best
 listed solution - e.g. Llama-3-70B ``down`` at M=256: 312 us heuristic vs
-178 us tuned (profiles/r1g_gemm_tuning.md).  Tables are produced by
+178 us tuned (profiles/r1g_tuned_gemm_prefill_attn.md).  Tables are produced by
 ``scripts/tune_gemms.py`` on the GPU and keyed by the hipBLASLt version
 (solution indices are only valid for the library that listed them).
 """
@@ -28,15 +28,12 @@ from ._ext import check, hipk, on_gpu, stream_ptr
 TUNED_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuned")
 _lock = threading.Lock()
 _table: dict[tuple[int, int, int, int], int] | None = None  # (M, N, K, ldx) -> solution index
+_ready: set[tuple[int, int, int, int]] = set()               # entries with a native plan
 _enabled = os.environ.get("DRTC_TUNED_GEMM", "1") != "0"
 
 
 def table_path(arch: str = "gfx950") -> str:
     return os.path.join(TUNED_DIR, f"gemm_{arch}.json")
-
-
-def _key_str(M: int, N: int, K: int, ldx: int) -> str:
-    return f"{M},{N},{K},{ldx}"
 
 
 def load_table(path: str | None = None) -> dict:
@@ -49,8 +46,8 @@ def load_table(path: str | None = None) -> dict:
 
 
 def _activate() -> dict:
-    """Register every entry for the running hipBLASLt version with the native
-    plan cache (creates descriptors + workspace: must run outside capture)."""
+    """Parse the entries of the running hipBLASLt version (no GPU work; each
+    entry is registered with the native plan cache on its first use)."""
     global _table
     if _table is not None:
         return _table
@@ -59,14 +56,28 @@ def _activate() -> dict:
             return _table
         tab: dict[tuple[int, int, int, int], int] = {}
         if _enabled and torch.cuda.is_available():
-            h = hipk()
-            ver = str(h.lt_version())
+            ver = str(hipk().lt_version())
             for ks, e in load_table().get(ver, {}).items():
                 M, N, K, ldx = (int(v) for v in ks.split(","))
-                if h.lt_set_algo(M, N, K, ldx, N, int(e["algo"])) == 0:
-                    tab[(M, N, K, ldx)] = int(e["algo"])
+                tab[(M, N, K, ldx)] = int(e["algo"])
+        _ready.clear()
         _table = tab
     return _table
+
+
+def _plan(key: tuple[int, int, int, int]) -> bool:
+    """Register a table entry's solution with the native plan cache (first
+    use happens in the eager warm-up run that precedes each graph capture).
+    A stale entry (solution no longer supports the problem) is dropped."""
+    if key in _ready:
+        return True
+    M, N, K, ldx = key
+    with _lock:
+        if hipk().lt_set_algo(M, N, K, ldx, N, _table[key]) != 0:
+            _table.pop(key, None)
+            return False
+        _ready.add(key)
+    return True
 
 
 def reset() -> None:
@@ -88,7 +99,8 @@ def linear(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
             and w.dtype == torch.bfloat16 and x.stride(1) == 1 and w.is_contiguous()):
         M, K = x.shape
         N = w.shape[0]
-        if (M, N, K, x.stride(0)) in _activate():
+        key = (M, N, K, x.stride(0))
+        if key in _activate() and _plan(key):
             y = torch.empty((M, N), dtype=x.dtype, device=x.device)
             check(hipk().lt_gemm(y.data_ptr(), x.data_ptr(), w.data_ptr(), M, N, K, x.stride(0),
                                  N, stream_ptr(x)), "lt_gemm")
@@ -129,5 +141,4 @@ def save_entries(entries: dict[str, dict], path: str | None = None) -> str:
     return path
 
 
-__all__ = ["linear", "tune", "save_entries", "load_table", "reset", "set_enabled", "table_path",
-           "_key_str"]
+__all__ = ["linear", "tune", "save_entries", "load_table", "reset", "set_enabled", "table_path"]
