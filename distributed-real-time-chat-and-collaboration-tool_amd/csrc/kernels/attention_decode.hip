@@ -18,7 +18,8 @@
 //   The S^T accumulators of the two 16-token halves of a block are fed back
 //   as the P^T B-operand with NO lane movement: lane l (g = l>>4) holds tokens
 //   {4g..4g+3} and {16+4g..16+4g+3}; the V^T A-operand is loaded with the
-//   same token permutation from the dim-major V block (two 8-B loads).
+//   same token permutation from the V block, stored as 8 groups of 4 tokens,
+//   dim-major inside a group (two 8-B loads, 128-B coalesced per d-tile).
 //   Columns are query heads: G <= 16 (Llama-3 4, 70B 8, Gemma-2B 8).
 #include "common.h"
 #include "launchers.h"
@@ -42,11 +43,13 @@ DRTC_DEVICE void load_kv_block(KVRegs<D>& r, const bf16_t* kb, const bf16_t* vb,
     r.k0[s] = load_bf16x8(kb + t * D + 32 * s + 8 * g);
     r.k1[s] = load_bf16x8(kb + (16 + t) * D + 32 * s + 8 * g);
   }
+  // V block = 8 groups of 4 tokens, each group dim-major [D][4] (kv_cache.py):
+  // tokens 4g..4g+3 of row d are 8 contiguous bytes, and the 16 rows of one
+  // d-tile are 128 contiguous bytes.
 #pragma unroll
   for (int i = 0; i < D / 16; ++i) {
-    const bf16_t* vrow = vb + (16 * i + t) * kBS;
-    r.vlo[i] = load_bf16x4(vrow + 4 * g);
-    r.vhi[i] = load_bf16x4(vrow + 16 + 4 * g);
+    r.vlo[i] = load_bf16x4(vb + g * (4 * D) + (16 * i + t) * 4);
+    r.vhi[i] = load_bf16x4(vb + (4 + g) * (4 * D) + (16 * i + t) * 4);
   }
 }
 

@@ -216,9 +216,11 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(
     const int h = item / (D / 8);
     const int c = (item - h * (D / 8)) * 8;
     bf16x8 v = load_bf16x8(row + (Hq + Hkv + h) * D + c);
-    bf16_t* vd = v_cache + ((blk * Hkv + h) * D + c) * block_size + off;
+    // V block layout: [block_size/4 groups][D][4 tokens] (see kv_write_v)
+    bf16_t* vd = v_cache + (blk * Hkv + h) * D * block_size + (off >> 2) * (4 * D) + c * 4 +
+                 (off & 3);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) vd[j * block_size] = v[j];
+    for (int j = 0; j < 8; ++j) vd[4 * j] = v[j];
   }
 }
 
@@ -245,11 +247,15 @@ int launch_rope_kv(void* qkv, int T, int qkv_stride, const int* positions,
 }
 
 // ------------------------------------------- prefill V write (transposed)
-// The decode kernel wants V dim-major inside each 32-token cache block.  A
-// per-token kernel would emit D scattered 2-byte stores per head; in prefill
-// a whole block's tokens are contiguous rows of the QKV buffer, so one
-// workgroup per (block segment, kv head) stages the [32][D] tile in LDS and
-// writes the [D][32] block with 16-byte stores (rows of 8 tokens).
+// V cache block layout (per kv head): 8 groups of 4 tokens, each group
+// dim-major [D][4] - the decode kernel's P.V operand wants 4 consecutive
+// tokens of one dim in 8 contiguous bytes, and a decode-time write of ONE
+// token then touches D 8-byte slots inside a 2*D-byte span (a plain [D][32]
+// dim-major block scatters it over D separate 64-B rows: ~8x the HBM write
+// traffic).  In prefill a whole block's tokens are contiguous rows of the
+// QKV buffer, so one workgroup per (block segment, kv head) stages the
+// [32][D] tile in LDS and writes the block with 16-byte stores (two dims x
+// 4 tokens each).
 template <int D>
 __global__ __launch_bounds__(256) void kv_write_v_kernel(
     bf16_t* __restrict__ v_cache, const bf16_t* __restrict__ qkv, int qkv_stride,
@@ -272,12 +278,12 @@ __global__ __launch_bounds__(256) void kv_write_v_kernel(
   }
   __syncthreads();
   bf16_t* dst = v_cache + (blk * Hkv + h) * (int64_t)D * BS;
-  for (int v = threadIdx.x; v < D * (BS / 8); v += 256) {
-    const int d = v / (BS / 8), g = (v - d * (BS / 8)) * 8;
+  for (int v = threadIdx.x; v < (BS / 4) * (D / 2); v += 256) {
+    const int q4 = v / (D / 2), d = (v - q4 * (D / 2)) * 2;
     bf16x8 y;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) y[j] = tile[(g + j) * ROW + d];
-    store_bf16x8(dst + d * BS + g, y);
+    for (int j = 0; j < 8; ++j) y[j] = tile[(4 * q4 + (j & 3)) * ROW + d + (j >> 2)];
+    store_bf16x8(dst + q4 * (4 * D) + d * 4, y);
   }
 }
 

@@ -2,7 +2,9 @@
 
 One contiguous allocation per engine, carved into per-layer views:
   k[layer] : [num_blocks, Hkv, 32, D]   token-major (MFMA A-operand rows)
-  v[layer] : [num_blocks, Hkv, D, 32]   dim-major  (P.V A-operand rows)
+  v[layer] : [num_blocks, Hkv, D, 32]   storage shape; a block holds 8 groups
+             of 4 tokens, dim-major inside a group (P.V A-operand: 4 tokens of
+             one dim = 8 contiguous bytes; a decode write spans 2*D bytes)
 The block count is derived from the free HBM left after the weights
 (``torch.cuda.mem_get_info``) times ``kv_fraction``; on a 288 GB MI355X with
 Llama-3-8B that is ~1.5 M cached tokens.  Blocks are handed out by the

@@ -10,6 +10,7 @@ import os
 import torch
 
 from ._ext import check, hipk, on_gpu, ptr, stream_ptr
+from .rope import v_block_tokens
 
 KV_BLOCK = 32  # tokens per cache block (fixed by the decode kernel)
 PREFILL_QTILE = 64
@@ -126,7 +127,8 @@ def paged_decode_ref(q, k_cache, v_cache, block_tables, context_lens, scale):
         nblk = (ctx + bs - 1) // bs
         blocks = block_tables[b, :nblk].long()
         k = k_cache[blocks].permute(1, 0, 2, 3).reshape(Hkv, nblk * bs, D)[:, :ctx].float()
-        v = v_cache[blocks].permute(1, 0, 3, 2).reshape(Hkv, nblk * bs, D)[:, :ctx].float()
+        v = v_block_tokens(v_cache[blocks]).permute(1, 0, 2, 3).reshape(Hkv, nblk * bs, D)
+        v = v[:, :ctx].float()
         qh = q[b].reshape(Hkv, G, D).float()
         s = torch.einsum("hgd,htd->hgt", qh, k) * scale
         p = torch.softmax(s, dim=-1)

@@ -4,7 +4,9 @@ HIP kernel: csrc/kernels/norm_act_rope.hip (rope_kv_kernel).
 
 KV-cache layout (per layer):
   k_cache [num_blocks, Hkv, block_size, D]   token-major rows
-  v_cache [num_blocks, Hkv, D, block_size]   dim-major (transposed) rows
+  v_cache [num_blocks, Hkv, D, block_size]   storage shape; inside a block the
+      tokens are 8 groups of 4, dim-major within a group ([8][D][4], see
+      ``v_block_tokens`` / ``v_block_storage`` and csrc/kernels/norm_act_rope.hip)
 """
 from __future__ import annotations
 
@@ -41,6 +43,21 @@ def build_rope_cache(max_pos: int, head_dim: int, theta: float,
     return table.to(device) if device is not None else table
 
 
+V_GROUP = 4  # tokens per dim-major group of a V cache block
+
+
+def v_block_tokens(vb: torch.Tensor) -> torch.Tensor:
+    """V cache blocks [..., D, bs] (storage) -> token-major [..., bs, D]."""
+    *lead, D, bs = vb.shape
+    return vb.reshape(*lead, bs // V_GROUP, D, V_GROUP).transpose(-1, -2).reshape(*lead, bs, D)
+
+
+def v_block_storage(v: torch.Tensor) -> torch.Tensor:
+    """Token-major [..., bs, D] -> V cache block storage [..., D, bs]."""
+    *lead, bs, D = v.shape
+    return v.reshape(*lead, bs // V_GROUP, V_GROUP, D).transpose(-1, -2).reshape(*lead, D, bs)
+
+
 def rope_kv_ref(qkv, positions, slots, cos_sin, Hq, Hkv, D, k_cache, v_cache, block_size):
     T = qkv.shape[0]
     nh = Hq + Hkv
@@ -60,7 +77,9 @@ def rope_kv_ref(qkv, positions, slots, cos_sin, Hq, Hkv, D, k_cache, v_cache, bl
         v = qkv[:, nh * D:(nh + Hkv) * D].reshape(T, Hkv, D)[valid]
         k_cache[blk, :, off, :] = k
         if v_cache is not None:
-            v_cache[blk, :, :, off] = v
+            nb, hkv, d, bs = v_cache.shape
+            vg = v_cache.view(nb, hkv, bs // V_GROUP, d, V_GROUP)
+            vg[blk, :, torch.div(off, V_GROUP, rounding_mode="floor"), :, off % V_GROUP] = v
     return qkv
 
 
@@ -68,9 +87,9 @@ def kv_write_v_ref(v_cache, qkv, seg_tok, seg_len, seg_blk, Hq, Hkv, D):
     bs = v_cache.shape[-1]
     for t0, n, b in zip(seg_tok.tolist(), seg_len.tolist(), seg_blk.tolist()):
         v = qkv[t0:t0 + n, (Hq + Hkv) * D:(Hq + 2 * Hkv) * D].reshape(n, Hkv, D)
-        blk = torch.zeros(Hkv, D, bs, dtype=v_cache.dtype, device=v_cache.device)
-        blk[:, :, :n] = v.permute(1, 2, 0)
-        v_cache[b] = blk
+        blk = torch.zeros(Hkv, bs, D, dtype=v_cache.dtype, device=v_cache.device)
+        blk[:, :n] = v.permute(1, 0, 2)
+        v_cache[b] = v_block_storage(blk)
 
 
 def kv_write_v(v_cache: torch.Tensor, qkv: torch.Tensor, segs, Hq: int, Hkv: int, D: int) -> None:

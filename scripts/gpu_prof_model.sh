@@ -19,7 +19,8 @@ echo "prof rc=$rc"
 cd "$R"
 T=$(find gpurun_out/prof_$TAG -name '*kernel_trace.csv' | head -1)
 S=$(find gpurun_out/prof_$TAG -name '*kernel_stats.csv' | head -1)
-[ -n "$T" ] && python scripts/prof_summary.py "$T" --top 20 > gpurun_out/${TAG}_summary.md
+[ -n "$T" ] && python scripts/prof_summary.py "$T" --top 20 > gpurun_out/${TAG}_summary.md && python scripts/prof_summary.py "$T" --top 25 --full-only > gpurun_out/${TAG}_summary_full.md
 [ -n "$S" ] && cp "$S" gpurun_out/${TAG}_kernel_stats.csv
+[ -n "$T" ] && gzip -c "$T" > gpurun_out/${TAG}_kernel_trace.csv.gz
 rm -rf gpurun_out/prof_$TAG
 exit $rc

@@ -7,7 +7,11 @@ prefill attention kernel) or decode (paged decode attention).  Prints, per
 phase: passes, mean GPU wall per pass, mean busy time per pass, and the
 per-kernel breakdown (shortened names) - a markdown table for profiles/.
 
-usage: prof_summary.py run_kernel_trace.csv [--top 15]
+usage: prof_summary.py run_kernel_trace.csv [--top 15] [--full-only]
+
+--full-only keeps, per phase, only the passes whose kernel-busy time is at
+least 80 % of the phase's largest pass (drops the graph-capture warm-up
+passes of the small batch buckets, so decode rows describe the full batch).
 """
 import collections
 import csv
@@ -36,7 +40,8 @@ def main():
     path = sys.argv[1]
     top = int(sys.argv[sys.argv.index("--top") + 1]) if "--top" in sys.argv else 15
     rows = []
-    with open(path) as f:
+    opener = __import__("gzip").open if path.endswith(".gz") else open
+    with opener(path, "rt") as f:
         for r in csv.DictReader(f):
             rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"])))
     rows.sort()
@@ -47,28 +52,43 @@ def main():
         if r[2] == "drtc::sample_kernel":
             passes.append(cur)
             cur = []
+    full_only = "--full-only" in sys.argv
     phase_k = {"prefill": collections.Counter(), "decode": collections.Counter()}
     phase_n = collections.Counter()
     phase_wall = collections.Counter()
     phase_busy = collections.Counter()
-    for p in passes:
+    phase_cnt = collections.Counter()
+    def phase_of(p):
         names = {x[2] for x in p}
-        ph = ("prefill" if "drtc::prefill_attn_kernel" in names else
-              "decode" if "drtc::paged_decode_kernel" in names else None)
+        if any("distribution_" in n for n in names):
+            return None  # random weight init before the first forward
+        return ("prefill" if "drtc::prefill_attn_kernel" in names else
+                "decode" if "drtc::paged_decode_kernel" in names else None)
+
+    busy_max = collections.Counter()
+    for p in passes:
+        ph = phase_of(p)
+        if ph:
+            busy_max[ph] = max(busy_max[ph], sum(e - s for s, e, _ in p))
+    for p in passes:
+        ph = phase_of(p)
         if ph is None:
+            continue
+        if full_only and sum(e - s for s, e, _ in p) < 0.8 * busy_max[ph]:
             continue
         # drop leading non-forward kernels (copies etc. are not kernels here)
         phase_n[ph] += 1
+        phase_cnt[ph] += len(p)
         phase_wall[ph] += p[-1][1] - p[0][0]
         for s, e, n in p:
             phase_k[ph][n] += e - s
             phase_busy[ph] += e - s
-    print("| phase | passes | mean GPU wall / pass (ms) | mean kernel-busy / pass (ms) |")
-    print("|---|---|---|---|")
+    print("| phase | passes | mean GPU wall / pass (ms) | mean kernel-busy / pass (ms) | kernels / pass |")
+    print("|---|---|---|---|---|")
     for ph in ("prefill", "decode"):
         if phase_n[ph]:
             print(f"| {ph} | {phase_n[ph]} | {phase_wall[ph] / phase_n[ph] / 1e6:.3f} | "
-                  f"{phase_busy[ph] / phase_n[ph] / 1e6:.3f} |")
+                  f"{phase_busy[ph] / phase_n[ph] / 1e6:.3f} | {phase_cnt[ph] / phase_n[ph]:.0f} |")
     for ph in ("prefill", "decode"):
         if not phase_n[ph]:
             continue

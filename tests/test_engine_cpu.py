@@ -109,6 +109,34 @@ def test_reference_ops_consistency():
     assert (dec.reshape(1, -1).float() - pre[-1:].float()).abs().max() < 0.02
 
 
+def test_v_cache_block_layout():
+    """V blocks are 8 groups of 4 tokens, dim-major inside a group: the
+    per-token (decode) write and the whole-block (prefill) write agree, and
+    the storage <-> token-major helpers are inverse."""
+    from drtc_amd.ops.rope import v_block_storage, v_block_tokens
+
+    torch.manual_seed(1)
+    Hq, Hkv, D, bs = 2, 2, 64, ops.KV_BLOCK
+    n = 45
+    qkv = torch.randn(n, (Hq + 2 * Hkv) * D).to(torch.bfloat16)
+    v = qkv[:, (Hq + Hkv) * D:].reshape(n, Hkv, D)
+    vc_tok = torch.zeros(3, Hkv, D, bs, dtype=torch.bfloat16)
+    kc = torch.zeros(3, Hkv, bs, D, dtype=torch.bfloat16)
+    ops.rope_kv_ref(qkv.clone(), torch.zeros(n, dtype=torch.int32), torch.arange(n) + bs,
+                    ops.build_rope_cache(8, D, 1e4), Hq, Hkv, D, kc, vc_tok, bs)
+    vc_blk = torch.zeros_like(vc_tok)
+    segs = (torch.tensor([0, bs]), torch.tensor([bs, n - bs]), torch.tensor([1, 2]))
+    ops.kv_write_v_ref(vc_blk, qkv, *segs, Hq, Hkv, D)
+    assert torch.equal(vc_tok, vc_blk)
+    tok = v_block_tokens(vc_blk[1:])                      # [2, Hkv, bs, D]
+    assert torch.equal(tok.permute(1, 0, 2, 3).reshape(Hkv, 2 * bs, D)[:, :n], v.transpose(0, 1))
+    assert torch.equal(v_block_storage(tok), vc_blk[1:])
+    # raw storage order: token t of dim d sits at (t // 4) * 4D + 4d + t % 4
+    flat = vc_blk[1, 0].reshape(-1)
+    for t, d in [(0, 0), (5, 3), (31, 63), (17, 40)]:
+        assert flat[(t // 4) * 4 * D + 4 * d + t % 4] == v[t, 0, d]
+
+
 def test_rope_llama3_scaling_and_sampler_ref():
     t = ops.build_rope_cache(16, 128, 5e5, {"rope_type": "llama3", "factor": 8.0, "low_freq_factor": 1.0,
                                            "high_freq_factor": 4.0, "original_max_position_embeddings": 8192})
