@@ -54,12 +54,13 @@ def main():
     shapes = SHAPES_70B if a.model == "70b" else SHAPES
     W = {k: torch.randn(n, kk, device=dev, dtype=torch.bfloat16) * 0.02 for k, (n, kk) in shapes.items()}
     H, inter = shapes["o"][0], shapes["down"][1]
+    wts = {}
     for mode in a.modes.split(","):
         if mode == "rocblas":
             torch.backends.cuda.preferred_blas_library("cublas")
         else:
             torch.backends.cuda.preferred_blas_library("cublaslt")
-        if mode == "tunable":
+        if mode in ("tunable", "nn_tunable"):
             torch.cuda.tunable.enable(True)
             torch.cuda.tunable.tuning_enable(True)
             torch.cuda.tunable.set_max_tuning_duration(200)
@@ -76,6 +77,12 @@ def main():
                     torch.cuda.synchronize()
                 if mode == "transposed":  # out^T = W @ x^T (library sees M'=N, N'=M)
                     t = bench(lambda: torch.mm(w, inp.t()).t().contiguous())
+                elif mode in ("nn", "nn_tunable"):  # weights stored [K, N]: x @ Wt
+                    wt = wts.setdefault(name, w.t().contiguous())
+                    if mode == "nn_tunable":
+                        torch.mm(inp, wt)
+                        torch.cuda.synchronize()
+                    t = bench(lambda: torch.mm(inp, wt))
                 else:
                     t = bench(lambda: F.linear(inp, w))
                 n, k = w.shape

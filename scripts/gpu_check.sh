@@ -1,5 +1,6 @@
 #!/bin/bash
-# GPU-box validation: build, GPU tests, 1-GPU bench, rocprofv3 kernel stats.
+# GPU-box validation: build, GPU tests, smoke(), 1-GPU bench, rocprofv3 kernel stats
+# (SKIP_TESTS / SKIP_BENCH / SKIP_PROF=1 skip a step; PYTEST_ARGS / BENCH_ARGS / PROF_ARGS).
 # Each GPU step has its own time limit; a crash/timeout/abort ends the script.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -17,6 +18,9 @@ if [ "${SKIP_TESTS:-0}" != "1" ]; then
   if fatal $rc; then echo "pytest fatal rc=$rc"; exit $rc; fi
   echo "pytest rc=$rc"
 fi
+
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
+rc=$?; tail -2 gpurun_out/smoke.log; echo "smoke rc=$rc"; [ $rc -ne 0 ] && exit $rc
 
 if [ "${SKIP_BENCH:-0}" != "1" ]; then
   timeout -k 10 900 python bench.py ${BENCH_ARGS:-} > gpurun_out/bench.json 2> gpurun_out/bench.err
