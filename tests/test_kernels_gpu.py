@@ -327,3 +327,19 @@ def test_tuned_linear(hipk, M, N, K):
         _close(yg, x.float() @ w.float().t(), 2e-2, 2e-2, "tuned linear (graph)")
     finally:
         gemm._table = saved
+
+
+@pytest.mark.parametrize("e_off,e_local", [(0, 8), (2, 3)])
+def test_moe_sorted_library_path(hipk, e_off, e_local):
+    """Large eager MoE calls take the sorted per-expert hipBLASLt path."""
+    from drtc_amd.ops import moe as moe_ops
+
+    torch.manual_seed(5)
+    T, H, I, E, k = moe_ops.MOE_LIBRARY_MIN_TOKENS + 37, 256, 128, 8, 2
+    x = torch.randn(T, H, device=DEV).to(torch.bfloat16)
+    lg = torch.randn(T, E, device=DEV).to(torch.bfloat16)
+    wgu = (torch.randn(e_local, 2 * I, H, device=DEV) * 0.05).to(torch.bfloat16)
+    wdn = (torch.randn(e_local, H, I, device=DEV) * 0.05).to(torch.bfloat16)
+    out = ops.fused_moe(x, lg, wgu, wdn, k, num_experts=E, e_off=e_off)
+    ref = moe_ops.fused_moe_ref(x, lg, wgu, wdn, k, e_off=e_off)
+    _close(out, ref, 1e-2, 2e-2, "moe library path")
