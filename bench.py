@@ -75,6 +75,8 @@ def main() -> None:
     ap.add_argument("--tp", type=int, default=1, help="tensor-parallel degree (= WORLD_SIZE)")
     ap.add_argument("--trace", default=None, metavar="PATH",
                     help="record engine/graph spans (roctx + Chrome trace JSON at PATH)")
+    ap.add_argument("--kv-fraction", type=float, default=0.85,
+                    help="fraction of the free HBM (after weights) given to the paged KV cache")
     ap.add_argument("--custom-allreduce", action="store_true",
                     help="TP: one-shot IPC all-reduce for decode-sized messages (else RCCL)")
     args = ap.parse_args()
@@ -85,6 +87,7 @@ def main() -> None:
     rank, world = init_distributed()
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if torch.cuda.is_available():
+        local %= torch.cuda.device_count()  # several ranks per GPU only in rehearsals
         torch.cuda.set_device(local)
         device = torch.device("cuda", local)
     else:
@@ -107,7 +110,7 @@ def main() -> None:
     model = TransformerLM(cfg, device, pc=pc, seed=1234, full_then_shard=False)
     eng = LLMEngine(model, max_batch=args.batch, max_model_len=args.max_model_len,
                     max_prefill_tokens=max(16384, args.batch * 400),
-                    use_graphs=not args.no_graphs, seed=dp_rank)
+                    kv_fraction=args.kv_fraction, use_graphs=not args.no_graphs, seed=dp_rank)
     eng.warmup(capture=True)
     if device.type == "cuda":
         torch.cuda.synchronize()
@@ -174,7 +177,7 @@ def main() -> None:
     tps = gen / elapsed
     if rank == 0:
         out = {
-            "metric": METRIC if (args.workload, args.model) == ("smart_reply", "llama-3-8b") else
+            "metric": METRIC if (args.workload, args.model, tp) == ("smart_reply", "llama-3-8b", 1) else
             f"{args.workload} tokens/sec (whole node) + p50 latency, {cfg.name} TP={tp}",
             "value": round(tps, 1),
             "unit": "tokens/s",

@@ -33,11 +33,16 @@ def init_distributed(backend: str | None = None, device: torch.device | None = N
         return dist.get_rank(), dist.get_world_size()
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     if backend is None:
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        # DRTC_DIST_BACKEND=gloo rehearses multi-rank GPU code paths with
+        # several ranks on ONE GPU (RCCL refuses two ranks per device)
+        backend = os.environ.get("DRTC_DIST_BACKEND") or (
+            "nccl" if torch.cuda.is_available() else "gloo")
     kw = {}
     if backend == "nccl":
         torch.cuda.set_device(local)
         kw["device_id"] = torch.device("cuda", local)
+    elif torch.cuda.is_available():
+        torch.cuda.set_device(local % torch.cuda.device_count())
     dist.init_process_group(backend=backend, rank=rank, world_size=world, **kw)
     return rank, world
 
