@@ -180,7 +180,9 @@ std::vector<std::pair<int, float>> lt_tune(void* y, const void* x, const void* w
     hipEventElapsedTime(&ms, e0, e1);
     return 1000.f * ms / float(n);
   };
-  // index -1 = hipBLASLt's heuristic pick (the untuned baseline)
+  // index -1 = hipBLASLt's heuristic pick (the untuned baseline), timed after
+  // a warm-up run of the same length so clocks have ramped for every candidate
+  time_algo(nullptr, iters);
   out.emplace_back(-1, time_algo(nullptr, iters));
   // pass 1: every supported solution, a few iterations each
   std::vector<std::pair<float, size_t>> first;
