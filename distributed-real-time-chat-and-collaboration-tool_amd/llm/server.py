@@ -5,7 +5,8 @@ on-node inference:
 
   --backend engine   (default) random-init model on the local MI355X GPUs;
                      ``--gpus N`` runs N data-parallel engine replicas, one
-                     process per GPU, behind a least-outstanding router;
+                     process per GPU (also for N = 1, unless --in-process),
+                     behind a least-outstanding router with health checks;
                      ``--tp N`` runs one tensor-parallel engine over N GPUs
                      (RCCL all-reduce over xGMI), e.g. Llama-3-70B TP=8;
   --backend scripted deterministic format-correct text (no model; CPU tests).
@@ -46,10 +47,10 @@ def build_backend(args):
 
         return TPEngineGroup(args.model, args.tp, engine_kw, tok,
                              custom_allreduce=args.custom_allreduce)
-    n = args.gpus
-    if n <= 1:
-        import torch
+    import torch
 
+    n = args.gpus
+    if n <= 1 and (getattr(args, "in_process", False) or not torch.cuda.is_available()):
         from ..engine.engine import LLMEngine
         from ..models import TransformerLM
         from .backends import EngineBackend
@@ -61,7 +62,10 @@ def build_backend(args):
         return EngineBackend(eng, tok)
     from .backends import ReplicaRouter, WorkerPool
 
-    pool = WorkerPool(args.model, [f"cuda:{i}" for i in range(n)], engine_kw)
+    # engines run in their own processes (one per GPU), so the gRPC handlers,
+    # prompt building and tokenization here never contend for the engine
+    # loop's GIL (scripts/service_bench.py: in-process 16.4k vs 17.7k tok/s)
+    pool = WorkerPool(args.model, [f"cuda:{i}" for i in range(max(1, n))], engine_kw)
     return ReplicaRouter(pool, tok, args.max_model_len)
 
 
@@ -86,12 +90,17 @@ def main(argv=None):
     ap.add_argument("--max-batch", type=int, default=256)
     ap.add_argument("--max-model-len", type=int, default=4096)
     ap.add_argument("--no-graphs", action="store_true")
-    ap.add_argument("--workers", type=int, default=64)
+    ap.add_argument("--in-process", action="store_true",
+                    help="1 GPU: run the engine in the server process (default: a worker process)")
+    ap.add_argument("--workers", type=int, default=None,
+                    help="gRPC handler threads; each blocks on one generation (default: "
+                         "max-batch x replicas + 16, so the engine batch can fill)")
     ap.add_argument("--log-level", default="INFO")
     args = parse_with_config(ap, argv)
     setup_logging(args.log_level)
     backend = build_backend(args)
-    server = serve(backend, args.port, args.workers)
+    workers = args.workers or args.max_batch * max(1, args.gpus) + 16
+    server = serve(backend, args.port, workers)
     log.info("LLM server on port %d (backend=%s model=%s gpus=%d tp=%d)", args.port, args.backend,
              args.model, args.gpus, args.tp)
     stop = threading.Event()

@@ -1,12 +1,17 @@
 #!/bin/bash
 # Service-level load driver on Llama-3-8B: gRPC clients -> llm.LLMService
 # directly, and through the Raft leader (raft.RaftNode/GetSmartReply).
+# Clients run in 8 separate processes; "pool" keeps the engine in its own
+# process (the server process only does gRPC, prompts, tokenization, parsing).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export HSA_ENABLE_IPC_MODE_LEGACY=0
-python -c "import __graft_entry__ as g; g.build()" > gpurun_out/build.log 2>&1 || { tail -30 gpurun_out/build.log; exit 1; }
-timeout -k 10 600 python scripts/service_bench.py --model llama-3-8b --mode direct --requests 2048 --concurrency 1024 --max-batch 1024 > gpurun_out/service_direct.json 2> gpurun_out/service_direct.err
-rc=$?; tail -2 gpurun_out/service_direct.err; cut -c1-700 gpurun_out/service_direct.json; [ $rc -ne 0 ] && exit $rc
-timeout -k 10 600 python scripts/service_bench.py --model llama-3-8b --mode raft --requests 1024 --concurrency 512 --max-batch 1024 > gpurun_out/service_raft.json 2> gpurun_out/service_raft.err
-rc=$?; tail -2 gpurun_out/service_raft.err; cut -c1-700 gpurun_out/service_raft.json; [ $rc -ne 0 ] && exit $rc
+run() {  # tag, args
+  local tag=$1; shift
+  timeout -k 10 600 python scripts/service_bench.py --model llama-3-8b "$@" > gpurun_out/service_$tag.json 2> gpurun_out/service_$tag.err
+  local rc=$?; tail -2 gpurun_out/service_$tag.err; cut -c1-420 gpurun_out/service_$tag.json; echo; return $rc
+}
+run direct_inproc --mode direct --requests 2048 --concurrency 1024 --max-batch 1024 || exit 1
+run direct_pool --backend pool --client-procs 8 --mode direct --requests 2048 --concurrency 1024 --max-batch 1024 || exit 1
+run raft_pool --backend pool --client-procs 8 --mode raft --requests 2048 --concurrency 1024 --max-batch 1024 || exit 1

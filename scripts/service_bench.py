@@ -18,6 +18,7 @@ Reports one JSON line: requests/s, generated tokens/s, p50/p99 latency.
 """
 import argparse
 import json
+import multiprocessing as mp
 import os
 import random
 import statistics
@@ -32,7 +33,7 @@ import grpc  # noqa: E402
 
 from drtc_amd.llm.server import serve as serve_llm  # noqa: E402
 from drtc_amd.llm.service import FeatureParams  # noqa: E402
-from drtc_amd.protos import LLM_SERVICE, llm_pb, make_stub, raft_pb  # noqa: E402
+from drtc_amd.protos import LLM_SERVICE, RAFT_SERVICE, llm_pb, make_stub, raft_pb  # noqa: E402
 from drtc_amd.utils.cluster import LocalCluster, free_port  # noqa: E402
 from drtc_amd.utils.metrics import METRICS  # noqa: E402
 from drtc_amd.utils.synthetic import channel_history  # noqa: E402
@@ -42,6 +43,15 @@ def build_backend(args):
     if args.backend == "scripted":
         from drtc_amd.llm.backends import ScriptedBackend
         return ScriptedBackend(), None
+    if args.backend == "pool":  # engine in its own process (as llm/server.py runs N GPUs)
+        from drtc_amd.engine import ChatTokenizer
+        from drtc_amd.llm.backends import ReplicaRouter, WorkerPool
+        from drtc_amd.models import get_config
+
+        cfg = get_config(args.model)
+        pool = WorkerPool(args.model, ["cuda:0"], dict(max_batch=args.max_batch, max_model_len=2048))
+        tok = ChatTokenizer(cfg.vocab_size, cfg.bos_token_id, cfg.eos_token_id)
+        return ReplicaRouter(pool, tok, 2048), None
     import torch
 
     from drtc_amd.engine import ChatTokenizer, LLMEngine
@@ -58,9 +68,60 @@ def build_backend(args):
                                             cfg.eos_token_id)), eng
 
 
+def run_load(target, n_requests: int, threads: int, seed: int):
+    """``threads`` client threads issue ``n_requests`` GetSmartReply RPCs in
+    total; returns (latencies s, errors, wall start, wall end)."""
+    mode, address, token = target
+    rng = random.Random(seed)
+    if mode == "raft":
+        def one(stub):
+            r = stub.GetSmartReply(raft_pb.SmartReplyRequest(token=token, channel_id="general"),
+                                   timeout=120)
+            assert r.success and len(r.suggestions) == 3
+        stubs = [make_stub(grpc.insecure_channel(address), RAFT_SERVICE) for _ in range(8)]
+    else:
+        histories = [[llm_pb.Message(sender=m.sender, content=m.content)
+                      for m in channel_history(rng, 5)] for _ in range(64)]
+
+        def one(stub):
+            r = stub.GetSmartReply(llm_pb.SmartReplyRequest(
+                recent_messages=histories[rng.randrange(len(histories))]), timeout=120)
+            assert len(r.suggestions) == 3
+        stubs = [make_stub(grpc.insecure_channel(address), LLM_SERVICE) for _ in range(8)]
+    lat, errors, lock, it = [], [], threading.Lock(), iter(range(n_requests))
+
+    def worker(k):
+        stub = stubs[k % len(stubs)]
+        while True:
+            with lock:
+                if next(it, None) is None:
+                    return
+            t = time.perf_counter()
+            try:
+                one(stub)
+            except (grpc.RpcError, AssertionError) as e:
+                with lock:
+                    errors.append(repr(e)[:200])
+                continue
+            with lock:
+                lat.append(time.perf_counter() - t)
+    ths = [threading.Thread(target=worker, args=(k,)) for k in range(threads)]
+    t_start = time.time()
+    [t.start() for t in ths]
+    [t.join() for t in ths]
+    return lat, errors, t_start, time.time()
+
+
+def _client_main(target, n_requests, threads, seed, q):
+    q.put(run_load(target, n_requests, threads, seed))
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--backend", choices=("engine", "scripted"), default="engine")
+    ap.add_argument("--backend", choices=("engine", "pool", "scripted"), default="engine",
+                    help="engine: in-process engine; pool: engine in a worker process")
+    ap.add_argument("--client-procs", type=int, default=0,
+                    help="run the load clients in this many separate processes (0: threads here)")
     ap.add_argument("--model", default="llama-3-8b")
     ap.add_argument("--mode", choices=("direct", "raft"), default="direct")
     ap.add_argument("--requests", type=int, default=1024)
@@ -86,56 +147,41 @@ def main():
             for m in channel_history(rng, 5):
                 st.SendMessage(raft_pb.SendMessageRequest(token=token, channel_id="general",
                                                           content=m.content))
-
-            def one(stub):
-                r = stub.GetSmartReply(raft_pb.SmartReplyRequest(token=token, channel_id="general"),
-                                       timeout=120)
-                assert r.success and len(r.suggestions) == 3
-            stubs = [cluster.stub(leader) for _ in range(8)]
+            target = (args.mode, cluster.addresses()[leader], token)
         else:
-            histories = [[llm_pb.Message(sender=m.sender, content=m.content)
-                          for m in channel_history(rng, 5)] for _ in range(64)]
-
-            def one(stub):
-                r = stub.GetSmartReply(llm_pb.SmartReplyRequest(
-                    recent_messages=histories[rng.randrange(len(histories))]), timeout=120)
-                assert len(r.suggestions) == 3
-            stubs = [make_stub(grpc.insecure_channel(f"127.0.0.1:{port}"), LLM_SERVICE)
-                     for _ in range(8)]
+            target = (args.mode, f"127.0.0.1:{port}", None)
 
         # warm-up (graph buckets, first-use GEMM kernels)
-        ths = [threading.Thread(target=one, args=(stubs[i % 8],)) for i in range(16)]
-        [t.start() for t in ths]
-        [t.join() for t in ths]
+        run_load(target, 16, 16, 0)
         if eng is not None:
             eng.stats.clear()
-        lat, errors, lock, it = [], [], threading.Lock(), iter(range(args.requests))
-
-        def worker(k):
-            stub = stubs[k % len(stubs)]
-            while True:
-                with lock:
-                    if next(it, None) is None:
-                        return
-                t = time.perf_counter()
-                try:
-                    one(stub)
-                except (grpc.RpcError, AssertionError) as e:
-                    with lock:
-                        errors.append(repr(e)[:200])
-                    continue
-                with lock:
-                    lat.append(time.perf_counter() - t)
-        t0 = time.perf_counter()
-        ths = [threading.Thread(target=worker, args=(k,)) for k in range(args.concurrency)]
-        [t.start() for t in ths]
-        [t.join() for t in ths]
-        dt = time.perf_counter() - t0
+        if args.client_procs > 0:  # clients outside this process (no shared GIL)
+            ctx = mp.get_context("spawn")
+            q = ctx.Queue()
+            k = args.client_procs
+            procs = [ctx.Process(target=_client_main,
+                                 args=(target, args.requests // k + (i < args.requests % k),
+                                       args.concurrency // k + (i < args.concurrency % k), i + 1, q))
+                     for i in range(k)]
+            [p.start() for p in procs]
+            lat, errors, starts, ends = [], [], [], []
+            for _ in procs:
+                la, er, t_s, t_e = q.get()
+                lat += la
+                errors += er
+                starts.append(t_s)
+                ends.append(t_e)
+            [p.join() for p in procs]
+            dt = max(ends) - min(starts)
+        else:
+            lat, errors, t_s, t_e = run_load(target, args.requests, args.concurrency, 1)
+            dt = t_e - t_s
         lat.sort()
-        gen_tokens = (len(lat) * fp.smart.max_new_tokens) if eng is not None else 0
+        gen_tokens = (len(lat) * fp.smart.max_new_tokens) if args.backend != "scripted" else 0
         out = {
             "metric": f"service smart-reply ({args.mode}) requests/s + latency",
-            "backend": args.backend, "model": args.model if eng else None,
+            "backend": args.backend, "model": args.model if args.backend != "scripted" else None,
+            "client_procs": args.client_procs,
             "requests": len(lat), "errors": len(errors), "concurrency": args.concurrency, "seconds": round(dt, 3),
             "requests_per_s": round(len(lat) / dt, 2),
             "gen_tokens_per_s": round(gen_tokens / dt, 1) if gen_tokens else None,
