@@ -42,6 +42,7 @@ def render(spec: dict) -> str:
 
 def main(outdir: str | None = None) -> list[str]:
     outdir = outdir or os.path.dirname(os.path.abspath(__file__))
+    os.makedirs(outdir, exist_ok=True)
     paths = []
     for spec in schema.ALL:
         p = os.path.join(outdir, spec["file"])

@@ -256,3 +256,17 @@ def test_config_file_layer(tmp_path):
     j.write_text('{"node_id": 3, "bogus": 1}')
     with _pytest.raises(SystemExit):
         parse_with_config(parser(), ["--config", str(j)])
+
+
+def test_checked_in_proto_files_match_schema(tmp_path):
+    """protos/*.proto (for protoc users / other languages) are generated from
+    the same schema the runtime descriptors are built from - no drift."""
+    import os
+
+    from drtc_amd.protos import gen_proto
+
+    here = os.path.dirname(gen_proto.__file__)
+    for p in gen_proto.main(str(tmp_path)):
+        name = os.path.basename(p)
+        with open(p) as a, open(os.path.join(here, name)) as b:
+            assert a.read() == b.read(), f"{name} is stale: run python -m drtc_amd.protos.gen_proto"
