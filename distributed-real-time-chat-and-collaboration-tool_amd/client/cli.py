@@ -26,6 +26,7 @@ import grpc
 
 from ..protos import raft_pb
 from ..utils.config import parse_with_config
+from ..utils.logging_utils import setup_logging
 from .connection import DEFAULT_CLUSTER, ClusterConnection, ClusterUnavailable
 
 BANNER = """
@@ -581,7 +582,9 @@ def main(argv=None):
     ap = argparse.ArgumentParser(description="drtc_amd chat client")
     ap.add_argument("--server", default=None, help="any node address (default: 3-node localhost cluster)")
     ap.add_argument("--nodes", default=None, help="comma-separated cluster addresses")
+    ap.add_argument("--log-level", default="WARNING")  # the reference client logs at WARNING
     a = parse_with_config(ap, argv)
+    setup_logging(a.log_level)
     nodes = a.nodes.split(",") if a.nodes else list(DEFAULT_CLUSTER)
     if a.server and a.server not in nodes:
         nodes.insert(0, a.server)

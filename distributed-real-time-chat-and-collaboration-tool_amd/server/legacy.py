@@ -32,6 +32,7 @@ import grpc
 from ..protos import CHAT_SERVICE, add_servicer, chat_pb
 from ..utils import auth, pickle_compat
 from ..utils.config import parse_with_config
+from ..utils.logging_utils import setup_logging
 
 log = logging.getLogger(__name__)
 
@@ -621,8 +622,9 @@ def main(argv=None):
     ap.add_argument("--port", type=int, default=50050)
     ap.add_argument("--node_id", type=int, default=1)
     ap.add_argument("--data-dir", default="server_data")
+    ap.add_argument("--log-level", default="INFO")
     a = parse_with_config(ap, argv)
-    logging.basicConfig(level=logging.INFO)
+    setup_logging(a.log_level)
     serve(a.port, a.data_dir, node_id=a.node_id)
 
 
