@@ -5,7 +5,10 @@ attention, o_proj, add+norm, gate|up GEMM, act, down, add+norm), LM head and
 the sampler, plus the RNG-step increment - is captured once per batch bucket
 and replayed with a single ``hipGraphLaunch``.  Per step the host only
 uploads three packed staging buffers (int32 / int64 / fp32) and reads back
-the sampled token ids.
+the sampled token ids.  Steps can be pipelined: the next step's input tokens
+are gathered from the previous step's samples on the device, so the engine
+enqueues step t+1 before it reads step t's tokens and the host bookkeeping of
+step t overlaps the GPU work of step t+1.
 """
 from __future__ import annotations
 
@@ -45,19 +48,26 @@ class DecodeRunner:
         self.ctx = self.i32[2 * B:3 * B]
         self.topk = self.i32[3 * B:4 * B]
         self.bt = self.i32[4 * B:4 * B + B * MB].view(B, MB)
-        self.slots = torch.full((B,), -1, dtype=torch.int64, device=dev)
+        # int64 staging: KV slot per sequence | source row of the input token
+        # in the previous step's sampled tokens (-1: take ``ids`` from the host)
+        self.i64 = torch.full((2 * B,), -1, dtype=torch.int64, device=dev)
+        self.slots = self.i64[0:B]
+        self.src = self.i64[B:2 * B]
         self.f32 = torch.zeros(2 * B, dtype=torch.float32, device=dev)
         self.temp = self.f32[0:B]
         self.topp = self.f32[B:2 * B]
         self.step_ctr = torch.zeros(1, dtype=torch.int64, device=dev)
         self.out = torch.zeros(B, dtype=torch.int32, device=dev)
         self.attn_out = torch.zeros((B, sh.hq, cfg.head_dim), dtype=model.dtype, device=dev)
-        # ---- pinned host staging
+        # ---- pinned host staging, double-buffered: step t+1 is staged while
+        # step t's copies may still be pending (pipelined decode)
         pin = dev.type == "cuda"
-        self.h_i32 = torch.zeros(n_i32, dtype=torch.int32, pin_memory=pin)
-        self.h_slots = torch.full((B,), -1, dtype=torch.int64, pin_memory=pin)
-        self.h_f32 = torch.zeros(2 * B, dtype=torch.float32, pin_memory=pin)
-        self.h_out = torch.zeros(B, dtype=torch.int32, pin_memory=pin)
+        self.h_i32 = [torch.zeros(n_i32, dtype=torch.int32, pin_memory=pin) for _ in range(2)]
+        self.h_i64 = [torch.full((2 * B,), -1, dtype=torch.int64, pin_memory=pin) for _ in range(2)]
+        self.h_f32 = [torch.zeros(2 * B, dtype=torch.float32, pin_memory=pin) for _ in range(2)]
+        self.h_out = [torch.zeros(B, dtype=torch.int32, pin_memory=pin) for _ in range(2)]
+        self.events = [torch.cuda.Event() if pin else None for _ in range(2)]
+        self._k = 0
         self.n_i32 = n_i32
         self._metas = {}
         self._graphs = {}
@@ -66,6 +76,7 @@ class DecodeRunner:
         # overhead accounting (decode wall time - GPU time)
         self.time_gpu = os.environ.get("DRTC_TIME_DECODE") == "1"
         self.gpu_ms: list[float] = []
+        self._timing: list = []
 
     # ------------------------------------------------------------------
     def bucket(self, n: int) -> int:
@@ -88,7 +99,12 @@ class DecodeRunner:
 
     def _forward(self, Bb: int) -> None:
         meta = self._meta(Bb)
-        logits = self.model.forward_decode(self.ids[:Bb], meta, self.kv, self.attn_out[:Bb])
+        # input tokens: the previous step's samples still on the device
+        # (pipelined steps, src >= 0) or host-provided ids (src = -1)
+        src = self.src[:Bb]
+        ids = torch.where(src >= 0, self.out[:Bb].index_select(0, src.clamp(min=0)),
+                          self.ids[:Bb])
+        logits = self.model.forward_decode(ids, meta, self.kv, self.attn_out[:Bb])
         ops.sample(logits, self.temp[:Bb], self.topk[:Bb], self.topp[:Bb], seed=self.seed,
                    step=self.step_ctr, out=self.out[:Bb])
         self.step_ctr.add_(1)
@@ -117,15 +133,21 @@ class DecodeRunner:
                 self.capture(Bb)
 
     # ------------------------------------------------------------------
-    def run(self, n: int, ids: np.ndarray, positions: np.ndarray, ctx: np.ndarray,
-            slots: np.ndarray, block_rows: np.ndarray, temp: np.ndarray, topk: np.ndarray,
-            topp: np.ndarray) -> np.ndarray:
-        """Run one decode step for ``n`` sequences (arrays of length n, block_rows
-        [n, max_blocks]) and return the sampled token ids."""
+    def launch(self, n: int, ids: np.ndarray | None, positions: np.ndarray, ctx: np.ndarray,
+               slots: np.ndarray, block_rows: np.ndarray, temp: np.ndarray, topk: np.ndarray,
+               topp: np.ndarray) -> tuple[int, int]:
+        """Enqueue one decode step for ``n`` sequences (arrays of length n,
+        block_rows [n, max_blocks]) without waiting for it.  ``ids=None``
+        takes every input token from the previous step's samples on the device
+        (same slot order: a pipelined step).  Returns a handle for
+        :meth:`wait`."""
         Bb = self.bucket(n)
         B, MB = self.max_batch, self.max_blocks
-        hi = self.h_i32.numpy()
-        hi[0:n] = ids
+        k = self._k
+        self._k ^= 1
+        hi = self.h_i32[k].numpy()
+        if ids is not None:
+            hi[0:n] = ids
         hi[n:Bb] = 0
         hi[B:B + n] = positions
         hi[B + n:B + Bb] = 0
@@ -136,18 +158,20 @@ class DecodeRunner:
         btv = hi[4 * B:4 * B + B * MB].reshape(B, MB)
         btv[:n] = block_rows
         btv[n:Bb] = 0
-        hs = self.h_slots.numpy()
-        hs[:n] = slots
-        hs[n:Bb] = -1
-        hf = self.h_f32.numpy()
+        hl = self.h_i64[k].numpy()
+        hl[:n] = slots
+        hl[n:Bb] = -1
+        hl[B:B + n] = -1 if ids is not None else np.arange(n)
+        hl[B + n:B + Bb] = -1
+        hf = self.h_f32[k].numpy()
         hf[:n] = temp
         hf[n:Bb] = 0.0
         hf[B:B + n] = topp
         hf[B + n:B + Bb] = 1.0
         nb = self.device.type == "cuda"
-        self.i32.copy_(self.h_i32, non_blocking=nb)
-        self.slots.copy_(self.h_slots, non_blocking=nb)
-        self.f32.copy_(self.h_f32, non_blocking=nb)
+        self.i32.copy_(self.h_i32[k], non_blocking=nb)
+        self.i64.copy_(self.h_i64[k], non_blocking=nb)
+        self.f32.copy_(self.h_f32[k], non_blocking=nb)
         g = self._graphs.get(Bb)
         if g is None and self.use_graphs:
             self.capture(Bb)
@@ -164,10 +188,25 @@ class DecodeRunner:
                 self._forward(Bb)
         if timing:
             ev1.record()
+            self._timing.append((ev0, ev1))
+        self.h_out[k][:n].copy_(self.out[:n], non_blocking=nb)
         if nb:
-            self.h_out[:n].copy_(self.out[:n], non_blocking=True)
-            torch.cuda.current_stream(self.device).synchronize()
-            if timing:
-                self.gpu_ms.append(ev0.elapsed_time(ev1))
-            return self.h_out[:n].numpy().copy()
-        return self.out[:n].numpy().copy()
+            self.events[k].record()
+        return n, k
+
+    def wait(self, handle: tuple[int, int]) -> np.ndarray:
+        """Sampled token ids of a launched step (blocks until it is done)."""
+        n, k = handle
+        if self.events[k] is not None:
+            self.events[k].synchronize()
+        while self._timing:
+            e0, e1 = self._timing.pop(0)
+            self.gpu_ms.append(e0.elapsed_time(e1))
+        return self.h_out[k][:n].numpy().copy()
+
+    def run(self, n: int, ids: np.ndarray, positions: np.ndarray, ctx: np.ndarray,
+            slots: np.ndarray, block_rows: np.ndarray, temp: np.ndarray, topk: np.ndarray,
+            topp: np.ndarray) -> np.ndarray:
+        """One synchronous decode step (launch + wait)."""
+        return self.wait(self.launch(n, ids, positions, ctx, slots, block_rows, temp, topk,
+                                     topp))

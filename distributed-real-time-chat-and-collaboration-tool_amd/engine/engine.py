@@ -87,6 +87,11 @@ class LLMEngine:
         self.nblk = np.zeros(max_batch, dtype=np.int32)       # cache blocks held
         self.stop_ids: dict[int, tuple] = {}                  # slot -> custom stop ids
         self.running: list[Request] = []
+        # pipelined decode: the launched-but-unread step, and requests that
+        # finished (EOS) while a later step holding their slot was in flight
+        self._inflight: dict | None = None
+        self._zombies: list[Request] = []
+        self.pipeline = True
         self.waiting: collections.deque[Request] = collections.deque()
         self.lock = threading.Lock()
         self.stats = collections.Counter()
@@ -110,7 +115,7 @@ class LLMEngine:
         return req
 
     def has_work(self) -> bool:
-        return bool(self.running or self.waiting)
+        return bool(self.running or self.waiting or self._inflight)
 
     def warmup(self, capture: bool = True, up_to: int | None = None) -> None:
         """Capture decode graphs up front (zeroed staging: no cache reads/writes)."""
@@ -127,12 +132,17 @@ class LLMEngine:
 
     def step(self) -> list[Request]:
         """One scheduler iteration. Returns requests finished in it."""
+        if self._inflight is not None and self._could_admit():
+            # a prefill changes the slot layout: read the in-flight step first
+            done = self._process_inflight()
+            self._record(done)
+            return done
         with self.lock:
             batch = self._admit()
         if batch:
             with tracing.span("engine.prefill", seqs=len(batch)):
                 done = self._run_prefill(batch)
-        elif self.running:
+        elif self.running or self._inflight is not None:
             with tracing.span("engine.decode", batch=len(self.running)):
                 done = self._run_decode()
         else:
@@ -344,36 +354,107 @@ class LLMEngine:
         self.stats["preemptions"] += 1
         self.waiting.appendleft(r)
 
+    def _could_admit(self) -> bool:
+        return bool(self.waiting) and len(self.running) < self.max_batch and not (
+            self._pressure and self.running)
+
     def _run_decode(self) -> list[Request]:
+        """Decode with one step in flight.  While the batch composition stays
+        fixed (no request can finish by length in the in-flight step, no
+        pending EOS finishes, no admissions, next KV slots allocatable without
+        preemption) step t+1 is enqueued - its input tokens gathered from step
+        t's samples on the device - BEFORE step t's tokens are read, so the
+        host bookkeeping of step t overlaps the GPU work of step t+1.  Any
+        composition change drains the pipeline and re-stages from the host."""
+        done: list[Request] = []
+        if self._inflight is not None:
+            if self._can_pipeline():
+                nxt = self._launch_decode(pipelined=True)
+                done = self._process(self._inflight, later_inflight=True)
+                self._inflight = nxt
+                return done
+            done = self._process_inflight()
+            if self._could_admit():
+                return done  # the next step() admits and prefills
         with self.lock:
             self._ensure_blocks()
+        if self.running:
+            self._inflight = self._launch_decode(pipelined=False)
+        return done
+
+    def _process_inflight(self) -> list[Request]:
+        step, self._inflight = self._inflight, None
+        return self._process(step, later_inflight=False)
+
+    def _can_pipeline(self) -> bool:
+        st = self._inflight
         n = len(self.running)
-        if n == 0:
-            return []
+        if not self.pipeline or self._zombies or n != st["n"] or self._could_admit():
+            return False
+        if np.any((st["gen"] >= self.max_new[:n]) | (st["ctx"] + 1 >= self.max_model_len)):
+            return False  # a request finishes by length in the in-flight step
+        pos = self.ctx[:n]
+        need = (pos % BS == 0) & (pos // BS >= self.nblk[:n])
+        k = int(need.sum())
+        if k == 0:
+            return True
+        with self.lock:
+            if not self.alloc.can_allocate(k):
+                return False  # would need a preemption: drain first
+            for s_ in np.nonzero(need)[0].tolist():
+                r = self.running[s_]
+                b = self.alloc.allocate_one()
+                r.blocks.append(b)
+                self.bt[s_, len(r.blocks) - 1] = b
+                self.nblk[s_] = len(r.blocks)
+        return True
+
+    def _launch_decode(self, pipelined: bool) -> dict:
+        n = len(self.running)
         pos = self.ctx[:n].copy()
         bidx = pos // BS
         slots = self.bt[np.arange(n), bidx].astype(np.int64) * BS + pos % BS
-        toks = self.runner.run(n, self.last[:n], pos, pos + 1, slots, self.bt[:n],
-                               self.temp[:n], self.topk[:n], self.topp[:n])
+        handle = self.runner.launch(n, None if pipelined else self.last[:n], pos, pos + 1, slots,
+                                    self.bt[:n], self.temp[:n], self.topk[:n], self.topp[:n])
         self.stats["decode_steps"] += 1
         self.stats["decode_tokens"] += n
+        if pipelined:
+            self.stats["decode_steps_pipelined"] += 1
         self.ctx[:n] += 1
-        self.last[:n] = toks
         self.gen[:n] += 1
-        reqs = list(self.running)
-        for r, tok in zip(reqs, toks.tolist()):
-            r.output_ids.append(tok)
+        return {"handle": handle, "n": n, "reqs": list(self.running),
+                "gen": self.gen[:n].copy(), "ctx": self.ctx[:n].copy()}
+
+    def _process(self, st: dict, later_inflight: bool) -> list[Request]:
+        """Read a launched step's tokens; finish requests.  With a later step
+        in flight a finished request keeps its slot (its next token is
+        discarded) until that step is read."""
+        toks = self.runner.wait(st["handle"])
+        n, reqs = st["n"], st["reqs"]
+        live = np.fromiter((r.state != RequestState.FINISHED for r in reqs), dtype=bool, count=n)
+        for r, tok, ok in zip(reqs, toks.tolist(), live.tolist()):
+            if ok:
+                r.output_ids.append(tok)
+        self.last[:n] = np.where(live, toks, self.last[:n])
         # finish conditions for the whole batch at once (see _finish_check)
         stop = self.eos_stop[:n] & (toks == self.cfg.eos_token_id)
         for s_, ids in self.stop_ids.items():
             if s_ < n and int(toks[s_]) in ids:
                 stop[s_] = True
-        length = (self.gen[:n] >= self.max_new[:n]) | (self.ctx[:n] + 1 >= self.max_model_len)
-        done_idx = np.nonzero(stop | length)[0].tolist()
+        length = (st["gen"] >= self.max_new[:n]) | (st["ctx"] + 1 >= self.max_model_len)
+        done_idx = np.nonzero((stop | length) & live)[0].tolist()
         finished = [(reqs[i], "stop" if stop[i] else "length") for i in done_idx]
         for r, reason in finished:
-            self._release_slot(r)
             r.mark_finished(reason)
+        if later_inflight:
+            self._zombies.extend(r for r, _ in finished)
+        else:
+            # release in descending slot order: a release moves the last slot
+            # into the hole, which must not be a slot still to be released
+            rel = sorted([r for r, _ in finished] + self._zombies, key=lambda r: -r.slot)
+            self._zombies = []
+            for r in rel:
+                self._release_slot(r)
         if finished:
             self._pressure = False
         return [r for r, _ in finished]

@@ -47,6 +47,41 @@ def test_engine_stop_conditions():
         eng.add_request(__import__("drtc_amd.engine", fromlist=["Request"]).Request([1] * 100))
 
 
+def test_pipelined_decode_matches_synchronous():
+    """Pipelined decode (step t+1 enqueued before step t is read, tokens fed
+    back on the device) produces exactly the synchronous engine's outputs,
+    including EOS/stop finishes discovered one step late (zombie slots),
+    length finishes, block growth and mid-run admissions."""
+    from drtc_amd.engine import Request
+
+    m = TransformerLM(TINY_LLAMA, "cpu", seed=5)
+    prompts = [list(range(1, 10 + 7 * i)) for i in range(6)]
+
+    def run(pipeline: bool):
+        eng = LLMEngine(m, max_batch=8, max_model_len=256, num_blocks=64, use_graphs=False)
+        eng.pipeline = pipeline
+        probe = eng.generate([prompts[0]], SamplingParams.greedy(5, ignore_eos=True))[0]
+        stop_tok = probe.output_ids[3]  # request 0 stops on its 4th token
+        params = [SamplingParams(max_new_tokens=12 + 5 * i, temperature=0.0, top_k=0, top_p=1.0,
+                                 stop_token_ids=(stop_tok,) if i == 0 else ())
+                  for i in range(6)]
+        reqs = [eng.add_request(Request(list(p), prm)) for p, prm in zip(prompts[:4], params[:4])]
+        for _ in range(6):  # a few decode steps, then two late arrivals
+            eng.step()
+        reqs += [eng.add_request(Request(list(p), prm)) for p, prm in zip(prompts[4:], params[4:])]
+        while eng.has_work():
+            eng.step()
+        assert eng.alloc.num_used == 0 and not eng.running
+        return [(r.output_ids, r.finish_reason) for r in reqs], eng.stats, stop_tok
+
+    sync, st_sync, stop_tok = run(False)
+    pipe, st_pipe, _ = run(True)
+    assert pipe == sync
+    assert sync[0][1] == "stop" and sync[0][0][-1] == stop_tok and stop_tok not in sync[0][0][:-1]
+    assert all(reason == "length" for _, reason in sync[1:])
+    assert st_pipe["decode_steps_pipelined"] > 0 and st_sync["decode_steps_pipelined"] == 0
+
+
 def test_tp2_matches_tp1_logits():
     """TP sharding math (head/column split + reductions) on one process by
     summing the shards' partial outputs by hand."""
