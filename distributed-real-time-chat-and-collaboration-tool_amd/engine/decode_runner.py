@@ -76,7 +76,7 @@ class DecodeRunner:
         # overhead accounting (decode wall time - GPU time)
         self.time_gpu = os.environ.get("DRTC_TIME_DECODE") == "1"
         self.gpu_ms: list[float] = []
-        self._timing: list = []
+        self._timing: dict[int, tuple] = {}  # staging set -> (start, end) events
 
     # ------------------------------------------------------------------
     def bucket(self, n: int) -> int:
@@ -188,7 +188,7 @@ class DecodeRunner:
                 self._forward(Bb)
         if timing:
             ev1.record()
-            self._timing.append((ev0, ev1))
+            self._timing[k] = (ev0, ev1)
         self.h_out[k][:n].copy_(self.out[:n], non_blocking=nb)
         if nb:
             self.events[k].record()
@@ -199,9 +199,9 @@ class DecodeRunner:
         n, k = handle
         if self.events[k] is not None:
             self.events[k].synchronize()
-        while self._timing:
-            e0, e1 = self._timing.pop(0)
-            self.gpu_ms.append(e0.elapsed_time(e1))
+        ev = self._timing.pop(k, None)
+        if ev is not None:
+            self.gpu_ms.append(ev[0].elapsed_time(ev[1]))
         return self.h_out[k][:n].numpy().copy()
 
     def run(self, n: int, ids: np.ndarray, positions: np.ndarray, ctx: np.ndarray,
