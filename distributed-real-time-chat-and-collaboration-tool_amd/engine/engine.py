@@ -25,6 +25,7 @@ from __future__ import annotations
 import collections
 import itertools
 import math
+import os
 import threading
 import time
 
@@ -91,7 +92,7 @@ class LLMEngine:
         # finished (EOS) while a later step holding their slot was in flight
         self._inflight: dict | None = None
         self._zombies: list[Request] = []
-        self.pipeline = True
+        self.pipeline = os.environ.get("DRTC_PIPELINE_DECODE", "1") != "0"
         self.waiting: collections.deque[Request] = collections.deque()
         self.lock = threading.Lock()
         self.stats = collections.Counter()
