@@ -155,14 +155,14 @@ class LLMEngine:
         """Serving metrics: TTFT / TPOT / end-to-end latency per finished
         request, KV-cache occupancy and queue depths per step."""
         M = METRICS
-        for r in done:
-            M.observe("engine.ttft_s", r.ttft)
-            M.observe("engine.e2e_s", r.finish_time - r.arrival_time)
-            if len(r.output_ids) > 1:
-                M.observe("engine.tpot_s", (r.finish_time - r.first_token_time)
-                          / (len(r.output_ids) - 1))
-            M.inc("engine.generated_tokens", len(r.output_ids))
-            M.inc("engine.finished")
+        if done:
+            M.observe_many("engine.ttft_s", [r.ttft for r in done])
+            M.observe_many("engine.e2e_s", [r.finish_time - r.arrival_time for r in done])
+            M.observe_many("engine.tpot_s", [(r.finish_time - r.first_token_time)
+                                             / (len(r.output_ids) - 1)
+                                             for r in done if len(r.output_ids) > 1])
+            M.inc("engine.generated_tokens", sum(len(r.output_ids) for r in done))
+            M.inc("engine.finished", len(done))
         used, free = self.alloc.num_used, self.alloc.num_free
         M.set_gauge("engine.kv_used_frac", used / max(1, used + free))
         M.set_gauge("engine.running", len(self.running))
@@ -250,7 +250,7 @@ class LLMEngine:
         dev = self.device
         # host metadata, vectorised over the batch (a 1024-prompt prefill is
         # ~150k tokens: per-request numpy calls would idle the GPU for ~50 ms)
-        seqs = [r.all_ids for r in batch]
+        seqs = [r.all_ids if r.output_ids else r.prompt_ids for r in batch]
         nseq = len(batch)
         lens_a = np.fromiter((len(x) for x in seqs), dtype=np.int64, count=nseq)
         lens = lens_a.tolist()

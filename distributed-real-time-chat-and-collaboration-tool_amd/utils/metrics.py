@@ -72,6 +72,15 @@ class Registry:
                 h = self.hists[name] = Histogram()
             h.observe(v)
 
+    def observe_many(self, name: str, values) -> None:
+        """Record a batch of observations under one lock acquisition."""
+        with self._lock:
+            h = self.hists.get(name)
+            if h is None:
+                h = self.hists[name] = Histogram()
+            for v in values:
+                h.observe(v)
+
     @contextmanager
     def timer(self, name: str):
         t = time.perf_counter()
