@@ -44,12 +44,10 @@ BS = ops.KV_BLOCK
 
 
 def _pad_tokens(T: int) -> int:
-    """Prefill token-count bucket (<= ~1.5% padding above 4k tokens)."""
+    """Prefill token-count bucket (< 256 padded rows above 256 tokens)."""
     if T <= 256:
         return -(-T // 32) * 32
-    if T <= 4096:
-        return -(-T // 256) * 256
-    return -(-T // 1024) * 1024
+    return -(-T // 256) * 256
 
 
 class LLMEngine:
@@ -64,6 +62,8 @@ class LLMEngine:
         self.max_batch = max_batch
         self.max_model_len = min(max_model_len, cfg.max_position)
         self.max_prefill_tokens = max_prefill_tokens
+        # prefill launch granularity (GEMMs stay at full efficiency from ~16k rows)
+        self.prefill_chunk_tokens = int(os.environ.get("DRTC_PREFILL_CHUNK", "32768"))
         self.max_blocks = math.ceil(self.max_model_len / BS)
         if num_blocks is None:
             num_blocks = PagedKVCache.auto_num_blocks(cfg, model.sh.hkv, self.device, kv_fraction)
@@ -247,7 +247,32 @@ class LLMEngine:
 
     # ------------------------------------------------------------ prefill
     def _run_prefill(self, batch: list[Request]) -> list[Request]:
+        """Packed varlen prefill of ``batch``, split into chunks of about
+        ``prefill_chunk_tokens`` tokens.  Each chunk's host metadata goes
+        through pinned staging and every copy is asynchronous, so the host
+        prepares chunk i+1 while the GPU runs chunk i (only the first chunk's
+        preparation is on the critical path); the sampled first tokens come
+        back through pinned buffers and are read after the last launch."""
+        chunks, cur, tok = [], [], 0
+        for r in batch:
+            n = r.num_tokens
+            if cur and tok + n > self.prefill_chunk_tokens:
+                chunks.append(cur)
+                cur, tok = [], 0
+            cur.append(r)
+            tok += n
+        chunks.append(cur)
+        launched = [self._launch_prefill(c) for c in chunks]
+        finished = []
+        for reqs, lens, h_tok, ev in launched:
+            if ev is not None:
+                ev.synchronize()
+            finished += self._finish_prefill(reqs, lens, h_tok.numpy())
+        return finished
+
+    def _launch_prefill(self, batch: list[Request]):
         dev = self.device
+        cuda = dev.type == "cuda"
         # host metadata, vectorised over the batch (a 1024-prompt prefill is
         # ~150k tokens: per-request numpy calls would idle the GPU for ~50 ms)
         seqs = [r.all_ids if r.output_ids else r.prompt_ids for r in batch]
@@ -283,10 +308,21 @@ class LLMEngine:
         seg_blk = blk_tab[s_seq, s_j].astype(np.int32)
         last_idx = np.asarray(cu[1:], dtype=np.int64) - 1
         ts, tq = ops.prefill_tiles(cu)
-        t_i32 = torch.from_numpy(np.concatenate([ids, pos, np.asarray(cu, np.int32),
-                                                 np.asarray(ts, np.int32), np.asarray(tq, np.int32),
-                                                 seg_tok, seg_len, seg_blk])).to(dev, non_blocking=True)
-        t_i64 = torch.from_numpy(np.concatenate([slots, last_idx])).to(dev, non_blocking=True)
+        self._prefill_step += 1
+        params = np.array([(r.params.temperature, r.params.top_p, r.params.top_k) for r in batch],
+                          dtype=np.float64).reshape(nseq, 3)
+        h_i32 = torch.from_numpy(np.concatenate([
+            ids, pos, np.asarray(cu, np.int32), np.asarray(ts, np.int32),
+            np.asarray(tq, np.int32), seg_tok, seg_len, seg_blk,
+            params[:, 2].astype(np.int32)]))
+        h_i64 = torch.from_numpy(np.concatenate([
+            slots, last_idx, np.array([self._prefill_step + (1 << 40)], dtype=np.int64)]))
+        h_f32 = torch.from_numpy(params[:, :2].T.astype(np.float32).reshape(-1))
+        if cuda:  # pinned staging: the copies stay asynchronous to the host
+            h_i32, h_i64, h_f32 = h_i32.pin_memory(), h_i64.pin_memory(), h_f32.pin_memory()
+        t_i32 = h_i32.to(dev, non_blocking=True)
+        t_i64 = h_i64.to(dev, non_blocking=True)
+        t_f32 = h_f32.to(dev, non_blocking=True)
         nt, ns = len(ts), len(seg_tok)
         o = 0
         d_ids = t_i32[o:o + Tp]; o += Tp
@@ -295,17 +331,26 @@ class LLMEngine:
         d_ts = t_i32[o:o + nt]; o += nt
         d_tq = t_i32[o:o + nt]; o += nt
         d_segs = (t_i32[o:o + ns], t_i32[o + ns:o + 2 * ns], t_i32[o + 2 * ns:o + 3 * ns])
+        o += 3 * ns
+        topk = t_i32[o:o + nseq]
         meta = PrefillMeta(positions=d_pos, slots=t_i64[:Tp], cu_seqlens=d_cu, cu_host=cu,
-                           tiles=(d_ts, d_tq), last_idx=t_i64[Tp:], v_segs=d_segs)
-        temp = torch.tensor([r.params.temperature for r in batch], dtype=torch.float32, device=dev)
-        topk = torch.tensor([r.params.top_k for r in batch], dtype=torch.int32, device=dev)
-        topp = torch.tensor([r.params.top_p for r in batch], dtype=torch.float32, device=dev)
-        self._prefill_step += 1
-        step = torch.tensor([self._prefill_step + (1 << 40)], dtype=torch.int64, device=dev)
+                           tiles=(d_ts, d_tq), last_idx=t_i64[Tp:Tp + nseq], v_segs=d_segs)
+        step = t_i64[Tp + nseq:Tp + nseq + 1]
+        temp, topp = t_f32[:nseq], t_f32[nseq:]
         logits = self.model.forward_prefill(d_ids, meta, self.kv)
-        toks = ops.sample(logits, temp, topk, topp, seed=self.seed, step=step).cpu().numpy()
+        toks = ops.sample(logits, temp, topk, topp, seed=self.seed, step=step)
+        h_tok = torch.empty(nseq, dtype=torch.int32, pin_memory=cuda)
+        h_tok.copy_(toks, non_blocking=cuda)
+        ev = None
+        if cuda:
+            ev = torch.cuda.Event()
+            ev.record()
         self.stats["prefill_steps"] += 1
         self.stats["prefill_tokens"] += T
+        return batch, lens, h_tok, ev
+
+    def _finish_prefill(self, batch: list[Request], lens: list[int], toks) -> list[Request]:
+        """Slot assignment + first-token bookkeeping of one prefill chunk."""
         now = time.perf_counter()
         finished = []
         for r, n, tok in zip(batch, lens, toks):
