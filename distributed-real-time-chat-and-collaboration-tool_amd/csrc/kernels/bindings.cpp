@@ -78,12 +78,12 @@ PYBIND11_MODULE(_hipk, m) {
   m.def("moe_workspace_bytes", &drtc::moe_workspace_bytes);
   m.def("custom_ar_buffer_bytes", &drtc::custom_ar_buffer_bytes);
   m.def("custom_allreduce", [](u64 out, u64 in, int64_t n, const std::vector<u64>& bases, int rank,
-                               int64_t stage_elems, u64 st) {
+                               int64_t stage_elems, int two_shot, u64 st) {
     drtc::ArPeers p{};
     if (bases.size() > 8) return -1;
     for (size_t i = 0; i < bases.size(); ++i) p.base[i] = P<char>(bases[i]);
     return drtc::launch_custom_allreduce(P<void>(out), P<const void>(in), n, p, rank,
-                                         (int)bases.size(), stage_elems, S(st));
+                                         (int)bases.size(), stage_elems, two_shot, S(st));
   });
   m.def("ar_alloc", [](int64_t bytes) {
     void* p = nullptr;

@@ -55,7 +55,7 @@ struct ArPeers {
 };
 int64_t custom_ar_buffer_bytes(int64_t stage_elems);
 int launch_custom_allreduce(void* out, const void* in, int64_t n, const ArPeers& peers, int rank,
-                            int world, int64_t stage_elems, hipStream_t st);
+                            int world, int64_t stage_elems, int two_shot, hipStream_t st);
 int ar_alloc(void** p, int64_t bytes);
 int ar_free(void* p);
 int ar_ipc_get(void* p, char* handle);  // 64-byte handle

@@ -1,4 +1,4 @@
-"""One-shot P2P all-reduce for small tensor-parallel messages.
+"""One-/two-shot P2P all-reduce for tensor-parallel messages.
 
 Kernel + memory protocol: csrc/kernels/allreduce.hip.  Each rank allocates
 one uncached device buffer (flags + double-buffered staging), exports it as
@@ -21,7 +21,7 @@ from ..ops._ext import check, hipk, stream_ptr
 
 class CustomAllReduce:
     def __init__(self, group=None, device: torch.device | None = None,
-                 max_bytes: int = 4 << 20):
+                 max_bytes: int = 4 << 20, two_shot_min_bytes: int = 256 << 10):
         """``group``: a CPU-capable (gloo) process group over the TP ranks."""
         self.group = group
         self.rank = dist.get_rank(group)
@@ -31,6 +31,9 @@ class CustomAllReduce:
         self.device = device or torch.device("cuda", torch.cuda.current_device())
         self.stage_elems = max_bytes // 2
         self.max_bytes = max_bytes
+        # messages from this size on use the two-shot (reduce-scatter +
+        # all-gather) kernel: 2(N-1)/N of the message read per rank, not N-1x
+        self.two_shot_min_bytes = two_shot_min_bytes
         lib = hipk()
         with torch.cuda.device(self.device):
             self.base = lib.ar_alloc(lib.custom_ar_buffer_bytes(self.stage_elems))
@@ -54,12 +57,17 @@ class CustomAllReduce:
         return (x.is_cuda and x.dtype == torch.bfloat16 and x.is_contiguous()
                 and x.numel() % 8 == 0 and x.numel() * 2 <= self.max_bytes)
 
-    def all_reduce(self, x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
-        """Sum of ``x`` over the group (in place unless ``out`` is given)."""
+    def all_reduce(self, x: torch.Tensor, out: torch.Tensor | None = None,
+                   two_shot: bool | None = None) -> torch.Tensor:
+        """Sum of ``x`` over the group (in place unless ``out`` is given).
+        ``two_shot`` (default: by size, world > 2) picks the kernel; every
+        rank of a group must make the same choice for the same call."""
         assert self.can(x), "tensor not eligible for the custom all-reduce"
         out = x if out is None else out
+        if two_shot is None:
+            two_shot = self.world > 2 and x.numel() * 2 >= self.two_shot_min_bytes
         check(hipk().custom_allreduce(out.data_ptr(), x.data_ptr(), x.numel(), self.bases,
-                                      self.rank, self.stage_elems, stream_ptr(x)),
+                                      self.rank, self.stage_elems, int(two_shot), stream_ptr(x)),
               "custom_allreduce")
         return out
 

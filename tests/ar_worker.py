@@ -30,15 +30,16 @@ def main():
     torch.cuda.set_device(0)
     car = CustomAllReduce(dist.group.WORLD, torch.device("cuda", 0), max_bytes=4 << 20)
     it = 0
-    for n in (8, 4096, 8 * 1001, 1 << 20, 2 << 20):
-        for _ in range(3):  # consecutive calls alternate the staging halves
-            x = data(rank, it, n).cuda()
-            y = car.all_reduce(x)
-            torch.cuda.synchronize()
-            if not torch.equal(y.cpu(), expected(world, it, n)):
-                print(f"rank {rank}: mismatch n={n} it={it}", flush=True)
-                sys.exit(3)
-            it += 1
+    for n in (8, 4096, 8 * 1001, 8 * 12345, 1 << 20, 2 << 20):
+        for mode in (None, False, True):  # by size / one-shot / two-shot, interleaved
+            for _ in range(3):  # consecutive calls alternate the staging halves
+                x = data(rank, it, n).cuda()
+                y = car.all_reduce(x, two_shot=mode)
+                torch.cuda.synchronize()
+                if not torch.equal(y.cpu(), expected(world, it, n)):
+                    print(f"rank {rank}: mismatch n={n} mode={mode} it={it}", flush=True)
+                    sys.exit(3)
+                it += 1
     # hipGraph capture + replay with fresh inputs
     n = 4096 * 8
     static = torch.zeros(n, dtype=torch.bfloat16, device="cuda")
@@ -51,12 +52,14 @@ def main():
     dist.barrier()
     gr = torch.cuda.CUDAGraph()
     with torch.cuda.graph(gr):
-        car.all_reduce(static)
+        car.all_reduce(static, two_shot=False)
+        car.all_reduce(static, two_shot=True)  # the sum, summed again: world * sum
     for _ in range(3):
         static.copy_(data(rank, it, n).cuda())
         gr.replay()
         torch.cuda.synchronize()
-        if not torch.equal(static.cpu(), expected(world, it, n)):
+        want = (expected(world, it, n).float() * world).to(torch.bfloat16)
+        if not torch.equal(static.cpu(), want):
             print(f"rank {rank}: graph mismatch it={it}", flush=True)
             sys.exit(4)
         it += 1
