@@ -111,6 +111,8 @@ def main() -> None:
     eng = LLMEngine(model, max_batch=args.batch, max_model_len=args.max_model_len,
                     max_prefill_tokens=max(16384, args.batch * 400),
                     kv_fraction=args.kv_fraction, use_graphs=not args.no_graphs, seed=dp_rank)
+    if world > 1:
+        dist.barrier()  # TP: the custom all-reduce's flag waits are time-bounded
     eng.warmup(capture=True)
     if device.type == "cuda":
         torch.cuda.synchronize()

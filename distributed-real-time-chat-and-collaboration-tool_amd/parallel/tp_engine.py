@@ -52,6 +52,9 @@ def tp_worker(rank: int, world: int, port: int, model_name: str, engine_kw: dict
         cfg = get_config(model_name)
         model = TransformerLM(cfg, dev, pc=pc, seed=1234)
         eng = LLMEngine(model, seed=0, **engine_kw)
+        # ranks finish weight init at different times; the custom all-reduce's
+        # flag waits are time-bounded, so enter the captured warm-up together
+        dist.barrier(group=cpu)
         eng.warmup(capture=True)
         if rank == 0:
             outq.put(("ready", 0, None))

@@ -1,6 +1,7 @@
-"""Custom one-shot IPC all-reduce (csrc/kernels/allreduce.hip) with 2 and 3
-ranks as separate processes sharing the box's GPU: exact (bitwise) sums vs a
-fixed-order fp32 reference, staging double-buffer reuse, hipGraph replay."""
+"""Custom one-/two-shot IPC all-reduce (csrc/kernels/allreduce.hip) with 2, 3
+and 4 ranks as separate processes sharing the box's GPU: exact (bitwise) sums
+vs a fixed-order fp32 reference, staging double-buffer reuse across both
+kernels, hipGraph replay."""
 import os
 import subprocess
 import sys
