@@ -64,3 +64,33 @@ def test_engine_sampling_and_preemption(hipk):
     assert all(len(r.output_ids) == 40 for r in reqs)
     assert eng.stats["preemptions"] > 0
     assert eng.alloc.num_used == 0
+
+
+def test_pipelined_decode_with_graphs_matches_synchronous(hipk):
+    """On the GPU with hipGraph decode: pipelined steps (input tokens gathered
+    on the device from the previous step's samples) give exactly the
+    synchronous engine's tokens, with stop-token finishes, staggered lengths
+    and a mid-run admission."""
+    from drtc_amd.engine import Request
+
+    prompts = [list(range(1, 8 + 9 * i)) for i in range(5)]
+    outs, stats = [], []
+    for pipeline in (False, True):
+        m = TransformerLM(TINY_LLAMA, "cuda", seed=9)
+        eng = LLMEngine(m, max_batch=8, max_model_len=512, num_blocks=128, use_graphs=True)
+        eng.pipeline = pipeline
+        probe = eng.generate([prompts[0]], SamplingParams.greedy(6, ignore_eos=True))[0]
+        params = [SamplingParams(max_new_tokens=10 + 7 * i, temperature=0.0, top_k=0, top_p=1.0,
+                                 stop_token_ids=(probe.output_ids[4],) if i == 0 else ())
+                  for i in range(5)]
+        reqs = [eng.add_request(Request(list(p), prm)) for p, prm in zip(prompts[:4], params[:4])]
+        for _ in range(5):
+            eng.step()
+        reqs.append(eng.add_request(Request(list(prompts[4]), params[4])))
+        while eng.has_work():
+            eng.step()
+        outs.append([(r.output_ids, r.finish_reason) for r in reqs])
+        stats.append(dict(eng.stats))
+        assert eng.alloc.num_used == 0
+    assert outs[0] == outs[1]
+    assert stats[1].get("decode_steps_pipelined", 0) > 0
