@@ -26,10 +26,13 @@ SHAPES = [  # (name, nseq, mean len, Hq, Hkv, D)
 
 
 def main():
+    only = sys.argv[sys.argv.index("--only") + 1] if "--only" in sys.argv else None
     dev = torch.device("cuda")
     rng = random.Random(0)
     variant = "v1" if os.environ.get("DRTC_PREFILL_ATTN_V1") else "v2"
     for name, nseq, mean, Hq, Hkv, D in SHAPES:
+        if only and name != only:
+            continue
         lens = [max(8, int(rng.gauss(mean, mean * 0.1))) for _ in range(nseq)]
         cu = [0]
         for n in lens:
