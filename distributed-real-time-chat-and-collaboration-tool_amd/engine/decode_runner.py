@@ -203,10 +203,3 @@ class DecodeRunner:
         if ev is not None:
             self.gpu_ms.append(ev[0].elapsed_time(ev[1]))
         return self.h_out[k][:n].numpy().copy()
-
-    def run(self, n: int, ids: np.ndarray, positions: np.ndarray, ctx: np.ndarray,
-            slots: np.ndarray, block_rows: np.ndarray, temp: np.ndarray, topk: np.ndarray,
-            topp: np.ndarray) -> np.ndarray:
-        """One synchronous decode step (launch + wait)."""
-        return self.wait(self.launch(n, ids, positions, ctx, slots, block_rows, temp, topk,
-                                     topp))
