@@ -114,6 +114,11 @@ PYBIND11_MODULE(_hipk, m) {
     return drtc::lt_gemm(P<void>(y), P<const void>(x), P<const void>(w), M, N, K, ldx, ldy, S(st));
   });
   m.def("lt_set_algo", &drtc::lt_set_algo);
+  m.def("skinny_gemm", [](u64 y, u64 x, u64 w, int M, int N, int K, int ldx, int ldy,
+                          int variant, u64 st) {
+    return drtc::launch_skinny_gemm(P<void>(y), P<const void>(x), P<const void>(w), M, N, K, ldx,
+                                    ldy, variant, S(st));
+  });
   m.def("lt_tune", [](u64 y, u64 x, u64 w, int64_t M, int64_t N, int64_t K, int64_t ldx,
                       int64_t ldy, int iters, int max_candidates, u64 st) {
     py::gil_scoped_release nogil;

@@ -73,6 +73,11 @@ std::vector<std::pair<int, float>> lt_tune(void* y, const void* x, const void* w
                                            int64_t N, int64_t K, int64_t ldx, int64_t ldy,
                                            int iters, int max_candidates, hipStream_t st);
 
+// Skinny projection GEMM for decode batches M <= 16 (gemv.hip): y[M,N] = x[M,K] @ W[N,K]^T.
+// variant 0 = by shape; returns -1 for a shape the chosen form does not cover.
+int launch_skinny_gemm(void* y, const void* x, const void* w, int M, int N, int K, int ldx,
+                       int ldy, int variant, hipStream_t st);
+
 // Raise the dynamic-LDS ceiling of the kernels that need > 64 KiB (head_dim
 // 256).  Called once at import, before any graph capture.
 int configure_kernels();

@@ -13,6 +13,13 @@ listed solution - e.g. Llama-3-70B ``down`` at M=256: 312 us heuristic vs
 178 us tuned (profiles/r1g_tuned_gemm_prefill_attn.md).  Tables are produced by
 ``scripts/tune_gemms.py`` on the GPU and keyed by the hipBLASLt version
 (solution indices are only valid for the library that listed them).
+
+Small decode batches (M <= 8 rows) are weight-streaming GEMVs, where the
+library reaches 3-4.5 TB/s on the 8B shapes; they run on the hand-written
+skinny kernels of ``csrc/kernels/gemv.hip`` (VALU dot2 form and MFMA form,
+several row/K-split decompositions) at up to 6.7 TB/s.  The table records,
+per measured shape, whether a skinny variant beat the library
+(``scripts/tune_skinny.py``); unmeasured shapes use ``skinny_variant``.
 """
 from __future__ import annotations
 
@@ -27,9 +34,16 @@ from ._ext import check, hipk, on_gpu, stream_ptr
 
 TUNED_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuned")
 _lock = threading.Lock()
-_table: dict[tuple[int, int, int, int], int] | None = None  # (M, N, K, ldx) -> solution index
+# (M, N, K, ldx) -> (hipBLASLt solution index or -1, skinny-kernel variant or 0)
+_table: dict[tuple[int, int, int, int], tuple[int, int]] | None = None
 _ready: set[tuple[int, int, int, int]] = set()               # entries with a native plan
 _enabled = os.environ.get("DRTC_TUNED_GEMM", "1") != "0"
+# decode batches up to this many rows may take the hand-written skinny kernel
+# (csrc/kernels/gemv.hip) instead of the library: the tuning table's choice
+# where the shape was measured, skinny_variant()'s default otherwise; 0
+# disables it
+SKINNY_MAX_M = int(os.environ.get("DRTC_SKINNY_MAX_M", "16"))
+SKINNY_DEFAULT_MAX_M = 8  # untuned shapes: measured gains up to M = 8 only
 
 
 def table_path(arch: str = "gfx950") -> str:
@@ -54,12 +68,12 @@ def _activate() -> dict:
     with _lock:
         if _table is not None:
             return _table
-        tab: dict[tuple[int, int, int, int], int] = {}
+        tab: dict[tuple[int, int, int, int], tuple[int, int]] = {}
         if _enabled and torch.cuda.is_available():
             ver = str(hipk().lt_version())
             for ks, e in load_table().get(ver, {}).items():
                 M, N, K, ldx = (int(v) for v in ks.split(","))
-                tab[(M, N, K, ldx)] = int(e["algo"])
+                tab[(M, N, K, ldx)] = (int(e.get("algo", -1)), int(e.get("skinny", 0)))
         _ready.clear()
         _table = tab
     return _table
@@ -73,7 +87,7 @@ def _plan(key: tuple[int, int, int, int]) -> bool:
         return True
     M, N, K, ldx = key
     with _lock:
-        if hipk().lt_set_algo(M, N, K, ldx, N, _table[key]) != 0:
+        if hipk().lt_set_algo(M, N, K, ldx, N, _table[key][0]) != 0:
             _table.pop(key, None)
             return False
         _ready.add(key)
@@ -93,6 +107,46 @@ def set_enabled(on: bool) -> None:
     reset()
 
 
+# rows of W per workgroup of each MFMA variant (gemv.hip launch_skinny_gemm)
+SKINNY_ROWS = {2: 16, 3: 16, 4: 32, 5: 32, 6: 16, 7: 64, 8: 128, 9: 64}
+
+
+def skinny_supports(v: int, M: int, N: int, K: int, ldx: int) -> bool:
+    """Whether skinny variant ``v`` covers the shape (mirrors the launcher)."""
+    if not 1 <= M <= 16 or ldx % 8 or N % 4:
+        return False
+    if v == 1:
+        return M <= 8 and K % 512 == 0
+    return v in SKINNY_ROWS and K % 128 == 0 and N % SKINNY_ROWS[v] == 0
+
+
+def skinny_variant(M: int, N: int, K: int, ldx: int) -> int:
+    """Default skinny-kernel form for an untuned shape: 1 = VALU dot2 for
+    M <= 2, 3 = MFMA (1 tile, 8 K-split waves) up to M = 8; 0 = leave it to
+    the library."""
+    if M > min(SKINNY_MAX_M, SKINNY_DEFAULT_MAX_M):
+        return 0
+    for v in ((1, 3) if M <= 2 else (3,)):
+        if skinny_supports(v, M, N, K, ldx):
+            return v
+    return 0
+
+
+def skinny_ok(M: int, N: int, K: int, ldx: int) -> bool:
+    return skinny_variant(M, N, K, ldx) != 0
+
+
+def skinny_linear(x: torch.Tensor, w: torch.Tensor, variant: int = 0) -> torch.Tensor:
+    """y = x @ w.T on the skinny decode kernel (M <= 16 rows of x)."""
+    M, K = x.shape
+    N = w.shape[0]
+    variant = variant or skinny_variant(M, N, K, x.stride(0))
+    y = torch.empty((M, N), dtype=x.dtype, device=x.device)
+    check(hipk().skinny_gemm(y.data_ptr(), x.data_ptr(), w.data_ptr(), M, N, K, x.stride(0), N,
+                             variant, stream_ptr(x)), "skinny_gemm")
+    return y
+
+
 def linear(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     """y = x @ w.T for x [M, K] (row stride ldx), w [N, K] contiguous."""
     if (on_gpu(x) and _enabled and x.dim() == 2 and x.dtype == torch.bfloat16
@@ -100,7 +154,14 @@ def linear(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
         M, K = x.shape
         N = w.shape[0]
         key = (M, N, K, x.stride(0))
-        if key in _activate() and _plan(key):
+        ent = _activate().get(key)
+        if ent is None:
+            v = skinny_variant(M, N, K, x.stride(0))
+            if v:
+                return skinny_linear(x, w, v)
+        elif ent[1] and M <= SKINNY_MAX_M:
+            return skinny_linear(x, w, ent[1])
+        elif ent[0] >= 0 and _plan(key):
             y = torch.empty((M, N), dtype=x.dtype, device=x.device)
             check(hipk().lt_gemm(y.data_ptr(), x.data_ptr(), w.data_ptr(), M, N, K, x.stride(0),
                                  N, stream_ptr(x)), "lt_gemm")
@@ -133,7 +194,9 @@ def save_entries(entries: dict[str, dict], path: str | None = None) -> str:
     path = path or table_path()
     data = load_table(path)
     ver = str(hipk().lt_version())
-    data.setdefault(ver, {}).update(entries)
+    cur = data.setdefault(ver, {})
+    for k, e in entries.items():
+        cur[k] = {**cur.get(k, {}), **e}
     os.makedirs(os.path.dirname(path), exist_ok=True)
     with open(path, "w") as f:
         json.dump(data, f, indent=1, sort_keys=True)
@@ -141,4 +204,4 @@ def save_entries(entries: dict[str, dict], path: str | None = None) -> str:
     return path
 
 
-__all__ = ["linear", "tune", "save_entries", "load_table", "reset", "set_enabled", "table_path"]
+__all__ = ["linear", "skinny_linear", "skinny_ok", "skinny_variant", "skinny_supports", "tune", "save_entries", "load_table", "reset", "set_enabled", "table_path"]

@@ -46,8 +46,10 @@ def merge(src: str) -> None:
         new = json.load(f)
     path = gemm.table_path()
     data = gemm.load_table(path)
-    for ver, entries in new.items():
-        data.setdefault(ver, {}).update(entries)
+    for ver, entries in new.items():  # per key: new fields over old (algo / skinny picks)
+        cur = data.setdefault(ver, {})
+        for k, e in entries.items():
+            cur[k] = {**cur.get(k, {}), **e}
     os.makedirs(os.path.dirname(path), exist_ok=True)
     with open(path, "w") as f:
         json.dump(data, f, indent=1, sort_keys=True)

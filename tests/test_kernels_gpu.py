@@ -315,7 +315,7 @@ def test_tuned_linear(hipk, M, N, K):
     ref = x.float() @ w.float().t()
     saved = gemm._table
     try:
-        gemm._table = {(M, N, K, K): r["algo"]}
+        gemm._table = {(M, N, K, K): (r["algo"], 0)}
         y = ops.linear(x, w)
         _close(y, ref, 2e-2, 2e-2, "tuned linear")
         g = torch.cuda.CUDAGraph()
@@ -327,6 +327,36 @@ def test_tuned_linear(hipk, M, N, K):
         _close(yg, x.float() @ w.float().t(), 2e-2, 2e-2, "tuned linear (graph)")
     finally:
         gemm._table = saved
+
+
+@pytest.mark.parametrize("M", [1, 2, 3, 5, 8, 13, 16])
+@pytest.mark.parametrize("N,K,ldx", [(256, 512, 512), (1152, 1536, 1536), (128, 4096, 4224),
+                                     (192, 14336, 14336), (96, 384, 392)])
+def test_skinny_gemm(hipk, M, N, K, ldx):
+    """Skinny decode GEMM (csrc/kernels/gemv.hip) vs fp32 x @ w.T: both forms
+    (VALU dot2, MFMA with every (tiles, waves) config), padded M, odd/even
+    step counts per wave, strided x rows, and inside a hipGraph through
+    ops.linear."""
+    from drtc_amd.ops import gemm
+
+    torch.manual_seed(M * 31 + N)
+    xs = torch.randn(M, ldx, device=DEV).to(torch.bfloat16)
+    x = xs[:, :K]
+    w = (torch.randn(N, K, device=DEV) * 0.05).to(torch.bfloat16)
+    ref = x.float() @ w.float().t()
+    variants = [v for v in range(1, 10) if gemm.skinny_supports(v, M, N, K, ldx)]
+    assert variants
+    for v in variants:
+        _close(gemm.skinny_linear(x, w, variant=v), ref, 2e-2, 2e-2, f"skinny gemm v{v}")
+    if not gemm.skinny_ok(M, N, K, ldx):
+        return
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        yg = ops.linear(x, w)
+    xs.copy_(torch.randn(M, ldx, device=DEV).to(torch.bfloat16))
+    g.replay()
+    torch.cuda.synchronize()
+    _close(yg, x.float() @ w.float().t(), 2e-2, 2e-2, "skinny gemm (graph)")
 
 
 @pytest.mark.parametrize("e_off,e_local", [(0, 8), (2, 3)])
