@@ -7,8 +7,10 @@
 //   share a kv head are processed together, so every K/V byte is read from
 //   HBM once per step.  Waves take the partition's 32-token cache blocks
 //   round-robin, keep an online softmax each, and merge through LDS; when a
-//   sequence spans several partitions the fp32 partials are merged by
-//   `decode_reduce_kernel` (flash-decoding split-K).
+//   sequence spans several partitions the fp32 partials are merged
+//   (flash-decoding split-K) by the last partition workgroup to finish
+//   (agent-scope counter per (sequence, kv head)), or by
+//   `decode_reduce_kernel` when no counter buffer is given.
 //
 // MFMA formulation (16x16x32 bf16, operand maps in common.h)
 //   S^T[tok, head] = K[tok, :] . Q[head, :]    A = K rows (16-B loads straight
@@ -56,8 +58,8 @@ DRTC_DEVICE void load_kv_block(KVRegs<D>& r, const bf16_t* kb, const bf16_t* vb,
 template <int D>
 __global__ __launch_bounds__(256, D >= 256 ? 1 : 2) void paged_decode_kernel(
     bf16_t* __restrict__ out, float* __restrict__ part_o,
-    float* __restrict__ part_ml, const bf16_t* __restrict__ q, int q_stride,
-    const bf16_t* __restrict__ k_cache, const bf16_t* __restrict__ v_cache,
+    float* __restrict__ part_ml, int* __restrict__ counters, const bf16_t* __restrict__ q,
+    int q_stride, const bf16_t* __restrict__ k_cache, const bf16_t* __restrict__ v_cache,
     const int* __restrict__ block_tables, int bt_stride,
     const int* __restrict__ context_lens, int Hq, int Hkv, float scale_log2e,
     int max_parts, int blocks_per_part) {
@@ -208,6 +210,45 @@ __global__ __launch_bounds__(256, D >= 256 ? 1 : 2) void paged_decode_kernel(
         part_ml[pi * 2 + 1] = L;
       }
     }
+  }
+  if (single || counters == nullptr) return;
+  // Split-K merge without a second launch: the last partition of this
+  // (sequence, kv head) to finish - counted with an agent-scope atomic after
+  // a release fence over the partial stores - merges all partitions in fixed
+  // order (deterministic) and re-arms the counter for the next launch.
+  __shared__ int is_last;
+  __shared__ float mh[16], ilh[16];
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int prev = __hip_atomic_fetch_add(counters + blockIdx.x, 1, __ATOMIC_ACQ_REL,
+                                            __HIP_MEMORY_SCOPE_AGENT);
+    is_last = (prev == nparts - 1);
+    if (is_last) __hip_atomic_store(counters + blockIdx.x, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  if (!is_last) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  if (threadIdx.x < G) {
+    const float* ml = part_ml + ((int64_t)b * Hq + h * G + threadIdx.x) * max_parts * 2;
+    float M = kNegBig;
+    for (int pp = 0; pp < nparts; ++pp) M = fmaxf(M, ml[2 * pp]);
+    float L = 0.f;
+    for (int pp = 0; pp < nparts; ++pp) L += ml[2 * pp + 1] * fast_exp2(ml[2 * pp] - M);
+    mh[threadIdx.x] = M;
+    ilh[threadIdx.x] = 1.f / L;
+  }
+  __syncthreads();
+  for (int item = threadIdx.x; item < G * D; item += 256) {
+    const int hh = item / D;
+    const int d = item - hh * D;
+    const int64_t bh = (int64_t)b * Hq + h * G + hh;
+    const float* ml = part_ml + bh * max_parts * 2;
+    const float M = mh[hh];
+    float O = 0.f;
+    for (int pp = 0; pp < nparts; ++pp)
+      O += part_o[(bh * max_parts + pp) * D + d] * fast_exp2(ml[2 * pp] - M);
+    out[bh * D + d] = f2bf(O * ilh[hh]);
   }
 }
 
@@ -386,7 +427,7 @@ __global__ __launch_bounds__(256) void decode_reduce_kernel(
   }
 }
 
-int launch_paged_decode(void* out, float* part_o, float* part_ml, const void* q,
+int launch_paged_decode(void* out, float* part_o, float* part_ml, int* counters, const void* q,
                         int q_stride, const void* k_cache, const void* v_cache,
                         const int* block_tables, int bt_stride,
                         const int* context_lens, int B, int Hq, int Hkv, int D,
@@ -422,18 +463,18 @@ int launch_paged_decode(void* out, float* part_o, float* part_ml, const void* q,
   const size_t lds = (128 + 4 * (size_t)D * 16) * sizeof(float);
   switch (D) {
     case 64:
-      hipLaunchKernelGGL(paged_decode_kernel<64>, grid, block, lds, st, (bf16_t*)out, part_o, part_ml, (const bf16_t*)q, q_stride, (const bf16_t*)k_cache, (const bf16_t*)v_cache, block_tables, bt_stride, context_lens, Hq, Hkv, sl2, max_parts, blocks_per_part);
+      hipLaunchKernelGGL(paged_decode_kernel<64>, grid, block, lds, st, (bf16_t*)out, part_o, part_ml, counters, (const bf16_t*)q, q_stride, (const bf16_t*)k_cache, (const bf16_t*)v_cache, block_tables, bt_stride, context_lens, Hq, Hkv, sl2, max_parts, blocks_per_part);
       break;
     case 128:
-      hipLaunchKernelGGL(paged_decode_kernel<128>, grid, block, lds, st, (bf16_t*)out, part_o, part_ml, (const bf16_t*)q, q_stride, (const bf16_t*)k_cache, (const bf16_t*)v_cache, block_tables, bt_stride, context_lens, Hq, Hkv, sl2, max_parts, blocks_per_part);
+      hipLaunchKernelGGL(paged_decode_kernel<128>, grid, block, lds, st, (bf16_t*)out, part_o, part_ml, counters, (const bf16_t*)q, q_stride, (const bf16_t*)k_cache, (const bf16_t*)v_cache, block_tables, bt_stride, context_lens, Hq, Hkv, sl2, max_parts, blocks_per_part);
       break;
     case 256:
-      hipLaunchKernelGGL(paged_decode_kernel<256>, grid, block, lds, st, (bf16_t*)out, part_o, part_ml, (const bf16_t*)q, q_stride, (const bf16_t*)k_cache, (const bf16_t*)v_cache, block_tables, bt_stride, context_lens, Hq, Hkv, sl2, max_parts, blocks_per_part);
+      hipLaunchKernelGGL(paged_decode_kernel<256>, grid, block, lds, st, (bf16_t*)out, part_o, part_ml, counters, (const bf16_t*)q, q_stride, (const bf16_t*)k_cache, (const bf16_t*)v_cache, block_tables, bt_stride, context_lens, Hq, Hkv, sl2, max_parts, blocks_per_part);
       break;
     default:
       return -1;
   }
-  if (max_parts > 1)
+  if (max_parts > 1 && counters == nullptr)
     hipLaunchKernelGGL(decode_reduce_kernel, dim3(B * Hq), dim3(256), 0, st,
                        (bf16_t*)out, (const float*)part_o, (const float*)part_ml,
                        context_lens, Hq, D, max_parts, blocks_per_part);

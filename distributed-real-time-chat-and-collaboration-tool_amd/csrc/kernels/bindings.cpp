@@ -49,12 +49,12 @@ PYBIND11_MODULE(_hipk, m) {
                                    P<const int>(seg_blk), nseg, Hq, Hkv, D, block_size, S(st));
   });
   m.def("paged_decode",
-        [](u64 out, u64 part_o, u64 part_ml, u64 q, int q_stride, u64 k_cache,
+        [](u64 out, u64 part_o, u64 part_ml, u64 counters, u64 q, int q_stride, u64 k_cache,
            u64 v_cache, u64 block_tables, int bt_stride, u64 context_lens, int B,
            int Hq, int Hkv, int D, float scale, int max_parts,
            int blocks_per_part, int variant, u64 st) {
           return drtc::launch_paged_decode(
-              P<void>(out), P<float>(part_o), P<float>(part_ml), P<const void>(q),
+              P<void>(out), P<float>(part_o), P<float>(part_ml), P<int>(counters), P<const void>(q),
               q_stride, P<const void>(k_cache), P<const void>(v_cache),
               P<const int>(block_tables), bt_stride, P<const int>(context_lens), B,
               Hq, Hkv, D, scale, max_parts, blocks_per_part, variant, S(st));

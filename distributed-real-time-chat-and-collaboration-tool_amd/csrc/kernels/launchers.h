@@ -27,7 +27,7 @@ int launch_kv_write_v(void* v_cache, const void* qkv, int qkv_stride, const int*
                       const int* seg_len, const int* seg_blk, int nseg, int Hq, int Hkv,
                       int D, int block_size, hipStream_t st);
 
-int launch_paged_decode(void* out, float* part_o, float* part_ml, const void* q,
+int launch_paged_decode(void* out, float* part_o, float* part_ml, int* counters, const void* q,
                         int q_stride, const void* k_cache, const void* v_cache,
                         const int* block_tables, int bt_stride,
                         const int* context_lens, int B, int Hq, int Hkv, int D,

@@ -95,6 +95,9 @@ def prefill_attention(qkv: torch.Tensor, cu_seqlens: torch.Tensor, Hq: int, Hkv:
 # merge.  Measured on MI355X (scripts/decode_attn_bench.py, Llama-3-8B heads):
 # equal at batch 1024 (4.8 TB/s), v1 ahead at long contexts.
 DECODE_VARIANT = int(os.environ.get("DRTC_DECODE_VARIANT", "1"))
+# variant 1 merges split-K partitions inside the attention kernel (last
+# workgroup to finish) instead of a separate decode_reduce launch
+FUSED_SPLIT_MERGE = os.environ.get("DRTC_DECODE_FUSED_MERGE", "1") != "0"
 
 
 def decode_partitioning(batch: int, Hkv: int, max_blocks: int, target_wgs: int = 256,
@@ -144,8 +147,11 @@ class DecodeWorkspace:
         if max_parts > 1:
             self.part_o = torch.empty((batch, Hq, max_parts, D), dtype=torch.float32, device=device)
             self.part_ml = torch.empty((batch, Hq, max_parts, 2), dtype=torch.float32, device=device)
+            # per-(sequence, kv head) arrival counters of the in-kernel split-K
+            # merge (variant 1); each launch leaves them at zero
+            self.counters = torch.zeros(batch * Hq, dtype=torch.int32, device=device)
         else:
-            self.part_o = self.part_ml = None
+            self.part_o = self.part_ml = self.counters = None
 
 
 def paged_decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor,
@@ -180,8 +186,9 @@ def paged_decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torc
     if out is None:
         out = torch.empty((B, Hq, D), dtype=q.dtype, device=q.device)
     assert out.is_contiguous() and out.shape == (B, Hq, D)
+    counters = ptr(workspace.counters) if variant == 1 and FUSED_SPLIT_MERGE else 0
     check(hipk().paged_decode(out.data_ptr(), ptr(workspace.part_o), ptr(workspace.part_ml),
-                              q.data_ptr(), q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
+                              counters, q.data_ptr(), q.stride(0), k_cache.data_ptr(), v_cache.data_ptr(),
                               block_tables.data_ptr(), block_tables.stride(0),
                               context_lens.data_ptr(), B, Hq, Hkv, D, float(scale),
                               workspace.max_parts, blocks_per_part, variant, stream_ptr(q)),

@@ -127,6 +127,44 @@ def test_paged_decode(hipk, D, Hq, Hkv, ctx_lens, variant):
     _close(out2, ref, 2e-2, 2e-2, "decode split")
 
 
+def test_paged_decode_fused_split_merge(hipk):
+    """Variant 1's in-kernel split-K merge (last partition workgroup merges)
+    is bitwise equal to the separate decode_reduce launch, leaves its arrival
+    counters at zero, and replays correctly from a hipGraph."""
+    from drtc_amd.ops import attention as attn_ops
+
+    Hq, Hkv, D = 32, 8, 128
+    ctx = [1, 40, 300, 1000, 2048, 129]
+    q, kc, vc, bt, cl = _paged_setup(len(ctx), Hq, Hkv, D, ctx, seed=3)
+    ref = ops.paged_decode_ref(q, kc, vc, bt, cl, D ** -0.5)
+    ws = ops.DecodeWorkspace(len(ctx), Hq, D, math.ceil(bt.shape[1] / 8), DEV)
+    run = lambda: ops.paged_decode_attention(q, kc, vc, bt, cl, D ** -0.5, blocks_per_part=8,
+                                             workspace=ws, variant=1)
+    saved = attn_ops.FUSED_SPLIT_MERGE
+    try:
+        attn_ops.FUSED_SPLIT_MERGE = False
+        unfused = run()
+        attn_ops.FUSED_SPLIT_MERGE = True
+        fused = run()
+        torch.cuda.synchronize()
+        assert torch.equal(fused, unfused)
+        _close(fused, ref, 2e-2, 2e-2, "fused merge")
+        assert int(ws.counters.abs().sum()) == 0
+        out = torch.empty_like(fused)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            ops.paged_decode_attention(q, kc, vc, bt, cl, D ** -0.5, out=out, blocks_per_part=8,
+                                       workspace=ws, variant=1)
+        for _ in range(3):
+            out.zero_()
+            g.replay()
+            torch.cuda.synchronize()
+            assert torch.equal(out, unfused)
+        assert int(ws.counters.abs().sum()) == 0
+    finally:
+        attn_ops.FUSED_SPLIT_MERGE = saved
+
+
 def test_paged_decode_wave_long_partition(hipk):
     """Variant 2 with a partition longer than 64 blocks (block-table slice reload)."""
     Hq, Hkv, D = 32, 8, 128
