@@ -114,6 +114,17 @@ PYBIND11_MODULE(_hipk, m) {
     return drtc::lt_gemm(P<void>(y), P<const void>(x), P<const void>(w), M, N, K, ldx, ldy, S(st));
   });
   m.def("lt_set_algo", &drtc::lt_set_algo);
+  m.def("skinny_glu_gemm", [](u64 y, u64 gu, u64 w, int M, int N, int K, int ldx, int ldy, int act,
+                              u64 st) {
+    return drtc::launch_skinny_glu_gemm(P<void>(y), P<const void>(gu), P<const void>(w), M, N, K,
+                                        ldx, ldy, act, S(st));
+  });
+  m.def("skinny_norm_gemm", [](u64 y, u64 h, u64 x, u64 res, u64 nw, u64 w, int M, int N, int K,
+                               int ldx, int ldr, int ldh, int ldy, float eps, bool gemma, u64 st) {
+    return drtc::launch_skinny_norm_gemm(P<void>(y), P<void>(h), P<const void>(x),
+                                         P<const void>(res), P<const void>(nw), P<const void>(w),
+                                         M, N, K, ldx, ldr, ldh, ldy, eps, gemma, S(st));
+  });
   m.def("skinny_gemm", [](u64 y, u64 x, u64 w, int M, int N, int K, int ldx, int ldy,
                           int variant, u64 st) {
     return drtc::launch_skinny_gemm(P<void>(y), P<const void>(x), P<const void>(w), M, N, K, ldx,

@@ -56,6 +56,19 @@ DRTC_DEVICE f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
+// Gated-MLP activation of the gate value (ACT 0 = SiLU, 1 = tanh-GELU); the
+// one definition shared by act_glu_kernel and the fused skinny GEMM.
+template <int ACT>
+DRTC_DEVICE float act_value(float gf) {
+  if constexpr (ACT == 0) {
+    return gf / (1.f + __expf(-gf));
+  } else {
+    const float k0 = 0.7978845608028654f;  // sqrt(2/pi)
+    const float inner = k0 * (gf + 0.044715f * gf * gf * gf);
+    return 0.5f * gf * (1.f + tanhf(inner));
+  }
+}
+
 DRTC_DEVICE int lane_id() { return threadIdx.x & 63; }
 DRTC_DEVICE int wave_id_uniform() {
   return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);

@@ -33,7 +33,23 @@ DRTC_DEVICE float dot8(const bf16x8& a, const bf16x8& b, float acc) {
   return acc;
 }
 
-template <int MT, int R>
+// x operand of the dot2 form: a plain row chunk, or (ACT >= 0) the gated
+// activation act(gate) * up of a fused [gate | up] row computed on the fly
+// (down projection: the act_glu launch disappears; up half at +K).
+template <int ACT>
+DRTC_DEVICE bf16x8 load_x8(const bf16_t* p, int K) {
+  if constexpr (ACT < 0) {
+    return load_bf16x8(p);
+  } else {
+    const bf16x8 g = load_bf16x8(p), u = load_bf16x8(p + K);
+    bf16x8 o;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) o[q] = f2bf(act_value<ACT>(bf2f(g[q])) * bf2f(u[q]));
+    return o;
+  }
+}
+
+template <int MT, int R, int ACT = -1>
 __global__ __launch_bounds__(256) void skinny_gemm_kernel(bf16_t* __restrict__ y,
                                                           const bf16_t* __restrict__ x,
                                                           const bf16_t* __restrict__ w, int M,
@@ -62,8 +78,8 @@ __global__ __launch_bounds__(256) void skinny_gemm_kernel(bf16_t* __restrict__ y
 #pragma unroll
     for (int m = 0; m < MT; ++m) {
       if (m < M) {
-        xa[m] = load_bf16x8(xrow + (int64_t)m * ldx + c * CH);
-        xb[m] = load_bf16x8(xrow + (int64_t)m * ldx + (c + 4) * CH);
+        xa[m] = load_x8<ACT>(xrow + (int64_t)m * ldx + c * CH, K);
+        xb[m] = load_x8<ACT>(xrow + (int64_t)m * ldx + (c + 4) * CH, K);
       }
     }
 #pragma unroll
@@ -78,7 +94,7 @@ __global__ __launch_bounds__(256) void skinny_gemm_kernel(bf16_t* __restrict__ y
     for (int r = 0; r < R; ++r) wa[r] = load_bf16x8(wrow + (int64_t)r * K + c * CH);
 #pragma unroll
     for (int m = 0; m < MT; ++m)
-      if (m < M) xa[m] = load_bf16x8(xrow + (int64_t)m * ldx + c * CH);
+      if (m < M) xa[m] = load_x8<ACT>(xrow + (int64_t)m * ldx + c * CH, K);
 #pragma unroll
     for (int r = 0; r < R; ++r)
 #pragma unroll
@@ -110,6 +126,170 @@ __global__ __launch_bounds__(256) void skinny_gemm_kernel(bf16_t* __restrict__ y
       y[(int64_t)m * ldy + n0 + r] = f2bf(s);
     }
   }
+}
+
+int launch_skinny_glu_gemm(void* y, const void* gu, const void* w, int M, int N, int K, int ldx,
+                           int ldy, int act, hipStream_t st) {
+  if (M < 1 || M > 2 || K % 512 != 0 || N % 4 != 0 || ldx % 8 != 0 || act < 0 || act > 1)
+    return -1;
+  const dim3 grid(N / 4), block(256);
+  bf16_t* yy = (bf16_t*)y;
+  const bf16_t* xx = (const bf16_t*)gu;
+  const bf16_t* ww = (const bf16_t*)w;
+  if (M == 1) {
+    if (act == 0) skinny_gemm_kernel<1, 4, 0><<<grid, block, 0, st>>>(yy, xx, ww, M, K, ldx, ldy);
+    else skinny_gemm_kernel<1, 4, 1><<<grid, block, 0, st>>>(yy, xx, ww, M, K, ldx, ldy);
+  } else {
+    if (act == 0) skinny_gemm_kernel<2, 4, 0><<<grid, block, 0, st>>>(yy, xx, ww, M, K, ldx, ldy);
+    else skinny_gemm_kernel<2, 4, 1><<<grid, block, 0, st>>>(yy, xx, ww, M, K, ldx, ldy);
+  }
+  return (int)hipGetLastError();
+}
+
+// RMSNorm fused into the dot2 form (decode, M <= 4, K = hidden size with
+// K % 2048 == 0): y = norm(x [+ res]) @ W^T, where h = bf16(x + res) is the
+// new residual stream (written by workgroup 0 to h_out) and norm(h) =
+// bf16(h * rsqrt(mean(h^2) + eps) * w) (Gemma: * (1 + w)) - the semantics of
+// rmsnorm_kernel, so the separate norm launch disappears from the decode
+// step.  Every workgroup needs the full-row sum of squares: its 256 threads
+// hold exactly the x chunks the dot products use (CPW = K / 2048 chunks of 8
+// per thread), so the prologue costs one extra load per chunk (res) and one
+// barrier.  The W loads of all chunks are issued FIRST - they do not depend
+// on x - so their HBM latency covers the norm prologue.  Measured (Llama-3-8B
+// decode, profiles/r1l_skinny_gemm.md): a win at M = 1 only - at M = 2..4 the
+// per-workgroup re-read of the M x K input costs what the saved launch gains
+// (also with 8 W rows per workgroup), so ops.norm_linear fuses at M = 1.
+template <int MT, int CPW, bool GEMMA, int R>
+__global__ __launch_bounds__(256) void skinny_norm_gemm_kernel(
+    bf16_t* __restrict__ y, bf16_t* __restrict__ h_out, const bf16_t* __restrict__ x,
+    const bf16_t* __restrict__ res, const bf16_t* __restrict__ nw,
+    const bf16_t* __restrict__ w, int M, int K, int ldx, int ldr, int ldh, int ldy, float eps) {
+  constexpr int CH = 512;
+  __shared__ float red[4][MT];
+  __shared__ float part[4][R * MT];
+  const int n0 = blockIdx.x * R;
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  bf16x8 wa[CPW][R];
+#pragma unroll
+  for (int j = 0; j < CPW; ++j)
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+      wa[j][r] = load_bf16x8(w + (int64_t)(n0 + r) * K + (wv + 4 * j) * CH + lane * 8);
+  bf16x8 hx[MT][CPW];
+  float ss[MT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {
+    ss[m] = 0.f;
+    if (m >= M) continue;
+#pragma unroll
+    for (int j = 0; j < CPW; ++j) {
+      const int k = (wv + 4 * j) * CH + lane * 8;
+      bf16x8 a = load_bf16x8(x + (int64_t)m * ldx + k);
+      if (res != nullptr) {
+        const bf16x8 rv = load_bf16x8(res + (int64_t)m * ldr + k);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) a[q] = f2bf(bf2f(a[q]) + bf2f(rv[q]));
+        if (blockIdx.x == 0) store_bf16x8(h_out + (int64_t)m * ldh + k, a);
+      }
+      hx[m][j] = a;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) ss[m] += bf2f(a[q]) * bf2f(a[q]);
+    }
+  }
+#pragma unroll
+  for (int m = 0; m < MT; ++m) {
+    const float v = wave_sum(ss[m]);
+    if (lane == 0) red[wv][m] = v;
+  }
+  __syncthreads();
+  float rstd[MT];
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+    rstd[m] = rsqrtf((red[0][m] + red[1][m] + red[2][m] + red[3][m]) / (float)K + eps);
+  float acc[R][MT];
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+#pragma unroll
+    for (int m = 0; m < MT; ++m) acc[r][m] = 0.f;
+#pragma unroll
+  for (int j = 0; j < CPW; ++j) {
+    const bf16x8 gv = load_bf16x8(nw + (wv + 4 * j) * CH + lane * 8);
+    float ww[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) ww[q] = bf2f(gv[q]) + (GEMMA ? 1.f : 0.f);
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      if (m >= M) continue;
+      bf16x8 xn;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) xn[q] = f2bf(bf2f(hx[m][j][q]) * rstd[m] * ww[q]);
+#pragma unroll
+      for (int r = 0; r < R; ++r) acc[r][m] = dot8(wa[j][r], xn, acc[r][m]);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+      float v = acc[r][m];
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+      acc[r][m] = v;
+    }
+  if (lane == 0) {
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+      for (int m = 0; m < MT; ++m) part[wv][r * MT + m] = acc[r][m];
+  }
+  __syncthreads();
+  const int t = threadIdx.x;
+  if (t < R * MT) {
+    const int r = t / MT, m = t - r * MT;
+    if (m < M) {
+      const float s = part[0][t] + part[1][t] + part[2][t] + part[3][t];
+      y[(int64_t)m * ldy + n0 + r] = f2bf(s);
+    }
+  }
+}
+
+template <int MT, bool GEMMA>
+static int launch_norm_mt(bf16_t* y, bf16_t* h, const bf16_t* x, const bf16_t* res,
+                          const bf16_t* nw, const bf16_t* w, int M, int N, int K, int ldx, int ldr,
+                          int ldh, int ldy, float eps, hipStream_t st) {
+  const dim3 grid(N / 4), block(256);
+  switch (K / 2048) {
+    case 1: skinny_norm_gemm_kernel<MT, 1, GEMMA, 4><<<grid, block, 0, st>>>(y, h, x, res, nw, w, M, K, ldx, ldr, ldh, ldy, eps); break;
+    case 2: skinny_norm_gemm_kernel<MT, 2, GEMMA, 4><<<grid, block, 0, st>>>(y, h, x, res, nw, w, M, K, ldx, ldr, ldh, ldy, eps); break;
+    case 4: skinny_norm_gemm_kernel<MT, 4, GEMMA, 4><<<grid, block, 0, st>>>(y, h, x, res, nw, w, M, K, ldx, ldr, ldh, ldy, eps); break;
+    default: return -1;
+  }
+  return 0;
+}
+
+int launch_skinny_norm_gemm(void* y, void* h_out, const void* x, const void* res, const void* nw,
+                            const void* w, int M, int N, int K, int ldx, int ldr, int ldh,
+                            int ldy, float eps, bool gemma, hipStream_t st) {
+  if (M < 1 || M > 4 || K % 2048 != 0 || N % 4 != 0 || ldx % 8 || (res && (ldr % 8 || ldh % 8)) ||
+      (res && !h_out))
+    return -1;
+  bf16_t* yy = (bf16_t*)y;
+  bf16_t* hh = (bf16_t*)h_out;
+  const bf16_t* xx = (const bf16_t*)x;
+  const bf16_t* rr = (const bf16_t*)res;
+  const bf16_t* gg = (const bf16_t*)nw;
+  const bf16_t* ww = (const bf16_t*)w;
+  int rc;
+  if (M == 1)
+    rc = gemma ? launch_norm_mt<1, true>(yy, hh, xx, rr, gg, ww, M, N, K, ldx, ldr, ldh, ldy, eps, st)
+               : launch_norm_mt<1, false>(yy, hh, xx, rr, gg, ww, M, N, K, ldx, ldr, ldh, ldy, eps, st);
+  else if (M == 2)
+    rc = gemma ? launch_norm_mt<2, true>(yy, hh, xx, rr, gg, ww, M, N, K, ldx, ldr, ldh, ldy, eps, st)
+               : launch_norm_mt<2, false>(yy, hh, xx, rr, gg, ww, M, N, K, ldx, ldr, ldh, ldy, eps, st);
+  else
+    rc = gemma ? launch_norm_mt<4, true>(yy, hh, xx, rr, gg, ww, M, N, K, ldx, ldr, ldh, ldy, eps, st)
+               : launch_norm_mt<4, false>(yy, hh, xx, rr, gg, ww, M, N, K, ldx, ldr, ldh, ldy, eps, st);
+  return rc ? rc : (int)hipGetLastError();
 }
 
 // MFMA form for M <= 16: a wave multiplies T 16-row W tiles (A operand,

@@ -78,6 +78,16 @@ std::vector<std::pair<int, float>> lt_tune(void* y, const void* x, const void* w
 int launch_skinny_gemm(void* y, const void* x, const void* w, int M, int N, int K, int ldx,
                        int ldy, int variant, hipStream_t st);
 
+// Gated activation fused into the skinny dot2 GEMM (gemv.hip): y = (act(gu[:, :K]) * gu[:, K:2K]) @ W^T,
+// gu row stride ldx; M <= 2, K % 512 == 0, act 0 = SiLU, 1 = tanh-GELU.
+int launch_skinny_glu_gemm(void* y, const void* gu, const void* w, int M, int N, int K, int ldx,
+                           int ldy, int act, hipStream_t st);
+// RMSNorm (+ residual add) fused into the skinny dot2 GEMM (gemv.hip): y = norm(x [+ res]) @ W^T,
+// h_out = x + res (written when res is given); M <= 4, K % 2048 == 0.
+int launch_skinny_norm_gemm(void* y, void* h_out, const void* x, const void* res, const void* nw,
+                            const void* w, int M, int N, int K, int ldx, int ldr, int ldh,
+                            int ldy, float eps, bool gemma, hipStream_t st);
+
 // Raise the dynamic-LDS ceiling of the kernels that need > 64 KiB (head_dim
 // 256).  Called once at import, before any graph capture.
 int configure_kernels();

@@ -134,16 +134,7 @@ __global__ __launch_bounds__(256) void act_glu_kernel(
     bf16x8 o;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const float gf = bf2f(g[j]);
-      float a;
-      if constexpr (ACT == 0) {
-        a = gf / (1.f + __expf(-gf));
-      } else {
-        const float k0 = 0.7978845608028654f;  // sqrt(2/pi)
-        const float inner = k0 * (gf + 0.044715f * gf * gf * gf);
-        a = 0.5f * gf * (1.f + tanhf(inner));
-      }
-      o[j] = f2bf(a * bf2f(u[j]));
+      o[j] = f2bf(act_value<ACT>(bf2f(g[j])) * bf2f(u[j]));
     }
     store_bf16x8(out + t * I + c, o);
   }

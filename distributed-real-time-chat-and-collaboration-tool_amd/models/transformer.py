@@ -211,12 +211,11 @@ class TransformerLM:
             h = h * float(torch.tensor(math.sqrt(self.cfg.hidden_size), dtype=h.dtype))
         return h
 
-    def _mlp(self, L: dict, x: torch.Tensor) -> torch.Tensor:
+    def _mlp(self, L: dict, x: ops.PendingNorm) -> torch.Tensor:
         if self.cfg.is_moe:
-            return self._moe(L, x)
-        gu = ops.linear(x, L["gate_up"])
-        a = ops.act_glu(gu, self.cfg.act)
-        y = ops.linear(a, L["down"])
+            return self._moe(L, x.materialize())
+        gu = ops.norm_linear(x, L["gate_up"])
+        y = ops.glu_linear(gu, L["down"], self.cfg.act)
         return self.pc.all_reduce_tp(y)
 
     def _moe(self, L: dict, x: torch.Tensor) -> torch.Tensor:
@@ -253,17 +252,19 @@ class TransformerLM:
         return self.pc.all_reduce_tp(out)
 
     def _layers(self, h: torch.Tensor, attn_fn) -> torch.Tensor:
+        """Pre-norm residual stack.  Each sublayer receives its input as an
+        ops.PendingNorm (norm(x + residual) not yet computed), so a small
+        decode batch can fuse the norm into the first projection."""
         cfg = self.cfg
-        residual = h
-        x = ops.rmsnorm(h, self.layers[0]["ln_in"], cfg.rms_eps, cfg.gemma_norm)
+        x = ops.PendingNorm(h, None, self.layers[0]["ln_in"], cfg.rms_eps, cfg.gemma_norm)
         n = len(self.layers)
         for i, L in enumerate(self.layers):
             o = attn_fn(i, L, x)
-            x = ops.rmsnorm(o, L["ln_post"], cfg.rms_eps, cfg.gemma_norm, residual=residual)
+            x = ops.PendingNorm(o, x.stream(), L["ln_post"], cfg.rms_eps, cfg.gemma_norm)
             m = self._mlp(L, x)
             nxt = self.layers[i + 1]["ln_in"] if i + 1 < n else self.final_norm
-            x = ops.rmsnorm(m, nxt, cfg.rms_eps, cfg.gemma_norm, residual=residual)
-        return x
+            x = ops.PendingNorm(m, x.stream(), nxt, cfg.rms_eps, cfg.gemma_norm)
+        return x.materialize()
 
     def _logits(self, x: torch.Tensor) -> torch.Tensor:
         logits = ops.linear(x, self.lm_head)
@@ -275,7 +276,7 @@ class TransformerLM:
         D = cfg.head_dim
 
         def attn(i, L, x):
-            qkv = ops.linear(x, L["qkv"])
+            qkv = ops.norm_linear(x, L["qkv"])
             kc, vc = kv_caches[i] if kv_caches is not None else (None, None)
             blockwise_v = kc is not None and meta.v_segs is not None
             ops.rope_kv_(qkv, meta.positions, meta.slots if kc is not None else None,
@@ -298,7 +299,7 @@ class TransformerLM:
         B = ids.shape[0]
 
         def attn(i, L, x):
-            qkv = ops.linear(x, L["qkv"])
+            qkv = ops.norm_linear(x, L["qkv"])
             kc, vc = kv_caches[i]
             ops.rope_kv_(qkv, meta.positions, meta.slots, self.cos_sin, sh.hq, sh.hkv, D,
                          kc, vc, ops.KV_BLOCK)

@@ -30,7 +30,7 @@ import threading
 import torch
 import torch.nn.functional as F
 
-from ._ext import check, hipk, on_gpu, stream_ptr
+from ._ext import check, hipk, on_gpu, ptr, stream_ptr
 
 TUNED_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuned")
 _lock = threading.Lock()
@@ -169,6 +169,73 @@ def linear(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     return F.linear(x, w)
 
 
+_fuse_norm = os.environ.get("DRTC_FUSED_NORM_GEMM", "1") != "0"
+# measured: the fused norm pays at M = 1 only (gemv.hip skinny_norm_gemm_kernel)
+NORM_FUSE_MAX_M = 1
+
+
+def _choice(M: int, N: int, K: int, ldx: int) -> int:
+    """Skinny variant ops.linear would run for this shape (0 = library)."""
+    ent = _activate().get((M, N, K, ldx))
+    if ent is None:
+        return skinny_variant(M, N, K, ldx)
+    return ent[1] if M <= SKINNY_MAX_M else 0
+
+
+def norm_linear(p, w: torch.Tensor) -> torch.Tensor:
+    """y = rmsnorm(p.x [+ p.residual]) @ w.T for an ``ops.PendingNorm`` p.
+
+    When the projection would run on the skinny dot2 kernel anyway (small
+    decode batches, measured per shape) the norm is fused into it
+    (gemv.hip ``skinny_norm_gemm_kernel``): one launch instead of two, and
+    the new residual stream is written by the GEMM.  Otherwise the norm is
+    materialised and ``linear`` runs."""
+    x, res = p.x, p.residual
+    if (_fuse_norm and p._out is None and on_gpu(x) and _enabled and x.dim() == 2
+            and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and x.stride(1) == 1
+            and w.is_contiguous() and p.w.is_contiguous()
+            and (res is None or (res.stride(1) == 1 and res.shape == x.shape))):
+        M, K = x.shape
+        N = w.shape[0]
+        if (M <= NORM_FUSE_MAX_M and K % 2048 == 0 and K <= 8192 and N % 4 == 0 and x.stride(0) % 8 == 0
+                and (res is None or res.stride(0) % 8 == 0) and _choice(M, N, K, K) == 1):
+            y = torch.empty((M, N), dtype=x.dtype, device=x.device)
+            h = torch.empty((M, K), dtype=x.dtype, device=x.device) if res is not None else None
+            check(hipk().skinny_norm_gemm(
+                y.data_ptr(), ptr(h), x.data_ptr(), ptr(res), p.w.data_ptr(), w.data_ptr(), M, N,
+                K, x.stride(0), res.stride(0) if res is not None else 0, K, N, float(p.eps),
+                bool(p.gemma), stream_ptr(x)), "skinny_norm_gemm")
+            p.applied(h if h is not None else x)
+            return y
+    return linear(p.materialize(), w)
+
+
+_fuse_glu = os.environ.get("DRTC_FUSED_GLU_GEMM", "1") != "0"
+GLU_FUSE_MAX_M = 1
+
+
+def glu_linear(gu: torch.Tensor, w: torch.Tensor, act: str = "silu") -> torch.Tensor:
+    """y = (act(gu[:, :I]) * gu[:, I:]) @ w.T (the down projection of a gated
+    MLP).  When the projection would run on the skinny dot2 kernel the
+    activation is computed inside it while loading its input (gemv.hip,
+    no act_glu launch); otherwise ops.act_glu + linear."""
+    from .activation import act_glu
+
+    if (_fuse_glu and on_gpu(gu) and _enabled and gu.dim() == 2 and gu.dtype == torch.bfloat16
+            and w.dtype == torch.bfloat16 and gu.stride(1) == 1 and w.is_contiguous()
+            and act in ("silu", "gelu_tanh")):
+        M, I2 = gu.shape
+        I, N = I2 // 2, w.shape[0]
+        if (M <= GLU_FUSE_MAX_M and I2 % 2 == 0 and w.shape[1] == I and I % 512 == 0
+                and N % 4 == 0 and gu.stride(0) % 8 == 0 and _choice(M, N, I, I) == 1):
+            y = torch.empty((M, N), dtype=gu.dtype, device=gu.device)
+            check(hipk().skinny_glu_gemm(y.data_ptr(), gu.data_ptr(), w.data_ptr(), M, N, I,
+                                         gu.stride(0), N, 0 if act == "silu" else 1,
+                                         stream_ptr(gu)), "skinny_glu_gemm")
+            return y
+    return linear(act_glu(gu, act), w)
+
+
 def tune(M: int, N: int, K: int, device, iters: int = 20, max_candidates: int = 12) -> dict:
     """Measure every hipBLASLt solution for y[M,N] = x[M,K] @ W[N,K]^T on
     random operands; returns {"algo", "us", "heuristic_us", "candidates"}."""
@@ -204,4 +271,4 @@ def save_entries(entries: dict[str, dict], path: str | None = None) -> str:
     return path
 
 
-__all__ = ["linear", "skinny_linear", "skinny_ok", "skinny_variant", "skinny_supports", "tune", "save_entries", "load_table", "reset", "set_enabled", "table_path"]
+__all__ = ["linear", "norm_linear", "glu_linear", "skinny_linear", "skinny_ok", "skinny_variant", "skinny_supports", "tune", "save_entries", "load_table", "reset", "set_enabled", "table_path"]

@@ -46,3 +46,38 @@ def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float, gemma: bool = False,
                          rows, H, float(eps), x.stride(0), out.stride(0), res_stride,
                          bool(gemma), stream_ptr(x)), "rmsnorm")
     return out
+
+
+class PendingNorm:
+    """A pre-norm sublayer input whose RMSNorm has not run yet: norm(x [+
+    residual]) * w.  The consumer either fuses the norm into its projection
+    (``ops.norm_linear``: small decode batches, csrc/kernels/gemv.hip) or
+    calls ``materialize()`` for the plain normalised tensor.  Either way
+    ``stream()`` afterwards is the post-add residual stream h = x + residual
+    (x itself when there is no residual), which the next PendingNorm adds to.
+    """
+
+    __slots__ = ("x", "residual", "w", "eps", "gemma", "_h", "_out")
+
+    def __init__(self, x: torch.Tensor, residual: torch.Tensor | None, w: torch.Tensor,
+                 eps: float, gemma: bool):
+        self.x, self.residual, self.w, self.eps, self.gemma = x, residual, w, eps, gemma
+        self._h: torch.Tensor | None = None
+        self._out: torch.Tensor | None = None
+
+    def applied(self, h: torch.Tensor) -> None:
+        """Record that a fused consumer computed h = x (+ residual)."""
+        self._h, self.x, self.residual = h, h, None
+
+    def materialize(self) -> torch.Tensor:
+        if self._out is None:
+            res = self.residual
+            self._out = rmsnorm(self.x, self.w, self.eps, self.gemma, residual=res)
+            self._h = res if res is not None else self.x  # rmsnorm updated res in place
+            self.x, self.residual = self._h, None
+        return self._out
+
+    def stream(self) -> torch.Tensor:
+        if self._h is None:
+            self.materialize()
+        return self._h

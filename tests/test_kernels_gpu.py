@@ -397,6 +397,73 @@ def test_skinny_gemm(hipk, M, N, K, ldx):
     _close(yg, x.float() @ w.float().t(), 2e-2, 2e-2, "skinny gemm (graph)")
 
 
+@pytest.mark.parametrize("M", [1, 2, 3, 4])
+@pytest.mark.parametrize("K", [2048, 4096, 8192])
+@pytest.mark.parametrize("resid,gemma", [(True, False), (False, False), (True, True)])
+def test_skinny_norm_gemm(hipk, M, K, resid, gemma):
+    """RMSNorm (+ residual add) fused into the skinny dot2 GEMM (gemv.hip):
+    y matches fp32 norm-then-project, the new residual stream is exactly
+    bf16(x + res), and the PendingNorm bookkeeping hands it on."""
+    from drtc_amd.ops import gemm
+
+    torch.manual_seed(M * 7 + K)
+    N = 1028
+    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    res = torch.randn(M, K, device=DEV).to(torch.bfloat16) if resid else None
+    nw = (torch.randn(K, device=DEV) * 0.1 + (0.0 if gemma else 1.0)).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=DEV) * 0.02).to(torch.bfloat16)
+    h_ref = (x.float() + res.float()).to(torch.bfloat16) if resid else x
+    xn = ops.rmsnorm_ref(h_ref, nw, 1e-5, gemma)
+    y_ref = xn.float() @ w.float().t()
+    saved, saved_max = gemm._table, gemm.NORM_FUSE_MAX_M
+    try:
+        gemm.NORM_FUSE_MAX_M = 4  # the kernel covers M <= 4; the engine fuses at M = 1
+        gemm._table = {(M, N, K, K): (-1, 1)}  # measured pick: dot2 kernel
+        p = ops.PendingNorm(x, res.clone() if resid else None, nw, 1e-5, gemma)
+        y = ops.norm_linear(p, w)
+        torch.cuda.synchronize()
+        assert p._out is None, "norm was not fused"
+        assert torch.equal(p.stream(), h_ref)
+        _close(y, y_ref, 3e-2, 2e-2, "norm gemm")
+        # unfused path gives the same stream and (within rounding) the same y
+        gemm._table = {(M, N, K, K): (-1, 0)}
+        q = ops.PendingNorm(x, res.clone() if resid else None, nw, 1e-5, gemma)
+        y2 = ops.norm_linear(q, w)
+        assert q._out is not None
+        assert torch.equal(q.stream(), h_ref)
+        _close(y2, y, 3e-2, 2e-2, "fused vs unfused")
+    finally:
+        gemm._table, gemm.NORM_FUSE_MAX_M = saved, saved_max
+
+
+@pytest.mark.parametrize("M", [1, 2])
+@pytest.mark.parametrize("I", [512, 1536, 14336])
+@pytest.mark.parametrize("act", ["silu", "gelu_tanh"])
+def test_skinny_glu_gemm(hipk, M, I, act):
+    """Gated activation fused into the skinny dot2 GEMM (gemv.hip): bitwise
+    the same operand as ops.act_glu, so y matches act_glu + linear."""
+    from drtc_amd.ops import gemm
+
+    torch.manual_seed(M + I)
+    N = 1028
+    gu = (torch.randn(M, 2 * I, device=DEV) * 2).to(torch.bfloat16)
+    w = (torch.randn(N, I, device=DEV) * 0.02).to(torch.bfloat16)
+    a = ops.act_glu(gu, act)
+    _close(a, ops.act_glu_ref(gu, act), 3e-2, 1e-2, "act")
+    y_ref = a.float() @ w.float().t()
+    saved, saved_max = gemm._table, gemm.GLU_FUSE_MAX_M
+    try:
+        gemm.GLU_FUSE_MAX_M = 2
+        gemm._table = {(M, N, I, I): (-1, 1)}
+        y = ops.glu_linear(gu, w, act)
+        _close(y, y_ref, 2e-2, 2e-2, "glu gemm")
+        y_unfused = gemm.skinny_linear(a, w, 1)
+        torch.cuda.synchronize()
+        assert torch.equal(y, y_unfused)  # same operand, same kernel order
+    finally:
+        gemm._table, gemm.GLU_FUSE_MAX_M = saved, saved_max
+
+
 @pytest.mark.parametrize("e_off,e_local", [(0, 8), (2, 3)])
 def test_moe_sorted_library_path(hipk, e_off, e_local):
     """Large eager MoE calls take the sorted per-expert hipBLASLt path."""
