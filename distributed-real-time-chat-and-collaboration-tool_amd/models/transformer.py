@@ -213,10 +213,22 @@ class TransformerLM:
 
     def _mlp(self, L: dict, x: ops.PendingNorm) -> torch.Tensor:
         if self.cfg.is_moe:
-            return self._moe(L, x.materialize())
+            return self._moe(L, x.materialize()), False
         gu = ops.norm_linear(x, L["gate_up"])
+        res = self._fusable_residual(gu, x)
+        if res is not None:
+            return ops.linear_residual(ops.act_glu(gu, self.cfg.act), L["down"], res), True
         y = ops.glu_linear(gu, L["down"], self.cfg.act)
-        return self.pc.all_reduce_tp(y)
+        return self.pc.all_reduce_tp(y), False
+
+    def _fusable_residual(self, a: torch.Tensor, x: ops.PendingNorm) -> torch.Tensor | None:
+        """The residual stream the o / down projection may add into inside its
+        GEMM epilogue (ops.linear_residual: prefill-sized passes, TP=1, where
+        the all-reduce would otherwise have to come before the add)."""
+        if self.pc.tp_size != 1:
+            return None
+        res = x.stream()
+        return res if ops.residual_fusable(a, res) else None
 
     def _moe(self, L: dict, x: torch.Tensor) -> torch.Tensor:
         """Top-k routed experts (Mixtral: softmax over the top-2 logits).
@@ -259,11 +271,14 @@ class TransformerLM:
         x = ops.PendingNorm(h, None, self.layers[0]["ln_in"], cfg.rms_eps, cfg.gemma_norm)
         n = len(self.layers)
         for i, L in enumerate(self.layers):
-            o = attn_fn(i, L, x)
-            x = ops.PendingNorm(o, x.stream(), L["ln_post"], cfg.rms_eps, cfg.gemma_norm)
-            m = self._mlp(L, x)
+            # (o, added): added = the projection already added the residual
+            # stream in its GEMM epilogue, o IS the new stream
+            o, added = attn_fn(i, L, x)
+            x = ops.PendingNorm(o, None if added else x.stream(), L["ln_post"], cfg.rms_eps,
+                                cfg.gemma_norm)
+            m, added = self._mlp(L, x)
             nxt = self.layers[i + 1]["ln_in"] if i + 1 < n else self.final_norm
-            x = ops.PendingNorm(m, x.stream(), nxt, cfg.rms_eps, cfg.gemma_norm)
+            x = ops.PendingNorm(m, None if added else x.stream(), nxt, cfg.rms_eps, cfg.gemma_norm)
         return x.materialize()
 
     def _logits(self, x: torch.Tensor) -> torch.Tensor:
@@ -286,7 +301,10 @@ class TransformerLM:
                 ops.kv_write_v(vc, qkv, meta.v_segs, sh.hq, sh.hkv, D)
             a = ops.prefill_attention(qkv, meta.cu_seqlens, sh.hq, sh.hkv, D, cfg.attn_scale,
                                       True, tiles=meta.tiles, cu_host=meta.cu_host)
-            return self.pc.all_reduce_tp(ops.linear(a, L["o"]))
+            res = self._fusable_residual(a, x)
+            if res is not None:
+                return ops.linear_residual(a, L["o"], res), True
+            return self.pc.all_reduce_tp(ops.linear(a, L["o"])), False
 
         x = self._layers(self._embed(ids), attn)
         return self._logits(x.index_select(0, meta.last_idx))
@@ -308,7 +326,7 @@ class TransformerLM:
                                            cfg.attn_scale, out=attn_out,
                                            blocks_per_part=meta.blocks_per_part,
                                            workspace=meta.workspace)
-            return self.pc.all_reduce_tp(ops.linear(a.view(B, sh.hq * D), L["o"]))
+            return self.pc.all_reduce_tp(ops.linear(a.view(B, sh.hq * D), L["o"])), False
 
         x = self._layers(self._embed(ids), attn)
         return self._logits(x)

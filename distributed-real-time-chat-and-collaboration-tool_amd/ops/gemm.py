@@ -169,6 +169,34 @@ def linear(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     return F.linear(x, w)
 
 
+_fuse_residual = os.environ.get("DRTC_RESIDUAL_GEMM", "1") != "0"
+# measured (scripts/residual_gemm_bench.py, MI355X, H=4096): at 16k rows the
+# beta=1 GEMM costs the same as beta=0 while the following RMSNorm drops from
+# ~90 us (read x + residual, write both) to ~39 us (read h, write out); at
+# 1024 rows both norms are launch-latency bound (7-8 us) - no gain
+RESIDUAL_FUSE_MIN_M = 4096
+
+
+def residual_fusable(x: torch.Tensor, residual: torch.Tensor) -> bool:
+    """Whether ``linear_residual`` pays for x [M, K] -> residual [M, N]: on
+    the GPU at prefill-sized M (bf16).  Elsewhere the caller runs ``linear``
+    and leaves the add to the next fused add-RMSNorm."""
+    return (_fuse_residual and on_gpu(x) and x.dim() == 2 and x.shape[0] >= RESIDUAL_FUSE_MIN_M
+            and x.dtype == residual.dtype == torch.bfloat16
+            and residual.dim() == 2 and residual.shape[0] == x.shape[0]
+            and residual.stride(1) == 1)
+
+
+def linear_residual(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor) -> torch.Tensor:
+    """residual += x @ w.T with the add in the GEMM epilogue (beta = 1, in
+    place into the residual stream), for the o / down projections of a
+    prefill pass; returns the updated residual.  One rounding to bf16 (of
+    the fp32 accumulator plus the residual) instead of two (GEMM output,
+    then the add in the norm kernel)."""
+    assert residual.shape == (x.shape[0], w.shape[0]) and w.dtype == x.dtype
+    return residual.addmm_(x, w.t())
+
+
 _fuse_norm = os.environ.get("DRTC_FUSED_NORM_GEMM", "1") != "0"
 # measured: the fused norm pays at M = 1 only (gemv.hip skinny_norm_gemm_kernel)
 NORM_FUSE_MAX_M = 1

@@ -478,3 +478,17 @@ def test_moe_sorted_library_path(hipk, e_off, e_local):
     out = ops.fused_moe(x, lg, wgu, wdn, k, num_experts=E, e_off=e_off)
     ref = moe_ops.fused_moe_ref(x, lg, wgu, wdn, k, e_off=e_off)
     _close(out, ref, 1e-2, 2e-2, "moe library path")
+
+
+@pytest.mark.parametrize("M,N,K", [(4096, 4096, 4096), (4352, 2048, 5632)])
+def test_linear_residual(hipk, M, N, K):
+    """residual += x @ w.T in the GEMM epilogue (ops.linear_residual) vs fp32."""
+    torch.manual_seed(3)
+    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=DEV) * 0.05).to(torch.bfloat16)
+    res = torch.randn(M, N, device=DEV).to(torch.bfloat16)
+    ref = x.float() @ w.float().t() + res.float()
+    assert ops.residual_fusable(x, res)
+    y = ops.linear_residual(x, w, res)
+    assert y.data_ptr() == res.data_ptr()
+    _close(y, ref, 3e-2, 2e-2, "linear_residual")
