@@ -18,6 +18,7 @@ int launch_rmsnorm(void* out, void* residual, const void* x, const void* w,
 int launch_act_glu(void* out, const void* gu, int64_t T, int I, int gu_stride,
                    int act, hipStream_t st);
 
+void set_rope_variant(int v);
 int launch_rope_kv(void* qkv, int T, int qkv_stride, const int* positions,
                    const int64_t* slots, const float* cos_sin, int Hq, int Hkv,
                    int D, void* k_cache, void* v_cache, int block_size, int write_v,

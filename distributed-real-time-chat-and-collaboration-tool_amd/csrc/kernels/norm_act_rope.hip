@@ -215,11 +215,99 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(
   }
 }
 
+// v2: a single pass over rope items + V items (block = their count rounded
+// up to whole waves, looping only past 1024), cos/sin read as 16-B vectors,
+// and the V scatter mapped one cache dim per lane: a wave's stores then hit
+// 64 consecutive 8-B slots of the dim-major V group (4 cache lines) instead of
+// 8 dims per lane (every store instruction spread over 32 lines).  Same math
+// and cache contents as rope_kv_kernel.
+template <int D>
+__global__ __launch_bounds__(1024) void rope_kv_kernel_v2(
+    bf16_t* __restrict__ qkv, int qkv_stride, const int* __restrict__ positions,
+    const int64_t* __restrict__ slots, const float* __restrict__ cos_sin,
+    int Hq, int Hkv, bf16_t* __restrict__ k_cache,
+    bf16_t* __restrict__ v_cache, int block_size, int write_v) {
+  constexpr int HV = D / 16;
+  const int t = blockIdx.x;
+  const int n_rope = (Hq + Hkv) * HV;
+  const int pos = positions[t];
+  const int64_t slot = slots ? slots[t] : -1;
+  const int n_items = n_rope + ((slot >= 0 && write_v) ? Hkv * (D / 2) : 0);
+  bf16_t* row = qkv + (int64_t)t * qkv_stride;
+  int64_t blk = 0, off = 0;
+  if (slot >= 0) {
+    blk = slot / block_size;
+    off = slot - blk * block_size;
+  }
+  for (int item = threadIdx.x; item < n_items; item += blockDim.x) {
+    if (item < n_rope) {
+      const int head = item / HV;
+      const int vi = item - head * HV;
+      const float* cs = cos_sin + (int64_t)pos * D + vi * 8;
+      const f32x4 ca = *reinterpret_cast<const f32x4*>(cs);
+      const f32x4 cb = *reinterpret_cast<const f32x4*>(cs + 4);
+      const f32x4 sa = *reinterpret_cast<const f32x4*>(cs + D / 2);
+      const f32x4 sb = *reinterpret_cast<const f32x4*>(cs + D / 2 + 4);
+      bf16_t* base = row + head * D + vi * 8;
+      const bf16x8 x1 = load_bf16x8(base);
+      const bf16x8 x2 = load_bf16x8(base + D / 2);
+      bf16x8 o1, o2;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float c = j < 4 ? ca[j] : cb[j - 4];
+        const float sn = j < 4 ? sa[j] : sb[j - 4];
+        const float a = bf2f(x1[j]), b = bf2f(x2[j]);
+        o1[j] = f2bf(a * c - b * sn);
+        o2[j] = f2bf(b * c + a * sn);
+      }
+      store_bf16x8(base, o1);
+      store_bf16x8(base + D / 2, o2);
+      if (head >= Hq && slot >= 0) {
+        bf16_t* kd = k_cache + ((blk * Hkv + (head - Hq)) * block_size + off) * D + vi * 8;
+        store_bf16x8(kd, o1);
+        store_bf16x8(kd + D / 2, o2);
+      }
+    } else {
+      // V block layout: [block_size/4 groups][D][4 tokens] (see kv_write_v)
+      const int vitem = item - n_rope;
+      const int h = vitem / (D / 2);
+      const int d = vitem - h * (D / 2);
+      const bf16_t* src = row + (Hq + Hkv + h) * D + d;
+      bf16_t* vd = v_cache + (blk * Hkv + h) * D * block_size + (off >> 2) * (4 * D) + d * 4 +
+                   (off & 3);
+      const bf16_t v0 = src[0], v1 = src[D / 2];
+      vd[0] = v0;
+      vd[2 * D] = v1;  // dim d + D/2: 4 * (D/2) elements further
+    }
+  }
+}
+
+static int g_rope_variant = 2;
+void set_rope_variant(int v) { g_rope_variant = v; }
+
 int launch_rope_kv(void* qkv, int T, int qkv_stride, const int* positions,
                    const int64_t* slots, const float* cos_sin, int Hq, int Hkv,
                    int D, void* k_cache, void* v_cache, int block_size, int write_v,
                    hipStream_t st) {
   if (T == 0) return 0;
+  const int items = (Hq + Hkv) * (D / 16) + (slots && write_v ? Hkv * (D / 2) : 0);
+  if (g_rope_variant == 2) {
+    dim3 grid(T), block(std::min(1024, (items + 63) / 64 * 64));
+    switch (D) {
+      case 64:
+        hipLaunchKernelGGL(rope_kv_kernel_v2<64>, grid, block, 0, st, (bf16_t*)qkv, qkv_stride, positions, slots, cos_sin, Hq, Hkv, (bf16_t*)k_cache, (bf16_t*)v_cache, block_size, write_v);
+        break;
+      case 128:
+        hipLaunchKernelGGL(rope_kv_kernel_v2<128>, grid, block, 0, st, (bf16_t*)qkv, qkv_stride, positions, slots, cos_sin, Hq, Hkv, (bf16_t*)k_cache, (bf16_t*)v_cache, block_size, write_v);
+        break;
+      case 256:
+        hipLaunchKernelGGL(rope_kv_kernel_v2<256>, grid, block, 0, st, (bf16_t*)qkv, qkv_stride, positions, slots, cos_sin, Hq, Hkv, (bf16_t*)k_cache, (bf16_t*)v_cache, block_size, write_v);
+        break;
+      default:
+        return -1;
+    }
+    return (int)hipGetLastError();
+  }
   dim3 grid(T), block(256);
   switch (D) {
     case 64:

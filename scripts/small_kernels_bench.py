@@ -35,9 +35,14 @@ def main():
     slots = (torch.randperm(nb - 1, device=dev)[:B] + 1).to(torch.int64) * 32 + \
         torch.randint(0, 32, (B,), device=dev)
     byts = qkv.numel() * 2 * 2 + B * Hkv * D * 2 * 2
-    for wv in (True, False):
-        us = timeit(lambda: ops.rope_kv_(qkv, pos, slots, cs, Hq, Hkv, D, kc, vc, 32, write_v=wv))
-        print(f"rope_kv B={B} write_v={wv}: {us:7.1f} us  {byts / us / 1e3:6.0f} GB/s", flush=True)
+    from drtc_amd.ops._ext import hipk
+    for variant in (1, 2):  # 1 = 256-thread loop, 2 = one item per thread (default)
+        hipk().set_rope_variant(variant)
+        for wv in (True, False):
+            us = timeit(lambda: ops.rope_kv_(qkv, pos, slots, cs, Hq, Hkv, D, kc, vc, 32, write_v=wv))
+            print(f"rope_kv v{variant} B={B} write_v={wv}: {us:7.1f} us  {byts / us / 1e3:6.0f} GB/s",
+                  flush=True)
+    hipk().set_rope_variant(2)
     x = torch.randn(B, H, device=dev).to(torch.bfloat16)
     r = torch.randn(B, H, device=dev).to(torch.bfloat16)
     w = torch.ones(H, device=dev, dtype=torch.bfloat16)

@@ -49,7 +49,8 @@ def test_act_glu(hipk, act, T, I):
     _close(ops.act_glu(gu, act), ops.act_glu_ref(gu, act), 3e-2, 1e-2, act)
 
 
-@pytest.mark.parametrize("D,Hq,Hkv", [(128, 32, 8), (256, 8, 1), (64, 4, 2)])
+# (128, 64, 8): 1088 items per token, more than one 1024-thread pass of rope_kv_kernel_v2
+@pytest.mark.parametrize("D,Hq,Hkv", [(128, 32, 8), (256, 8, 1), (64, 4, 2), (128, 64, 8)])
 def test_rope_kv(hipk, D, Hq, Hkv):
     torch.manual_seed(1)
     T, nb, bs = 70, 16, ops.KV_BLOCK
