@@ -301,13 +301,21 @@ class TransformerLM:
                 ops.kv_write_v(vc, qkv, meta.v_segs, sh.hq, sh.hkv, D)
             a = ops.prefill_attention(qkv, meta.cu_seqlens, sh.hq, sh.hkv, D, cfg.attn_scale,
                                       True, tiles=meta.tiles, cu_host=meta.cu_host)
+            if i == last:
+                # Every position's K/V is cached and attended to by now; only
+                # each sequence's last token feeds the logits, so the last
+                # layer's o-projection, MLP and final norm run on those rows
+                # alone (exact: the other rows' outputs are never read).
+                a = a.index_select(0, meta.last_idx)
+                x.select_rows(meta.last_idx)
             res = self._fusable_residual(a, x)
             if res is not None:
                 return ops.linear_residual(a, L["o"], res), True
             return self.pc.all_reduce_tp(ops.linear(a, L["o"])), False
 
+        last = len(self.layers) - 1
         x = self._layers(self._embed(ids), attn)
-        return self._logits(x.index_select(0, meta.last_idx))
+        return self._logits(x)
 
     def forward_decode(self, ids: torch.Tensor, meta: DecodeMeta, kv_caches,
                        attn_out: torch.Tensor | None = None) -> torch.Tensor:

@@ -81,3 +81,16 @@ class PendingNorm:
         if self._h is None:
             self.materialize()
         return self._h
+
+    def select_rows(self, idx: torch.Tensor) -> None:
+        """Keep only the rows ``idx`` (int64) of every tensor this input holds:
+        the last layer of a prefill pass continues with each sequence's last
+        token only once its attention has read (and cached) every position."""
+        if self._out is not None:
+            self._out = self._out.index_select(0, idx)
+        if self._h is not None:  # x is _h (materialize / applied alias them)
+            self._h = self.x = self._h.index_select(0, idx)
+            return
+        self.x = self.x.index_select(0, idx)
+        if self.residual is not None:
+            self.residual = self.residual.index_select(0, idx)

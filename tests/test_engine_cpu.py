@@ -25,6 +25,30 @@ def test_engine_greedy_matches_full_forward(cfg):
     assert eng.alloc.num_used == 0
 
 
+@pytest.mark.parametrize("cfg", [TINY_LLAMA, TINY_MIXTRAL], ids=lambda c: c.name)
+def test_packed_prefill_last_layer_pruning(cfg):
+    """forward_prefill runs the last layer's o-projection / MLP / final norm
+    on each sequence's last token only: the packed logits equal the last rows
+    of the unpruned per-sequence forward (last_idx = every position)."""
+    from drtc_amd.models.transformer import PrefillMeta
+
+    m = TransformerLM(cfg, "cpu", seed=7)
+    seqs = [list(range(1, 12)), [3, 4], list(range(5, 45))]
+    cu = [0]
+    for s in seqs:
+        cu.append(cu[-1] + len(s))
+    ids = torch.tensor(sum(seqs, []), dtype=torch.long)
+    pos = torch.cat([torch.arange(len(s), dtype=torch.int32) for s in seqs])
+    meta = PrefillMeta(positions=pos, slots=torch.full((cu[-1],), -1, dtype=torch.int64),
+                       cu_seqlens=torch.tensor(cu, dtype=torch.int32), cu_host=cu, tiles=None,
+                       last_idx=torch.tensor(cu[1:], dtype=torch.int64) - 1)
+    got = m.forward_prefill(ids, meta, None).float()
+    assert got.shape[0] == len(seqs)
+    for j, s in enumerate(seqs):
+        ref = m.forward_reference([s])[0][-1].float()
+        assert (got[j] - ref).abs().max() <= 2e-2 * max(1.0, ref.abs().max().item())
+
+
 def test_engine_preemption_and_recompute():
     m = TransformerLM(TINY_LLAMA, "cpu", seed=3)
     eng = LLMEngine(m, max_batch=8, max_model_len=512, num_blocks=12, use_graphs=False)
