@@ -18,22 +18,28 @@
 //
 // Memory: one uncached (fine-grained) device allocation per rank, mapped
 // into the peers with hipIpcOpenMemHandle:
-//   [0, 2 KiB)        flags[block][src_rank]   written remotely by peers
-//   [2 KiB, 2.25 KiB) per-block epoch counters (local)
-//   [2.25 KiB, +4)    error word (a flag wait that timed out)
-//   [4 KiB, 6 KiB)    phase-2 flags[block][src_rank] (two-shot)
-//   [8 KiB, ...)      input staging, then two-shot result staging, each
+//   [0, 4 KiB)        flags[block][src_rank] (u64 epochs) written remotely by peers
+//   [4 KiB, 8 KiB)    phase-2 flags[block][src_rank] (two-shot)
+//   [8 KiB, +512)     per-block epoch counters (u64, local)
+//   [8.5 KiB, +4)     error word (a flag wait that timed out)
+//   [16 KiB, ...)     input staging, then two-shot result staging, each
 //                     double-buffered by epoch parity
-// Synchronisation is per block: block b of every rank owns the same chunk of
-// the message, so block b only waits for block b of the peers (no grid-wide
-// barrier, no deadlock whatever the residency).  Epochs grow monotonically,
-// so flags never need resetting and the kernel is hipGraph-replayable.  The
-// double buffer makes a second barrier unnecessary: a rank can reuse a
-// staging half only two calls later, after every peer has raised a flag for
-// the intermediate call, i.e. after it finished reading the half.
+// Synchronisation is per block: the message is cut into FIXED chunks of
+// `chunk` vectors (stage_elems / 64 blocks, the same for every call of a
+// communicator), block b always owns chunk b, and block b only waits for
+// block b of the peers (no grid-wide barrier, no deadlock whatever the
+// residency).  Because chunk b's staging range never depends on the message
+// size, the double buffer needs no second barrier even across calls of
+// different sizes: block b reuses a staging half only two of ITS calls later,
+// after every peer's block b has raised a flag for the intermediate call,
+// i.e. after it finished reading the half.  Epochs are 64-bit and grow
+// monotonically (no wrap in any realistic uptime: 2^64 calls), so flags never
+// need resetting and the kernel is hipGraph-replayable.
 //
 // Every flag wait has a wall-clock bound (s_memrealtime, 100 MHz): a missing
-// peer sets the error word and the kernel drains instead of hanging the GPU.
+// peer sets the error word and the kernel drains instead of hanging the GPU;
+// the TP engine checks the word at every step boundary and fails the group
+// (parallel/tp_engine.py).
 #include "common.h"
 #include "launchers.h"
 
@@ -41,19 +47,21 @@ namespace drtc {
 
 constexpr int kArMaxBlocks = 64;
 constexpr int kArMaxRanks = 8;
-constexpr int64_t kArHeader = 8192;
+constexpr int64_t kArHeader = 16384;
 constexpr int64_t kArFlags2 = 4096;
+constexpr int64_t kArCounters = 8192;
+constexpr int64_t kArError = 8192 + 512;
 constexpr uint64_t kArTimeoutTicks = 200000000ull;  // 2 s at 100 MHz
 
 // Publish `epoch` into every peer's flag slot [b][rank] and wait until every
 // peer has published it into ours (thread q < world handles peer q).
-DRTC_DEVICE void ar_exchange(const ArPeers& P, int64_t flag_off, int* my_flags, int* err, int b,
-                             int rank, int world, int epoch) {
+DRTC_DEVICE void ar_exchange(const ArPeers& P, int64_t flag_off, uint64_t* my_flags, int* err,
+                             int b, int rank, int world, uint64_t epoch) {
   const int tid = threadIdx.x;
   if (tid < world) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    int* peer_flags = reinterpret_cast<int*>(P.base[tid] + flag_off);
+    uint64_t* peer_flags = reinterpret_cast<uint64_t*>(P.base[tid] + flag_off);
     __hip_atomic_store(peer_flags + b * kArMaxRanks + rank, epoch, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_SYSTEM);
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
@@ -72,24 +80,23 @@ DRTC_DEVICE void ar_exchange(const ArPeers& P, int64_t flag_off, int* my_flags, 
 
 __global__ __launch_bounds__(512) void custom_allreduce_2shot_kernel(
     bf16_t* __restrict__ out, const bf16_t* __restrict__ in, ArPeers P, int rank, int world,
-    int64_t n8, int64_t stage_elems) {
-  __shared__ int s_epoch;
-  const int b = blockIdx.x, nb = gridDim.x, tid = threadIdx.x;
+    int64_t n8, int64_t stage_elems, int64_t chunk) {
+  __shared__ uint64_t s_epoch;
+  const int b = blockIdx.x, tid = threadIdx.x;
   char* mine = P.base[rank];
-  int* ctr = reinterpret_cast<int*>(mine + 2048);
-  int* err = reinterpret_cast<int*>(mine + 2048 + 256);
+  uint64_t* ctr = reinterpret_cast<uint64_t*>(mine + kArCounters);
+  int* err = reinterpret_cast<int*>(mine + kArError);
   if (tid == 0) {
-    const int e = ctr[b] + 1;
+    const uint64_t e = ctr[b] + 1;
     ctr[b] = e;
     s_epoch = e;
   }
   __syncthreads();
-  const int epoch = s_epoch;
+  const uint64_t epoch = s_epoch;
   const int64_t in_off = kArHeader + (int64_t)(epoch & 1) * stage_elems * 2;
   const int64_t res_off = kArHeader + (int64_t)(2 + (epoch & 1)) * stage_elems * 2;
-  const int64_t per = (n8 + nb - 1) / nb;
-  const int64_t c0 = (int64_t)b * per;
-  const int64_t c1 = c0 + per < n8 ? c0 + per : n8;
+  const int64_t c0 = (int64_t)b * chunk;  // fixed per block, whatever the message size
+  const int64_t c1 = c0 + chunk < n8 ? c0 + chunk : n8;
   const int64_t sub = (c1 - c0 + world - 1) / world;  // sub-chunk reduced by each rank
 
   bf16x8* my_stage = reinterpret_cast<bf16x8*>(mine + in_off);
@@ -97,7 +104,7 @@ __global__ __launch_bounds__(512) void custom_allreduce_2shot_kernel(
   for (int64_t i = c0 + tid; i < c1; i += blockDim.x) my_stage[i] = src[i];
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  ar_exchange(P, 0, reinterpret_cast<int*>(mine), err, b, rank, world, epoch);
+  ar_exchange(P, 0, reinterpret_cast<uint64_t*>(mine), err, b, rank, world, epoch);
   // reduce-scatter: my sub-chunk of this block, summed over ranks in order
   const int64_t r0 = c0 + rank * sub;
   const int64_t r1 = r0 + sub < c1 ? r0 + sub : c1;
@@ -116,7 +123,8 @@ __global__ __launch_bounds__(512) void custom_allreduce_2shot_kernel(
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  ar_exchange(P, kArFlags2, reinterpret_cast<int*>(mine + kArFlags2), err, b, rank, world, epoch);
+  ar_exchange(P, kArFlags2, reinterpret_cast<uint64_t*>(mine + kArFlags2), err, b, rank, world,
+              epoch);
   // all-gather: sub-chunk q of this block from rank q's result area
   bf16x8* dst = reinterpret_cast<bf16x8*>(out);
   for (int64_t i = c0 + tid; i < c1; i += blockDim.x) {
@@ -127,24 +135,23 @@ __global__ __launch_bounds__(512) void custom_allreduce_2shot_kernel(
 
 __global__ __launch_bounds__(512) void custom_allreduce_kernel(
     bf16_t* __restrict__ out, const bf16_t* __restrict__ in, ArPeers P, int rank, int world,
-    int64_t n8, int64_t stage_elems) {
-  __shared__ int s_epoch;
-  const int b = blockIdx.x, nb = gridDim.x, tid = threadIdx.x;
+    int64_t n8, int64_t stage_elems, int64_t chunk) {
+  __shared__ uint64_t s_epoch;
+  const int b = blockIdx.x, tid = threadIdx.x;
   char* mine = P.base[rank];
-  int* flags = reinterpret_cast<int*>(mine);
-  int* ctr = reinterpret_cast<int*>(mine + 2048);
-  int* err = reinterpret_cast<int*>(mine + 2048 + 256);
+  uint64_t* flags = reinterpret_cast<uint64_t*>(mine);
+  uint64_t* ctr = reinterpret_cast<uint64_t*>(mine + kArCounters);
+  int* err = reinterpret_cast<int*>(mine + kArError);
   if (tid == 0) {
-    const int e = ctr[b] + 1;
+    const uint64_t e = ctr[b] + 1;
     ctr[b] = e;
     s_epoch = e;
   }
   __syncthreads();
-  const int epoch = s_epoch;
+  const uint64_t epoch = s_epoch;
   const int64_t buf_off = kArHeader + (int64_t)(epoch & 1) * stage_elems * 2;
-  const int64_t per = (n8 + nb - 1) / nb;
-  const int64_t c0 = (int64_t)b * per;
-  const int64_t c1 = c0 + per < n8 ? c0 + per : n8;
+  const int64_t c0 = (int64_t)b * chunk;  // fixed per block, whatever the message size
+  const int64_t c1 = c0 + chunk < n8 ? c0 + chunk : n8;
 
   bf16x8* my_stage = reinterpret_cast<bf16x8*>(mine + buf_off);
   const bf16x8* src = reinterpret_cast<const bf16x8*>(in);
@@ -155,7 +162,7 @@ __global__ __launch_bounds__(512) void custom_allreduce_kernel(
     // publish my chunk to peer `tid`, then wait for peer `tid`'s chunk
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    int* peer_flags = reinterpret_cast<int*>(P.base[tid]);
+    uint64_t* peer_flags = reinterpret_cast<uint64_t*>(P.base[tid]);
     __hip_atomic_store(peer_flags + b * kArMaxRanks + rank, epoch, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_SYSTEM);
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
@@ -195,14 +202,15 @@ int launch_custom_allreduce(void* out, const void* in, int64_t n, const ArPeers&
       n > stage_elems)
     return -1;
   const int64_t n8 = n / 8;
-  int64_t nb = (n8 + 1023) / 1024;  // >= 2 vectors per thread
-  nb = nb < 1 ? 1 : (nb > kArMaxBlocks ? kArMaxBlocks : nb);
+  // fixed partition of the staging area: chunk b always belongs to block b
+  const int64_t chunk = (stage_elems / 8 + kArMaxBlocks - 1) / kArMaxBlocks;
+  const int64_t nb = (n8 + chunk - 1) / chunk;
   if (two_shot)
     hipLaunchKernelGGL(custom_allreduce_2shot_kernel, dim3((int)nb), dim3(512), 0, st,
-                       (bf16_t*)out, (const bf16_t*)in, peers, rank, world, n8, stage_elems);
+                       (bf16_t*)out, (const bf16_t*)in, peers, rank, world, n8, stage_elems, chunk);
   else
     hipLaunchKernelGGL(custom_allreduce_kernel, dim3((int)nb), dim3(512), 0, st, (bf16_t*)out,
-                       (const bf16_t*)in, peers, rank, world, n8, stage_elems);
+                       (const bf16_t*)in, peers, rank, world, n8, stage_elems, chunk);
   return (int)hipGetLastError();
 }
 
@@ -232,8 +240,19 @@ int ar_ipc_close(void* p) { return (int)hipIpcCloseMemHandle(p); }
 
 int ar_error(void* base) {
   int v = 0;
-  hipError_t e = hipMemcpy(&v, (char*)base + 2048 + 256, 4, hipMemcpyDeviceToHost);
+  hipError_t e = hipMemcpy(&v, (char*)base + kArError, 4, hipMemcpyDeviceToHost);
   return e != hipSuccess ? -(int)e : v;
+}
+
+// Test hook: start every local epoch counter and flag at `epoch` (all ranks
+// must call it with the same value, with no all-reduce in flight).
+int ar_set_epoch(void* base, uint64_t epoch) {
+  uint64_t h[kArMaxBlocks * kArMaxRanks];
+  for (auto& v : h) v = epoch;
+  hipError_t e = hipMemcpy(base, h, sizeof(h), hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy((char*)base + kArFlags2, h, sizeof(h), hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy((char*)base + kArCounters, h, 8 * kArMaxBlocks, hipMemcpyHostToDevice);
+  return (int)e;
 }
 
 }  // namespace drtc

@@ -76,6 +76,14 @@ PYBIND11_MODULE(_hipk, m) {
                             P<const void>(w_gu), P<const void>(w_dn), T, H, I, E, k, e_off,
                             e_local, act, P<void>(ws), ws_bytes, variant, S(st));
   });
+  m.def("gemm", [](u64 c, u64 a, u64 b, u64 r, int M, int N, int K, int lda, int ldb, int ldc,
+                   int ldr, int epi, int up_off, int variant, int splitk, int group_m, u64 slab,
+                   int64_t slab_bytes, u64 counters, int n_counters, u64 st) {
+    return drtc::launch_gemm(P<void>(c), P<const void>(a), P<const void>(b), P<const void>(r), M,
+                             N, K, lda, ldb, ldc, ldr, epi, up_off, variant, splitk, group_m,
+                             P<void>(slab), slab_bytes, P<int>(counters), n_counters, S(st));
+  });
+  m.def("gemm_workspace_bytes", &drtc::gemm_workspace_bytes);
   m.def("moe_workspace_bytes", &drtc::moe_workspace_bytes);
   m.def("custom_ar_buffer_bytes", &drtc::custom_ar_buffer_bytes);
   m.def("custom_allreduce", [](u64 out, u64 in, int64_t n, const std::vector<u64>& bases, int rank,
@@ -109,6 +117,7 @@ PYBIND11_MODULE(_hipk, m) {
   });
   m.def("ar_ipc_close", [](u64 p) { return drtc::ar_ipc_close(P<void>(p)); });
   m.def("ar_error", [](u64 base) { return drtc::ar_error(P<void>(base)); });
+  m.def("ar_set_epoch", [](u64 base, uint64_t e) { return drtc::ar_set_epoch(P<void>(base), e); });
   m.def("lt_version", &drtc::lt_version);
   m.def("lt_gemm", [](u64 y, u64 x, u64 w, int64_t M, int64_t N, int64_t K, int64_t ldx,
                       int64_t ldy, u64 st) {

@@ -7,6 +7,8 @@ int configure_kernels() {
   if (e) return e;
   e = configure_prefill();
   if (e) return e;
-  return configure_moe();
+  e = configure_moe();
+  if (e) return e;
+  return configure_gemm();
 }
 }  // namespace drtc

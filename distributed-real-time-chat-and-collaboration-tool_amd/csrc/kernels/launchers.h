@@ -63,6 +63,7 @@ int ar_ipc_get(void* p, char* handle);  // 64-byte handle
 int ar_ipc_open(const char* handle, void** p);
 int ar_ipc_close(void* p);
 int ar_error(void* base);
+int ar_set_epoch(void* base, uint64_t epoch);
 
 // Tuned hipBLASLt projection GEMM y[M,N] = x[M,K] @ W[N,K]^T, bf16 (gemm_lt.cpp).
 int lt_version();
@@ -89,11 +90,21 @@ int launch_skinny_norm_gemm(void* y, void* h_out, const void* x, const void* res
                             const void* w, int M, int N, int K, int ldx, int ldr, int ldh,
                             int ldy, float eps, bool gemma, hipStream_t st);
 
+// Hand-written MFMA GEMM (gemm.hip): c[M,N] = epi(a[M,K] . b[N,K]^T); epi 0 store, 1 + r
+// (residual, may alias c), 2/3 SiLU/GELU gated (b rows [0,up_off) gate, [up_off,2 up_off) up,
+// N = up_off).  variant = pipeline (1..3); splitk > 1 needs slab + counters (zeroed once).
+int launch_gemm(void* c, const void* a, const void* b, const void* r, int M, int N, int K,
+                int lda, int ldb, int ldc, int ldr, int epi, int up_off, int variant, int splitk,
+                int group_m, void* slab, int64_t slab_bytes, int* counters, int n_counters,
+                hipStream_t st);
+int64_t gemm_workspace_bytes(int64_t M, int64_t N, int splitk);
+
 // Raise the dynamic-LDS ceiling of the kernels that need > 64 KiB (head_dim
 // 256).  Called once at import, before any graph capture.
 int configure_kernels();
 int configure_decode();
 int configure_prefill();
 int configure_moe();
+int configure_gemm();
 
 }  // namespace drtc

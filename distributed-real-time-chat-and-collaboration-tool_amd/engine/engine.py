@@ -69,6 +69,9 @@ class LLMEngine:
         self.max_blocks = math.ceil(self.max_model_len / BS)
         if num_blocks is None:
             num_blocks = PagedKVCache.auto_num_blocks(cfg, model.sh.hkv, self.device, kv_fraction)
+        # lockstep (SPMD) TP/EP ranks must schedule identically: every rank
+        # sizes its cache from the same (smallest) block count
+        num_blocks = model.pc.agree_min(num_blocks)
         self.kv = PagedKVCache(cfg, model.sh.hkv, num_blocks, self.device, model.dtype)
         self.alloc = self.kv.allocator
         self.runner = DecodeRunner(model, self.kv, max_batch, self.max_blocks,

@@ -264,6 +264,66 @@ def glu_linear(gu: torch.Tensor, w: torch.Tensor, act: str = "silu") -> torch.Te
     return linear(act_glu(gu, act), w)
 
 
+# ------------------------------------------------------------ hand-written MFMA GEMM
+EPI = {"store": 0, "residual": 1, "silu": 2, "gelu_tanh": 3}
+_ws_lock = threading.Lock()
+_ws: dict[int, tuple[torch.Tensor, torch.Tensor]] = {}
+WS_SLAB_BYTES = 128 << 20   # fp32 split-K slabs (per device)
+WS_COUNTERS = 1 << 16
+
+
+def gemm_workspace(dev: torch.device) -> tuple[torch.Tensor, torch.Tensor]:
+    """Split-K workspace of a device: fp32 slabs + per-tile arrival counters
+    (zeroed once; the last arriver of each tile re-arms its counter).  One
+    per device, shared by every GEMM that runs on the engine's stream; a GEMM
+    issued concurrently on another stream must pass its own (``ws=``).
+    Create it before any graph capture (the engine's eager warm-up does)."""
+    key = dev.index if dev.index is not None else torch.cuda.current_device()
+    ws = _ws.get(key)
+    if ws is None:
+        with _ws_lock:
+            ws = _ws.get(key)
+            if ws is None:
+                ws = (torch.empty(WS_SLAB_BYTES // 4, dtype=torch.float32, device=dev),
+                      torch.zeros(WS_COUNTERS, dtype=torch.int32, device=dev))
+                _ws[key] = ws
+    return ws
+
+
+def new_gemm_workspace(dev: torch.device) -> tuple[torch.Tensor, torch.Tensor]:
+    """A private split-K workspace (for GEMMs on a second stream)."""
+    return (torch.empty(WS_SLAB_BYTES // 4, dtype=torch.float32, device=dev),
+            torch.zeros(WS_COUNTERS, dtype=torch.int32, device=dev))
+
+
+def mfma_gemm(x: torch.Tensor, w: torch.Tensor, epi: str = "store",
+              residual: torch.Tensor | None = None, out: torch.Tensor | None = None,
+              variant: int = 2, splitk: int = 1, group_m: int = 8,
+              ws: tuple[torch.Tensor, torch.Tensor] | None = None) -> torch.Tensor:
+    """Hand-written CDNA4 GEMM (csrc/kernels/gemm.hip): y = epi(x @ w.T).
+
+    epi "store": y = x @ w.T; "residual": y = x @ w.T + residual (``out`` may
+    be ``residual`` itself: in-place add into the residual stream);
+    "silu" / "gelu_tanh": w is the fused [gate; up] weight [2I, K] and
+    y[:, n] = act(x . gate_n) * (x . up_n) has I columns (no act_glu pass).
+    Shapes: K % 64 == 0, N % 256 == 0 (I % 128 == 0 for the gated forms),
+    (K / 64) % splitk == 0; rows of x are unrestricted."""
+    M, K = x.shape
+    glu = epi in ("silu", "gelu_tanh")
+    N = w.shape[0] // 2 if glu else w.shape[0]
+    if out is None:
+        out = torch.empty((M, N), dtype=x.dtype, device=x.device)
+    st = stream_ptr(x)
+    slab, cnt = ((ws or gemm_workspace(x.device)) if splitk > 1 else (None, None))
+    check(hipk().gemm(out.data_ptr(), x.data_ptr(), w.data_ptr(), ptr(residual), M, N, K,
+                      x.stride(0), w.stride(0), out.stride(0),
+                      residual.stride(0) if residual is not None else 0, EPI[epi],
+                      N if glu else 0, variant, splitk, group_m, ptr(slab),
+                      slab.numel() * 4 if slab is not None else 0, ptr(cnt),
+                      cnt.numel() if cnt is not None else 0, st), "gemm")
+    return out
+
+
 def tune(M: int, N: int, K: int, device, iters: int = 20, max_candidates: int = 12) -> dict:
     """Measure every hipBLASLt solution for y[M,N] = x[M,K] @ W[N,K]^T on
     random operands; returns {"algo", "us", "heuristic_us", "candidates"}."""

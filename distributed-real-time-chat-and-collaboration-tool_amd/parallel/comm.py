@@ -84,6 +84,24 @@ class ParallelContext:
         cpu_group = dist.new_group(ranks=ranks, backend="gloo")
         self.custom_ar = CustomAllReduce(cpu_group, max_bytes=max_bytes)
 
+    def agree_min(self, v: int) -> int:
+        """MIN of an integer over every rank that runs this model in lockstep
+        (TP and EP groups).  Used for host-side sizing decisions that must be
+        identical on all ranks - e.g. the KV-cache block count, which each
+        rank derives from its own free HBM: differing counts would make the
+        SPMD schedulers admit / preempt differently and issue collectives of
+        different sizes (a hang, or silent corruption with the custom
+        all-reduce)."""
+        groups = [g for size, g in ((self.tp_size, self.tp_group), (self.ep_size, self.ep_group))
+                  if size > 1]
+        for g in groups:
+            dev = (torch.device("cuda", torch.cuda.current_device())
+                   if dist.get_backend(g) == "nccl" else torch.device("cpu"))
+            t = torch.tensor([int(v)], dtype=torch.int64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MIN, group=g)
+            v = int(t.item())
+        return int(v)
+
     def all_reduce_tp(self, x: torch.Tensor) -> torch.Tensor:
         if self.tp_size > 1:
             if self.custom_ar is not None and self.custom_ar.can(x):

@@ -62,6 +62,19 @@ def tp_worker(rank: int, world: int, port: int, model_name: str, engine_kw: dict
         if rank == 0:
             outq.put(("fatal", 0, repr(e)))
         raise
+    try:
+        _serve_loop(rank, eng, pc, cpu, inq, outq)
+    except BaseException as e:
+        if rank == 0:
+            outq.put(("fatal", 0, repr(e)))
+        raise
+    dist.barrier(group=cpu)
+    dist.destroy_process_group()
+
+
+def _serve_loop(rank, eng, pc, cpu, inq, outq):
+    import torch.distributed as dist
+
     while True:
         new = []
         if rank == 0:
@@ -84,11 +97,15 @@ def tp_worker(rank: int, world: int, port: int, model_name: str, engine_kw: dict
             break
         if eng.has_work():
             done = eng.step()
+            # a flag wait of the custom all-reduce that timed out means a peer
+            # missed a call and this step summed stale staging: fail the whole
+            # group (the supervisor starts fresh processes) instead of
+            # returning tokens computed from wrong hidden states
+            if pc.custom_ar is not None and pc.custom_ar.error():
+                raise RuntimeError("custom all-reduce flag wait timed out (peer missed a call)")
             if rank == 0:
                 for r in done:
                     outq.put(("done", r.request_id, (r.output_ids, r.finish_reason)))
-    dist.barrier(group=cpu)
-    dist.destroy_process_group()
 
 
 class TPEngineGroup:
@@ -112,6 +129,7 @@ class TPEngineGroup:
         self.tok = tokenizer
         self.max_model_len = engine_kw.get("max_model_len", 4096)
         self._futs: dict[str, tuple] = {}
+        self.error = None
         self._lock = threading.Lock()
         self._ids = itertools.count()
         threading.Thread(target=self._collect, daemon=True).start()
@@ -119,6 +137,14 @@ class TPEngineGroup:
     def _collect(self):
         while True:
             kind, rid, payload = self.outq.get()
+            if kind == "fatal":  # the group died: fail every outstanding request
+                with self._lock:
+                    futs, self._futs = list(self._futs.values()), {}
+                    self.error = payload
+                for ev, slot in futs:
+                    slot.append(([], f"error: TP group failed: {payload}"))
+                    ev.set()
+                continue
             with self._lock:
                 f = self._futs.pop(rid, None)
             if f is not None:
@@ -137,6 +163,8 @@ class TPEngineGroup:
             rid = f"tp-{next(self._ids)}"
             ev, slot = threading.Event(), []
             with self._lock:
+                if self.error is not None:
+                    raise RuntimeError(f"TP group failed: {self.error}")
                 self._futs[rid] = (ev, slot)
             self.inq.put((rid, ids, prm))
             hs.append((ev, slot))

@@ -110,6 +110,11 @@ class RaftConfig:
 
 
 NOOP = "NOOP"
+# The leader's no-op carries "{}": a reference node replaying this log
+# (ref server/raft_node.py:1196-1241) json-decodes it and logs "Unknown
+# command" instead of failing on an empty payload (its except handler would
+# then hit an unbound ``command`` at log index 0 and crash).
+NOOP_DATA = b"{}"
 
 
 @dataclass
@@ -298,7 +303,7 @@ class RaftCore:
             self.backoff[p] = 1
             self.last_sent[p] = -1e9
         if self.cfg.leader_noop:
-            self._append_local([Entry(self.term, NOOP, b"")])
+            self._append_local([Entry(self.term, NOOP, NOOP_DATA)])
         for p in self.peers:
             self._send_append(p)
         self._advance_commit()

@@ -61,7 +61,7 @@ class RaftRuntime:
                  storage: str = "native", config: RaftConfig | None = None,
                  state: ChatState | None = None, fsync: bool = False, tick: float = 0.01,
                  persist_interval: float = 0.2, seed_defaults=None, snapshot_every: int = 0,
-                 snapshot_chunk: int = 4 << 20):
+                 snapshot_chunk: int = 4 << 20, export_interval: float = 5.0):
         self.id = node_id
         self.port = port
         self.peers = {int(k): v for k, v in peers.items() if int(k) != node_id}
@@ -73,6 +73,7 @@ class RaftRuntime:
         self.core_lock = threading.RLock()
         self.tick_interval = tick
         self.persist_interval = persist_interval
+        self.export_interval = export_interval  # reference-format log pickle refresh (s)
         self.waiters: dict[int, _Waiter] = {}
         self.apply_listeners = []
         if snapshot_every and storage != "native":
@@ -215,12 +216,27 @@ class RaftRuntime:
         return raft_snap_pb.InstallSnapshotResponse(term=r.term, success=r.success)
 
     def _persist_loop(self) -> None:
+        last_export = time.monotonic()
         while self.running:
             time.sleep(self.persist_interval)
             try:
                 self.persist()
+                if self.export_interval and time.monotonic() - last_export >= self.export_interval:
+                    self.export_reference_log()
+                    last_export = time.monotonic()
             except Exception:  # pragma: no cover - disk errors are logged, not fatal
                 log.exception("persist failed")
+
+    def export_reference_log(self) -> None:
+        """Refresh the reference-format log pickle (raft_log_port_*.pkl) and the
+        clamped state pickle; the O(log) pickling runs outside core_lock."""
+        with self.core_lock:
+            snap = self.storage.export_begin()
+        if snap is None:
+            return
+        last = self.storage.export_write(snap)
+        with self.core_lock:
+            self.storage.export_end(last)
 
     def persist(self, all_files: bool = False) -> None:
         with self.state_lock:

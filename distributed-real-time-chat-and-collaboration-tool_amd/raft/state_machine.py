@@ -10,7 +10,14 @@ stay byte-compatible.  Differences, all deliberate:
 * JOIN_CHANNEL for an unknown channel is dropped instead of silently joining
   the first default channel found (survey quirk Q13);
 * ``apply`` is deterministic given the entry - nothing node-local (sessions,
-  presence) is touched, so every replica converges to the same state.
+  presence) is touched, so every replica converges to the same state;
+* CREATE_CHANNEL may carry ``created_at`` (ISO string, the proposing leader's
+  clock; an additive key the reference's apply ignores) so the timestamp -
+  and therefore channels.pkl - is identical on every replica;
+* REVOKE_TOKEN (an additive command; a reference node logs "Unknown command"
+  and skips it) replicates logout: {username, token_hash, exp, ts}; revoked
+  hashes are dropped deterministically once the entry clock ``ts`` passes
+  their ``exp``.
 """
 from __future__ import annotations
 
@@ -28,7 +35,8 @@ DEFAULT_USERS = (("alice", "alice123"), ("bob", "bob123"), ("charlie", "charlie1
 DEFAULT_CHANNELS = ("general", "random", "tech")
 
 COMMANDS = ("CREATE_USER", "LOGIN_USER", "CREATE_CHANNEL", "JOIN_CHANNEL", "LEAVE_CHANNEL",
-            "SEND_MESSAGE", "SEND_DM", "UPLOAD_FILE")
+            "SEND_MESSAGE", "SEND_DM", "UPLOAD_FILE", "REVOKE_TOKEN")
+GENESIS_CREATED_AT = "2025-01-01T00:00:00+00:00"
 
 
 def _utcnow() -> _dt.datetime:
@@ -44,6 +52,7 @@ class ChatState:
         self.direct_messages: list[dict] = []
         self.files: dict[str, dict] = {}
         self.online_users: set[str] = set()
+        self.revoked_tokens: dict[str, int] = {}   # sha256(token) hex -> exp (epoch s)
         self._msg_ids: set[str] = set()
         self._dm_ids: set[str] = set()
         self._dm_pair: dict[tuple, list] = defaultdict(list)
@@ -84,10 +93,16 @@ class ChatState:
         cid = d["channel_id"]
         if cid in self.channels:
             return
+        created = _utcnow()
+        if isinstance(d.get("created_at"), str):
+            try:
+                created = _dt.datetime.fromisoformat(d["created_at"])
+            except ValueError:
+                pass
         self.channels[cid] = {
             "id": cid, "name": d["name"], "description": d["description"],
             "is_private": d["is_private"], "members": set(d["members"]),
-            "admins": set(d["admins"]), "created_at": _utcnow(),
+            "admins": set(d["admins"]), "created_at": created,
         }
         self.channel_messages.setdefault(cid, [])
         self.dirty.add("channels")
@@ -130,6 +145,14 @@ class ChatState:
         if d["recipient_id"] != d["sender_id"]:
             self._dm_user[d["recipient_id"]].append(d)
 
+    def _apply_revoke_token(self, d: dict) -> None:
+        ts = int(d.get("ts", 0))
+        for h in [h for h, exp in self.revoked_tokens.items() if exp < ts]:
+            del self.revoked_tokens[h]
+        if int(d.get("exp", 0)) >= ts:
+            self.revoked_tokens[d["token_hash"]] = int(d["exp"])
+        self.dirty.add("revoked_tokens")
+
     def _apply_upload_file(self, d: dict) -> None:
         fid = d["file_id"]
         if fid in self.files:
@@ -155,6 +178,29 @@ class ChatState:
         return self._dm_user.get(user_id, [])
 
     # ------------------------------------------------------------- seeding
+    def genesis_entries(self, hash_password) -> list[tuple[str, dict]]:
+        """The default users/channels as log entries (CREATE_USER /
+        CREATE_CHANNEL) for whatever is still missing: proposed once by the
+        first leader of a fresh cluster, so every replica applies the same
+        bcrypt hashes and timestamps (byte-identical pickles).
+        Ids are the names, as in the reference (server/raft_node.py:426-467)."""
+        out = []
+        ids = [name for name, _ in DEFAULT_USERS]
+        for name, pw in DEFAULT_USERS:
+            if name not in self.users:
+                out.append(("CREATE_USER", {
+                    "user_id": name, "username": name,
+                    "password": hash_password(pw.encode()).decode("latin1"),
+                    "email": f"{name}@chat.com", "display_name": name.title(), "is_admin": False}))
+        for cname in DEFAULT_CHANNELS:
+            if cname not in self.channels:
+                out.append(("CREATE_CHANNEL", {
+                    "channel_id": cname, "name": cname,
+                    "description": f"Default {cname} channel (public)", "is_private": False,
+                    "members": list(ids), "admins": list(ids),
+                    "created_at": GENESIS_CREATED_AT}))
+        return out
+
     def seed_defaults(self, hash_password) -> None:
         """Default users/channels with deterministic ids (username / channel
         name), identical on every node (server/raft_node.py:426-467)."""
@@ -178,7 +224,9 @@ class ChatState:
 
     # --------------------------------------------------------- persistence
     FILES = {"users": "users.pkl", "channels": "channels.pkl", "messages": "messages.pkl",
-             "direct_messages": "direct_messages.pkl"}
+             "direct_messages": "direct_messages.pkl",
+             # not part of the reference layout: replicated logout revocations
+             "revoked_tokens": "revoked_tokens.pkl"}
 
     def snapshot_obj(self, which: str):
         if which == "users":
@@ -197,6 +245,8 @@ class ChatState:
             return self.channel_messages
         if which == "direct_messages":
             return self.direct_messages
+        if which == "revoked_tokens":
+            return self.revoked_tokens
         raise KeyError(which)
 
     def save(self, data_dir: str, which=None, fsync: bool = False) -> None:
@@ -234,6 +284,9 @@ class ChatState:
         p = os.path.join(data_dir, "direct_messages.pkl")
         if os.path.exists(p):
             self.direct_messages = pickle_compat.safe_load(p)
+        p = os.path.join(data_dir, "revoked_tokens.pkl")
+        if os.path.exists(p):
+            self.revoked_tokens = dict(pickle_compat.safe_load(p))
         self.reindex()
 
     # ------------------------------------------------- Raft snapshot image
@@ -244,7 +297,8 @@ class ChatState:
         compacted log would otherwise lose them."""
         return pickle.dumps({"users": self.users, "users_by_id": self.users_by_id,
                              "channels": self.channels, "messages": self.channel_messages,
-                             "direct_messages": self.direct_messages, "files": self.files},
+                             "direct_messages": self.direct_messages, "files": self.files,
+                             "revoked_tokens": self.revoked_tokens},
                             protocol=pickle_compat.PROTOCOL)
 
     def restore_image(self, data: bytes) -> None:
@@ -252,6 +306,7 @@ class ChatState:
         self.users, self.users_by_id = d["users"], d["users_by_id"]
         self.channels, self.channel_messages = d["channels"], d["messages"]
         self.direct_messages, self.files = d["direct_messages"], d["files"]
+        self.revoked_tokens = dict(d.get("revoked_tokens", {}))
         self.reindex()
         self.dirty.update(self.FILES)
 

@@ -8,9 +8,25 @@ Layout: ``<base>/raft_node_{id}_data/`` (server/raft_node.py:100-105)
 
 ``NativeStorage`` (default) appends each entry to the C++ LogStore
 (csrc/runtime/log_store.cpp) and rewrites the reference-format log pickle
-only on ``export()`` (snapshots, clean shutdown), instead of on every write
-(survey quirk Q5).  ``PickleStorage`` reproduces the reference exactly
-(whole-log pickle per append).  Either imports a reference data dir.
+only on ``export()`` (periodically from the runtime's persister, on
+snapshots and at clean shutdown), instead of on every write (survey quirk
+Q5).  ``PickleStorage`` reproduces the reference exactly (whole-log pickle
+per append).  Either imports a reference data dir.
+
+Durability (``fsync=True``, the server default): a batch of appended entries
+is made durable with ONE fdatasync before the append returns (group commit:
+an AppendEntries batch or a leader proposal is acknowledged only after it),
+and a change of ``current_term`` / ``voted_for`` is fsynced (file + directory)
+before a vote is answered.  ``commit_index`` / ``last_applied`` are
+recomputable and written without a sync.
+
+Crash consistency of the reference-format PAIR: the state pickle is written
+on every state change but its ``commit_index`` / ``last_applied`` are
+clamped to the last index present in the exported log pickle (recorded in
+``raft_log_port_{port}.exported``), so after a crash at any point the pair
+on disk never claims a commit beyond the log it holds - a reference node
+booting from it replays a consistent committed prefix (the app-state
+pickles, which it loads afterwards, carry the rest).
 
 Log compaction (opt-in; the reference has none): ``raft_snapshot_port_{port}.pkl``
 holds ``{'index', 'term', 'data'}`` (the state-machine image at ``index``) and
@@ -118,6 +134,9 @@ class PickleStorage:
     def export(self) -> None:
         pass
 
+    def export_begin(self):
+        return None  # the log pickle is rewritten on every append already
+
     def flush(self) -> None:
         pass
 
@@ -132,6 +151,7 @@ class NativeStorage:
         self.port = port
         self.fsync = fsync
         self.log_path = os.path.join(directory, f"raft_log_port_{port}.pkl")
+        self.export_path = os.path.join(directory, f"raft_log_port_{port}.exported")
         self.state = _StateFile(os.path.join(directory, f"raft_state_port_{port}.pkl"), fsync)
         self.snap = _SnapshotFile(os.path.join(directory, f"raft_snapshot_port_{port}.pkl"), fsync)
         pkg = __name__.rsplit(".", 2)[0]
@@ -140,13 +160,39 @@ class NativeStorage:
         fresh = not segs
         self.base = segs[-1][0] if segs else 0
         self.seg_path = segs[-1][1] if segs else self._seg_name(0)
-        self.store = self._native.LogStore(self.seg_path, fsync)
+        # per-entry syncs off: append() syncs once per batch (group commit)
+        self.store = self._native.LogStore(self.seg_path, False)
         for _, old in segs[:-1]:  # leftovers of an interrupted compaction
             os.unlink(old)
         self.entries: list[Entry] = []
+        self._state: dict = {}
+        self._durable = (None, None)  # (term, voted_for) last fsynced
+        self._trunc_floor = 1 << 62
+        self.exported_last = self._read_exported()
         if fresh and os.path.exists(self.log_path):  # migrate a reference data dir
-            for e in _load_ref_log(self.log_path):
+            ref = _load_ref_log(self.log_path)
+            for e in ref:
                 self.store.append(e.term, e.command, e.data)
+            self.store.sync()
+            self.exported_last = len(ref) - 1
+            self._write_exported()
+
+    # -- the exported reference-format log: last absolute index it holds
+    def _read_exported(self) -> int:
+        try:
+            with open(self.export_path) as f:
+                return int(f.read().strip() or -1)
+        except (OSError, ValueError):
+            return -1
+
+    def _write_exported(self) -> None:
+        tmp = self.export_path + ".tmp"
+        with open(tmp, "w") as f:
+            f.write(str(self.exported_last))
+            if self.fsync:
+                f.flush()
+                os.fsync(f.fileno())
+        os.replace(tmp, self.export_path)
 
     def _seg_name(self, base: int) -> str:
         tail = ".seg" if base == 0 else f".b{base}.seg"
@@ -176,16 +222,28 @@ class NativeStorage:
             self.entries.append(Entry(int(t), c, bytes(d)))
         if skip > 0:  # finish an interrupted compaction
             self._rewrite(st["snap_index"] + 1, self.entries)
+        self._state = dict(st)
+        self._durable = (st.get("current_term"), st.get("voted_for"))
         return st, list(self.entries)
 
     def append(self, entries) -> None:
         for e in entries:
             self.store.append(e.term, e.command, e.data)
+        if self.fsync:
+            self.store.sync()  # one fdatasync per batch, before the caller acknowledges
         self.entries.extend(entries)
 
     def truncate_from(self, index: int) -> None:
         self.store.truncate_from(index - self.base)
+        if self.fsync:
+            self.store.sync()
         del self.entries[index - self.base:]
+        self._trunc_floor = min(self._trunc_floor, index)
+        if self.exported_last >= index:
+            # the exported pickle now holds replaced (uncommitted) entries past
+            # index - 1: never let the reference state point into them
+            self.exported_last = index - 1
+            self._write_exported()
 
     def _rewrite(self, base: int, entries) -> None:
         """Move the log to a fresh segment starting at absolute index ``base``."""
@@ -193,7 +251,7 @@ class NativeStorage:
         tmp = path + ".tmp"
         if os.path.exists(tmp):
             os.unlink(tmp)
-        st = self._native.LogStore(tmp, self.fsync)
+        st = self._native.LogStore(tmp, False)
         for e in entries:
             st.append(e.term, e.command, e.data)
         st.sync()
@@ -201,7 +259,7 @@ class NativeStorage:
         os.replace(tmp, path)
         old = self.seg_path
         self.store.close()
-        self.store = self._native.LogStore(path, self.fsync)
+        self.store = self._native.LogStore(path, False)
         self.seg_path, self.base = path, base
         self.entries = list(entries)
         if old != path and os.path.exists(old):
@@ -219,11 +277,49 @@ class NativeStorage:
         self._rewrite(index + 1, list(keep))
 
     def save_state(self, state: dict) -> None:
-        self.state.save(state)
+        self._state.update(state)
+        st = self._state
+        clamp = self.exported_last
+        ref = {"current_term": st["current_term"], "voted_for": st["voted_for"],
+               "commit_index": min(int(st["commit_index"]), clamp),
+               "last_applied": min(int(st["last_applied"]), clamp)}
+        hard = (st["current_term"], st["voted_for"])
+        durable = self.fsync and hard != self._durable  # term / vote: sync before replying
+        pickle_compat.dump(ref, self.state.path, durable)
+        if durable:
+            self._durable = hard
+
+    # -- export of the reference-format log, in three steps so the runtime can
+    # pickle a large log outside its consensus lock
+    def export_begin(self):
+        """Under the consensus lock: (base, entries) to write, or None."""
+        last = self.base + len(self.entries) - 1
+        if last == self.exported_last and os.path.exists(self.log_path):
+            return None
+        self._trunc_floor = last + 1  # lowest index truncated while the export runs
+        return self.base, list(self.entries)
+
+    def export_write(self, snapshot) -> int:
+        """Any thread: write the log pickle; returns the last index written."""
+        base, entries = snapshot
+        _dump_ref_log(entries, self.log_path, self.fsync)
+        return base + len(entries) - 1
+
+    def export_end(self, last: int) -> None:
+        """Under the consensus lock: record the export, re-clamp the state."""
+        # a truncation while the pickle was being written invalidates it
+        # from the truncation point on (entries there may have been replaced)
+        last = min(last, self._trunc_floor - 1, self.base + len(self.entries) - 1)
+        self.exported_last = last
+        self._write_exported()
+        if self._state:
+            self.save_state({})
 
     def export(self) -> None:
-        """Write the reference-format log pickle (for tools / the reference)."""
-        _dump_ref_log(self.entries, self.log_path, False)
+        """Write the reference-format log pickle and the matching state."""
+        snap = self.export_begin()
+        if snap is not None:
+            self.export_end(self.export_write(snap))
 
     def flush(self) -> None:
         self.store.sync()

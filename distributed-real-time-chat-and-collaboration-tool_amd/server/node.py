@@ -86,7 +86,10 @@ def main(argv=None) -> None:
     ap.add_argument("--local-commit", action="store_true", help="reference quirk Q1 behaviour")
     ap.add_argument("--token-mode", choices=("replicated", "reference"), default="replicated")
     ap.add_argument("--bcrypt-rounds", type=int, default=12)
-    ap.add_argument("--fsync", action="store_true")
+    ap.add_argument("--fsync", dest="fsync", action="store_true", default=True,
+                    help="fsync log appends and votes before acknowledging (default)")
+    ap.add_argument("--no-fsync", dest="fsync", action="store_false",
+                    help="reference behaviour: no fsync (acknowledged writes can be lost)")
     ap.add_argument("--snapshot-every", type=int, default=0,
                     help="snapshot the state machine and compact the log every N entries "
                          "(native storage; 0 = keep the whole log like the reference)")

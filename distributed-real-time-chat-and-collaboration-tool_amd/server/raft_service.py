@@ -11,11 +11,22 @@ marked with the survey quirk they address:
   Q6  tokens verify by signature + replicated user (valid on every node,
       survive failover) unless ``token_mode="reference"``;
   Q8  an auto-join on SendMessage is replicated (JOIN_CHANNEL), not local;
-  Q9  GetMessages / GetDirectMessages honour ``offset``.
+  Q9  GetMessages / GetDirectMessages honour ``offset``;
+  Q11 the default users/channels are seeded through the log (genesis entries
+      proposed once by the first leader of a fresh cluster: identical bcrypt
+      hashes, ids and timestamps on every replica) unless ``seed_mode="local"``
+      restores the reference's per-node seeding;
+  --  logout is replicated (REVOKE_TOKEN), so a logged-out token stays invalid
+      on every node and across failover;
+  --  writes carrying the optional ``request_id`` (an additive proto field)
+      are idempotent: the id becomes the message / DM / file id, which the
+      state machine already de-duplicates, so a client retry after a
+      DEADLINE_EXCEEDED cannot duplicate the write.
 """
 from __future__ import annotations
 
 import datetime as _dt
+import hashlib
 import logging
 import mimetypes
 import threading
@@ -30,6 +41,7 @@ from ..raft.core import NotLeaderError, RaftConfig
 from ..raft.node import RaftRuntime
 from ..utils import auth
 from ..utils.metrics import METRICS
+from ..raft.state_machine import DEFAULT_USERS as DEFAULT_USERS_ALL
 
 log = logging.getLogger(__name__)
 
@@ -62,8 +74,9 @@ class NodeConfig:
     write_timeout: float = 5.0
     grpc_workers: int = 32
     advertise_host: str = "localhost"
-    fsync: bool = False
+    fsync: bool = True   # durable votes / log appends before acknowledging (Raft safety)
     seed_defaults: bool = True
+    seed_mode: str = "log"                          # log (replicated genesis) | local (reference)
     snapshot_every: int = 0                         # compact the log every N applied entries (0: never)
     llm_timeouts: dict = field(default_factory=lambda: {
         "smart": 20.0, "summary": 10.0, "answer": 10.0, "suggest": 20.0})
@@ -108,19 +121,62 @@ class ChatNode:
                 salt = lambda: auth.bcrypt_gensalt(cfg.bcrypt_rounds)  # noqa: E731
                 state.seed_defaults(lambda pw: auth.bcrypt_hashpw(pw, salt()))
 
+        local_seed = cfg.seed_defaults and cfg.seed_mode == "local"
         self.rt = RaftRuntime(cfg.node_id, cfg.port, cfg.peers, cfg.data_root, cfg.storage,
-                              cfg.raft, fsync=cfg.fsync, seed_defaults=seed,
+                              cfg.raft, fsync=cfg.fsync, seed_defaults=seed if local_seed else None,
                               snapshot_every=cfg.snapshot_every)
         self.state = self.rt.state
         self.llm = LLMClient(cfg.llm_address)
+        self.genesis_done = threading.Event()
+        if not (cfg.seed_defaults and cfg.seed_mode == "log"):
+            self.genesis_done.set()
+        self._running = False
 
     # ------------------------------------------------------------ helpers
     def start(self):
         self.rt.start()
+        self._running = True
+        if not self.genesis_done.is_set():
+            threading.Thread(target=self._genesis_loop, name=f"genesis-{self.cfg.node_id}",
+                             daemon=True).start()
         return self
 
     def stop(self):
+        self._running = False
         self.rt.stop()
+
+    def _genesis_loop(self) -> None:
+        """Seed the default users/channels through the log: once
+        this node leads and has applied its whole log (its NOOP committed, so
+        every earlier entry is in the state), propose whatever default record
+        is still missing.  Apply is idempotent by username / channel id, so a
+        leader change halfway through only completes the set."""
+        while self._running and not self.genesis_done.is_set():
+            time.sleep(0.02)
+            info = self.rt.leader_info()
+            with self.rt.state_lock:
+                have = all(n in self.st.users for n, _ in DEFAULT_USERS_ALL) and all(
+                    c in self.st.channels for c in DEFAULT_PUBLIC)
+            if have:
+                self.genesis_done.set()
+                return
+            if not info["is_leader"] or self.rt.core.last_applied < info["log"] - 1:
+                continue
+            salt = lambda: auth.bcrypt_gensalt(self.cfg.bcrypt_rounds)  # noqa: E731
+            with self.rt.state_lock:
+                entries = self.st.genesis_entries(lambda pw: auth.bcrypt_hashpw(pw, salt()))
+            for cmd, data in entries:
+                if self._propose(cmd, data) is not None:
+                    break  # lost leadership / timeout: re-evaluate
+
+    def _await_genesis(self, timeout: float = 5.0) -> None:
+        """Early requests on a fresh cluster wait briefly for the defaults."""
+        if not self.genesis_done.is_set():
+            self.genesis_done.wait(timeout)
+
+    @staticmethod
+    def _token_hash(token: str) -> str:
+        return hashlib.sha256(token.encode()).hexdigest()
 
     @property
     def st(self):
@@ -147,6 +203,9 @@ class ChatNode:
                 return None
         if token in self.revoked:
             return None
+        with self.rt.state_lock:
+            if self.st.revoked_tokens and self._token_hash(token) in self.st.revoked_tokens:
+                return None
         return payload
 
     def _propose(self, command: str, data: dict) -> str | None:
@@ -181,6 +240,7 @@ class ChatNode:
     # ------------------------------------------------------------ auth
     def Signup(self, request, context):
         username = request.username.strip()
+        self._await_genesis()
         with self.rt.state_lock:
             if username in self.st.users:
                 return raft_pb.SignupResponse(success=False, message="Username already exists")
@@ -200,6 +260,7 @@ class ChatNode:
 
     def Login(self, request, context):
         username = request.username.strip()
+        self._await_genesis()
         with self.rt.state_lock:
             user = self.st.users.get(username)
             stored = user["password"] if user else None
@@ -234,6 +295,11 @@ class ChatNode:
         if not p:
             return raft_pb.StatusResponse(success=False, message="Invalid token")
         name = p["username"]
+        if self.rt.is_leader():
+            # replicated: the token stays invalid on every node and after failover
+            self._propose("REVOKE_TOKEN", {"username": name,
+                                           "token_hash": self._token_hash(request.token),
+                                           "exp": int(p.get("exp", 0)), "ts": int(time.time())})
         with self.rt.state_lock:
             self.sessions.pop(request.token, None)
             self.revoked.add(request.token)
@@ -260,7 +326,8 @@ class ChatNode:
         cid = str(uuid.uuid4())
         data = {"channel_id": cid, "name": name,
                 "description": request.description or f"Channel {name}",
-                "is_private": request.is_private, "members": [p["user_id"]], "admins": [p["user_id"]]}
+                "is_private": request.is_private, "members": [p["user_id"]], "admins": [p["user_id"]],
+                "created_at": _dt.datetime.now(_dt.timezone.utc).isoformat()}
         err = self._propose("CREATE_CHANNEL", data)
         if err:
             return raft_pb.StatusResponse(success=False, message=err)
@@ -374,12 +441,23 @@ class ChatNode:
             err = self._propose("JOIN_CHANNEL", {"channel_id": cid, "user_id": p["user_id"]})
             if err:
                 return raft_pb.StatusResponse(success=False, message=err)
-        msg = {"id": str(uuid.uuid4()), "sender_id": p["user_id"], "sender_name": p["username"],
-               "channel_id": cid, "content": request.content, "timestamp": int(time.time() * 1000)}
+        msg = {"id": self._write_id(request), "sender_id": p["user_id"],
+               "sender_name": p["username"], "channel_id": cid, "content": request.content,
+               "timestamp": int(time.time() * 1000)}
         err = self._propose("SEND_MESSAGE", msg)
         if err:
             return raft_pb.StatusResponse(success=False, message=err)
         return raft_pb.StatusResponse(success=True, message="Message sent")
+
+    @staticmethod
+    def _write_id(request) -> str:
+        """Record id of a write: the client's request_id when it sent one (a
+        retry then maps onto the same record and the apply de-duplicates
+        it), else a fresh uuid4 as in the reference."""
+        rid = getattr(request, "request_id", "")
+        if rid and len(rid) <= 64:
+            return rid
+        return str(uuid.uuid4())
 
     @staticmethod
     def _window(items, limit: int, offset: int):
@@ -412,7 +490,7 @@ class ChatNode:
             if rec is None:
                 return raft_pb.StatusResponse(success=False, message="User not found")
             rid = rec["id"]
-        dm = {"id": str(uuid.uuid4()), "sender_id": p["user_id"], "sender_name": p["username"],
+        dm = {"id": self._write_id(request), "sender_id": p["user_id"], "sender_name": p["username"],
               "recipient_id": rid, "recipient_name": request.recipient_username,
               "content": request.content, "timestamp": int(time.time() * 1000), "is_read": False}
         err = self._propose("SEND_DM", dm)
@@ -474,7 +552,7 @@ class ChatNode:
             return raft_pb.FileUploadResponse(success=False, message="Invalid token")
         if not self.rt.is_leader():
             return raft_pb.FileUploadResponse(success=False, message="Not the leader")
-        fid = str(uuid.uuid4())
+        fid = self._write_id(request)
         mime = request.mime_type or mimetypes.guess_type(request.file_name)[0] or "application/octet-stream"
         data = {"file_id": fid, "name": request.file_name, "data": request.file_data.hex(),
                 "size": len(request.file_data), "mime_type": mime, "uploader_id": p["user_id"],

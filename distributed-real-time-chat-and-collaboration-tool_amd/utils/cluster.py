@@ -61,10 +61,12 @@ class LocalCluster:
             self.kill(i)
 
     def leader(self, timeout: float = 10.0) -> int:
+        """Id of the current leader, once it has the default users/channels
+        (a fresh cluster seeds them through the log right after election)."""
         t_end = time.time() + timeout
         while time.time() < t_end:
             ls = [i for i, n in self.nodes.items() if n.rt.is_leader()]
-            if ls:
+            if ls and self.nodes[ls[0]].genesis_done.is_set():
                 return ls[0]
             time.sleep(0.01)
         raise TimeoutError("no leader")

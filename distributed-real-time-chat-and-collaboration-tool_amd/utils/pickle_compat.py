@@ -40,6 +40,14 @@ def safe_load(path: str):
         return SafeUnpickler(f).load()
 
 
+def _fsync_dir(d: str) -> None:
+    fd = os.open(d, os.O_RDONLY)
+    try:
+        os.fsync(fd)
+    finally:
+        os.close(fd)
+
+
 def dump(obj, path: str, fsync: bool = False) -> None:
     """Atomic write (temp file + rename) of ``pickle.dumps(obj, protocol=4)``."""
     d = os.path.dirname(os.path.abspath(path))
@@ -53,6 +61,8 @@ def dump(obj, path: str, fsync: bool = False) -> None:
                 f.flush()
                 os.fsync(f.fileno())
         os.replace(tmp, path)
+        if fsync:
+            _fsync_dir(d)
     except BaseException:
         try:
             os.unlink(tmp)

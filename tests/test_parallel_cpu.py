@@ -57,6 +57,30 @@ def _tp_worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
+def _tp_engine_worker(rank, world, port, q):
+    """TP=2 engines whose ranks see different free memory: the block count is
+    agreed (MIN over the group), so the lockstep schedulers admit and preempt
+    identically and produce the same tokens (engine.py:71)."""
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from drtc_amd.engine import LLMEngine, SamplingParams
+    from drtc_amd.engine.kv_cache import PagedKVCache
+    from drtc_amd.models import TINY_LLAMA, TransformerLM
+    from drtc_amd.parallel.comm import ParallelContext
+
+    # rank-dependent "free HBM": 12 blocks on rank 0, 40 on rank 1
+    PagedKVCache.auto_num_blocks = staticmethod(lambda *a, **k: 12 + 28 * rank)
+    pc = ParallelContext.from_world(tp=True)
+    m = TransformerLM(TINY_LLAMA, "cpu", pc=pc, seed=5)
+    eng = LLMEngine(m, max_batch=8, max_model_len=256, use_graphs=False)
+    prompts = [list(range(1 + i, 40 + 3 * i)) for i in range(6)]
+    reqs = eng.generate(prompts, SamplingParams.greedy(48, ignore_eos=True))
+    q.put((rank, {"blocks": eng.kv.num_blocks, "preempt": eng.stats["preemptions"],
+                  "out": [r.output_ids for r in reqs]}))
+    dist.destroy_process_group()
+
+
 def _run(fn, world=2):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -80,3 +104,10 @@ def test_tp_and_ep_model_forward_matches_single_process():
     for rank, res in _run(_tp_worker):
         for name, rel in res.items():
             assert rel < 0.03, (rank, name, rel)
+
+
+def test_tp_engines_agree_on_kv_blocks_under_preemption():
+    res = dict(_run(_tp_engine_worker))
+    assert res[0]["blocks"] == res[1]["blocks"] == 12
+    assert res[0]["preempt"] == res[1]["preempt"] > 0
+    assert res[0]["out"] == res[1]["out"]

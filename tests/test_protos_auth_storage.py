@@ -41,8 +41,20 @@ def _norm(fd):
 @have_ref
 @pytest.mark.parametrize("name", ["raft_node", "llm_service", "chat_service", "chat_client"])
 def test_descriptors_match_reference(name):
+    """Every reference message/field/RPC is present unchanged; the only extra
+    fields are the documented additive ones (schema.ADDITIONS)."""
+    from drtc_amd.protos.schema import ADDITIONS
+
     mine = file_descriptor_protos()[name + ".proto"]
-    assert _norm(mine) == _norm(_ref_fdp(name))
+    pkg, msgs, svc = _norm(mine)
+    rpkg, rmsgs, rsvc = _norm(_ref_fdp(name))
+    assert (pkg, svc) == (rpkg, rsvc)
+    assert msgs.keys() == rmsgs.keys()
+    extra = ADDITIONS.get(name + ".proto", {})
+    for m, fields in rmsgs.items():
+        added = [f for f in msgs[m] if f not in fields]
+        assert set(fields) <= set(msgs[m]), m
+        assert sorted(f[0] for f in added) == sorted(extra.get(m, [])), m
 
 
 def test_wire_roundtrip():
