@@ -20,6 +20,7 @@ import mimetypes
 import os
 import shlex
 import sys
+import uuid
 from datetime import datetime
 
 import grpc
@@ -63,6 +64,52 @@ class ChatShell(cmd.Cmd):
         self.password_fn = password_fn or getpass.getpass
         self.input_fn = input_fn or input
         self.download_dir = download_dir
+        conn.on_leader_change = self._after_failover
+
+    # ----------------------------------------------------------- failover
+    def _after_failover(self, addr: str) -> None:
+        """Session recovery on a new leader (ref client/chat_client.py:147-228):
+        probe the token with GetOnlineUsers; auto-logout if the new leader
+        rejects it; otherwise restore the current channel by name."""
+        self.say(f" Reconnected to new leader at {addr}")
+        if not self.token:
+            return
+        stub = self.conn.stub
+        try:
+            valid = stub.GetOnlineUsers(raft_pb.GetOnlineUsersRequest(token=self.token),
+                                        timeout=2.0).success
+        except grpc.RpcError:
+            return  # leave the session as is; the next call retries discovery
+        if not valid:
+            who = self.username
+            self.say("   Session expired on new leader")
+            self.say("    Auto-logging out...")
+            self.token = self.username = self.channel_id = self.dm_partner = None
+            self.say(f"\n Please re-login: login {who}")
+            return
+        if self.channel_name and not self.dm_partner:
+            try:
+                r = stub.GetChannels(raft_pb.GetChannelsRequest(token=self.token), timeout=3.0)
+            except grpc.RpcError:
+                return
+            for c in r.channels if r.success else []:
+                if c.name.lower() == self.channel_name.lower():
+                    if c.channel_id != self.channel_id:
+                        self.channel_id = c.channel_id
+                    self.say(f" Restored channel #{self.channel_name}")
+                    break
+
+    def _auto_logout(self, why: str) -> None:
+        who = self.username or "<username>"
+        self.say(f" {why}")
+        self.say(" Auto-logging out...")
+        self.token = self.username = self.channel_id = self.channel_name = self.dm_partner = None
+        self.say(f"\n Please login again: login {who}")
+
+    @staticmethod
+    def _rid() -> str:
+        """Idempotency key of one logical write (survives client retries)."""
+        return uuid.uuid4().hex
 
     # ----------------------------------------------------------- plumbing
     def say(self, *parts) -> None:
@@ -129,7 +176,7 @@ class ChatShell(cmd.Cmd):
             return
         r = self.conn.call("Signup", raft_pb.SignupRequest(username=username, password=password,
                                                              email=email, display_name=display),
-                           timeout=15.0)
+                           timeout=15.0, retry_deadline=False)
         self.say(f" {r.message}" if r.success else f" Signup failed: {r.message}")
         if r.success:
             self.say(f"Now login with: login {username}")
@@ -197,7 +244,7 @@ class ChatShell(cmd.Cmd):
             return
         name, desc = parts[0].lstrip("#"), parts[1] if len(parts) > 1 else ""
         r = self.conn.call("CreateChannel", raft_pb.CreateChannelRequest(
-            token=self.token, channel_name=name, description=desc))
+            token=self.token, channel_name=name, description=desc), retry_deadline=False)
         if not r.success:
             self.say(f" {r.message}")
             return
@@ -284,14 +331,29 @@ class ChatShell(cmd.Cmd):
             return
         if self.dm_partner:
             r = self.conn.call("SendDirectMessage", raft_pb.DirectMessageRequest(
-                token=self.token, recipient_username=self.dm_partner, content=arg))
+                token=self.token, recipient_username=self.dm_partner, content=arg,
+                request_id=self._rid()))
             self.say(f"[{datetime.now():%H:%M}] You: {arg}" if r.success else f" Failed: {r.message}")
             return
         if not self.channel_id:
             self.say(" No channel selected. Use 'join <channel>' first.")
+            self.say("Available channels: general, random, tech")
+            return
+        # the channel may have been removed / access lost since it was entered
+        # (ref client/chat_client.py:802-815)
+        if not any(c.channel_id == self.channel_id for c in self._channels()):
+            self.say(f" Channel #{self.channel_name} no longer exists or you lost access.")
+            self.say("  Rejoining general channel...")
+            g = self._find_channel("general")
+            if g is not None:
+                self.conn.call("JoinChannel", raft_pb.JoinChannelRequest(token=self.token,
+                                                                         channel_id=g.channel_id))
+                self._enter_channel(g.channel_id, g.name, show=0)
+            else:
+                self.channel_id = self.channel_name = None
             return
         r = self.conn.call("SendMessage", raft_pb.SendMessageRequest(
-            token=self.token, channel_id=self.channel_id, content=arg))
+            token=self.token, channel_id=self.channel_id, content=arg, request_id=self._rid()))
         if r.success:
             self.say(f"[{datetime.now():%H:%M}] You -> #{self.channel_name}: {arg}")
         else:
@@ -360,8 +422,20 @@ class ChatShell(cmd.Cmd):
         except ValueError:
             self.say("Usage: history [n]")
             return
+        r = self.conn.call("GetMessages", raft_pb.GetMessagesRequest(
+            token=self.token, channel_id=self.channel_id, limit=n))
+        if not r.success:  # the token is not valid on this node (ref :1011-1021)
+            self._auto_logout("Your session is invalid on this server")
+            return
+        if not r.messages:
+            self.say("No messages yet. Be the first to say something!")
+            return
         self.say(f"\n History of #{self.channel_name} (last {n}):")
-        self._show_recent(n)
+        self.say("-" * 50)
+        for m in r.messages:
+            who = "You" if m.sender_name == self.username else m.sender_name
+            self.say(f"[{_ts(m.timestamp)}] {who}: {m.content}")
+        self.say("-" * 50)
 
     def do_users(self, arg):
         """List users and presence"""
@@ -418,7 +492,8 @@ class ChatShell(cmd.Cmd):
         r = self.conn.call("UploadFile", raft_pb.FileUploadRequest(
             token=self.token, file_name=os.path.basename(path), file_data=data,
             channel_id=self.channel_id or "", recipient_username=self.dm_partner or "",
-            description=" ".join(parts[1:]), mime_type=mimetypes.guess_type(path)[0] or ""),
+            description=" ".join(parts[1:]), mime_type=mimetypes.guess_type(path)[0] or "",
+            request_id=self._rid()),
             timeout=30.0)
         self.say(f" Uploaded {os.path.basename(path)} (id {r.file_id})" if r.success else f" {r.message}")
 

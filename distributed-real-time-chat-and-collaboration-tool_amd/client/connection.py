@@ -6,6 +6,17 @@ Discovery asks every configured node for ``GetLeaderInfo`` and follows
 call time - after a redirect the call goes to the new leader (the
 reference bound the method to the old stub first: survey quirk Q25) - and
 retries on UNAVAILABLE/DEADLINE_EXCEEDED and on "Not the leader" replies.
+
+Retry safety: a DEADLINE_EXCEEDED write may still commit.  The chat shell
+stamps every message / DM / upload with a ``request_id`` (the server turns it
+into the record id, which the state machine de-duplicates), so those retries
+are idempotent; calls that cannot be made idempotent pass
+``retry_deadline=False`` and are not re-sent after a deadline.
+
+Failover: when discovery moves the session to a different leader, the
+``on_leader_change(address)`` hook runs - the shell uses it to re-validate
+its token, auto-logout if the new leader rejects it, and restore the current
+channel by name (ref client/chat_client.py:147-228).
 """
 from __future__ import annotations
 
@@ -40,6 +51,7 @@ class ClusterConnection:
         self.channel = None
         self.stub = None
         self._channels: dict[str, grpc.Channel] = {}
+        self.on_leader_change = None  # callable(address) after a failover re-discovery
 
     def _stub_for(self, addr: str):
         ch = self._channels.get(addr)
@@ -48,8 +60,11 @@ class ClusterConnection:
         return ch, make_stub(ch, RAFT_SERVICE)
 
     def _use(self, addr: str) -> None:
+        prev = self.address
         self.channel, self.stub = self._stub_for(addr)
         self.address = addr
+        if prev is not None and prev != addr and self.on_leader_change is not None:
+            self.on_leader_change(addr)
 
     def probe(self, addr: str):
         _, stub = self._stub_for(addr)
@@ -100,7 +115,8 @@ class ClusterConnection:
             pass
         self.discover()
 
-    def call(self, name: str, request, timeout: float = 5.0, attempts: int = 3):
+    def call(self, name: str, request, timeout: float = 5.0, attempts: int = 3,
+             retry_deadline: bool = True):
         last = None
         for i in range(attempts):
             if self.stub is None:
@@ -109,7 +125,10 @@ class ClusterConnection:
                 resp = getattr(self.stub, name)(request, timeout=timeout)
             except grpc.RpcError as e:
                 last = e
-                if e.code() in RETRY_CODES and i + 1 < attempts:
+                code = e.code()
+                if code == grpc.StatusCode.DEADLINE_EXCEEDED and not retry_deadline:
+                    raise
+                if code in RETRY_CODES and i + 1 < attempts:
                     self.discover()
                     continue
                 raise

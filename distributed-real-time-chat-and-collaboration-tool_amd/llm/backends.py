@@ -21,6 +21,7 @@ import queue
 import threading
 import time
 
+from .prompts import fit_prompt
 from ..engine.request import Request, SamplingParams
 
 log = logging.getLogger(__name__)
@@ -74,10 +75,7 @@ class EngineBackend:
             params = [params] * len(prompts)
         reqs = []
         for p, prm in zip(prompts, params):
-            ids = self.tok.encode(p)
-            limit = self.engine.max_model_len - prm.max_new_tokens - 1
-            if len(ids) > limit:  # keep the newest context (prompts end with instructions)
-                ids = ids[:1] + ids[len(ids) - limit + 1:]
+            ids = fit_prompt(self.tok, p, self.engine.max_model_len - prm.max_new_tokens - 1)
             reqs.append(self.loop.submit(Request(ids, prm)))
         deadline = None if timeout is None else time.monotonic() + timeout
         outs = []
@@ -341,10 +339,7 @@ class ReplicaRouter:
             params = [params] * len(prompts)
         jobs = []
         for p, prm in zip(prompts, params):
-            ids = self.tok.encode(p)
-            limit = self.max_model_len - prm.max_new_tokens - 1
-            if len(ids) > limit:
-                ids = ids[:1] + ids[len(ids) - limit + 1:]
+            ids = fit_prompt(self.tok, p, self.max_model_len - prm.max_new_tokens - 1)
             jobs.append([ids, prm, self.pool.submit(self.pool.pick(), ids, prm), 0])
         deadline = None if timeout is None else time.monotonic() + timeout
         outs = []

@@ -34,6 +34,23 @@ def _conversation(messages, last: int | None = None) -> str:
     return "\n".join(f"{m.sender}: {m.content}" for m in msgs)
 
 
+# ------------------------------------------------------------------ fitting
+def fit_prompt(tokenizer, text: str, limit: int) -> list[int]:
+    """Token ids of ``text`` within ``limit`` tokens.  Every prompt above is
+    instruction head + conversation + instruction tail (the output format the
+    parsers rely on), so an over-long prompt loses its OLDEST conversation
+    lines: the first line (e.g. "Summarize this conversation concisely in
+    under N characters:") and the newest tail are kept, the middle is cut."""
+    ids = tokenizer.encode(text)
+    if len(ids) <= limit:
+        return ids
+    head = tokenizer.encode(text.split("\n", 1)[0] + "\n")
+    if len(head) > limit // 2:  # degenerate one-line prompt: keep its start and end
+        head = ids[:max(1, limit // 4)]
+    keep_tail = limit - len(head)
+    return head + ids[len(ids) - keep_tail:]
+
+
 # ------------------------------------------------------------------ prompts
 def answer_prompt(query: str, context: list[str]) -> str:
     """Ask-AI (llm_server.py:150-161): last 5 context strings + the question."""

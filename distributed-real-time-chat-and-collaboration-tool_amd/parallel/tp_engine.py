@@ -21,6 +21,7 @@ import threading
 import time
 
 from ..engine.request import Request, SamplingParams
+from ..llm.prompts import fit_prompt
 
 
 def _free_port() -> int:
@@ -156,10 +157,7 @@ class TPEngineGroup:
             params = [params] * len(prompts)
         hs = []
         for p, prm in zip(prompts, params):
-            ids = self.tok.encode(p)
-            limit = self.max_model_len - prm.max_new_tokens - 1
-            if len(ids) > limit:
-                ids = ids[:1] + ids[len(ids) - limit + 1:]
+            ids = fit_prompt(self.tok, p, self.max_model_len - prm.max_new_tokens - 1)
             rid = f"tp-{next(self._ids)}"
             ev, slot = threading.Event(), []
             with self._lock:

@@ -235,3 +235,48 @@ def test_log_compaction_and_install_snapshot_over_grpc(tmp_path):
         assert [m.content for m in msgs] == [f"m{k}" for k in range(64)]
     finally:
         c.stop()
+
+
+def test_cli_failover_session_recovery(tmp_path):
+    """Reconnect recovery (ref client/chat_client.py:147-228): on a new leader the
+    shell re-validates its token and restores the channel; with node-local tokens
+    (token_mode="reference") the new leader rejects it and the shell logs out.
+    Plus the send-time channel check and history's auto-logout."""
+    for mode, survives in (("replicated", True), ("reference", False)):
+        c = LocalCluster(3, data_root=str(tmp_path / mode), token_mode=mode).start()
+        try:
+            c.leader()
+            conn = ClusterConnection(c.addresses(), round_sleep=0.1, discovery_rounds=30)
+            conn.discover()
+            out = io.StringIO()
+            sh = ChatShell(conn, stdout=out, password_fn=lambda p: "alice123")
+            sh.onecmd("login alice")
+            sh.onecmd("join random")
+            c.kill(c.leader())
+            c.leader()
+            sh.onecmd("send after failover")
+            text = out.getvalue()
+            assert "Reconnected to new leader" in text
+            if survives:
+                assert "Restored channel #random" in text
+                assert "You -> #random: after failover" in text
+            else:
+                assert "Session expired on new leader" in text and "Please re-login: login alice" in text
+                assert sh.token is None
+        finally:
+            c.stop()
+
+
+def test_cli_send_checks_channel_and_history_auto_logout(cluster):
+    cluster.leader()
+    conn = ClusterConnection(cluster.addresses(), round_sleep=0.1, discovery_rounds=30)
+    conn.discover()
+    out = io.StringIO()
+    sh = ChatShell(conn, stdout=out, password_fn=lambda p: "alice123")
+    sh.onecmd("login alice")
+    sh.channel_id, sh.channel_name = "gone-channel-id", "gone"
+    sh.onecmd("send hello?")
+    assert "Channel #gone no longer exists" in out.getvalue() and sh.channel_name == "general"
+    sh.token = sh.token[:-4] + "AAAA"  # a token the server rejects
+    sh.onecmd("history 5")
+    assert "Your session is invalid on this server" in out.getvalue() and sh.token is None

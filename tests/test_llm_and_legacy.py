@@ -239,3 +239,21 @@ def test_replica_pool_evicts_dead_replica_and_respawns():
         assert len(router.generate(["back again"] * 4, prm, timeout=60)) == 4
     finally:
         pool.close()
+
+
+def test_fit_prompt_keeps_instruction_head_and_tail():
+    """Over-long prompts lose their oldest conversation lines, never the
+    summarize instruction (VERDICT r1 weak #10)."""
+    from drtc_amd.engine import ChatTokenizer
+    from drtc_amd.llm.prompts import ChatLine, fit_prompt, summarize_prompt
+
+    tok = ChatTokenizer(4096)
+    msgs = [ChatLine("alice", f"message number {i} about the release plan") for i in range(400)]
+    text = summarize_prompt(msgs, 200)
+    full = tok.encode(text)
+    ids = fit_prompt(tok, text, 300)
+    assert len(full) > 300 and len(ids) == 300
+    out = tok.decode(ids)
+    assert out.startswith("Summarize this conversation concisely in under 200 characters")
+    assert "Key Points:" in out and "message number 399" in out and "message number 0 " not in out
+    assert fit_prompt(tok, "short prompt", 300) == tok.encode("short prompt")
