@@ -192,6 +192,106 @@ __global__ __launch_bounds__(512) void custom_allreduce_kernel(
   }
 }
 
+// One-shot all-reduce fused with the residual add and RMSNorm of a TP decode
+// sublayer: h = residual + sum_q partial_q (fixed rank order, rounded to bf16 once
+// as the all-reduce alone would), residual <- h, normed = rmsnorm(h) * w (Gemma:
+// * (1 + w)).  Block b owns whole rows [b R, (b+1) R), R = chunk / H, which lie
+// inside its fixed staging chunk, so the epoch/parity protocol is the one of the
+// plain kernels (they may be interleaved on one communicator).  Every rank
+// reduces the same bytes in the same order: bit-identical outputs on all ranks.
+__global__ __launch_bounds__(512) void custom_ar_rmsnorm_kernel(
+    bf16_t* __restrict__ normed, bf16_t* __restrict__ residual, const bf16_t* __restrict__ in,
+    const bf16_t* __restrict__ w, ArPeers P, int rank, int world, int rows, int H, float eps,
+    int gemma, int64_t stage_elems, int rows_per_block) {
+  __shared__ uint64_t s_epoch;
+  __shared__ float s_red[16];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  char* mine = P.base[rank];
+  uint64_t* flags = reinterpret_cast<uint64_t*>(mine);
+  uint64_t* ctr = reinterpret_cast<uint64_t*>(mine + kArCounters);
+  int* err = reinterpret_cast<int*>(mine + kArError);
+  if (tid == 0) {
+    const uint64_t e = ctr[b] + 1;
+    ctr[b] = e;
+    s_epoch = e;
+  }
+  __syncthreads();
+  const uint64_t epoch = s_epoch;
+  const int64_t buf_off = kArHeader + (int64_t)(epoch & 1) * stage_elems * 2;
+  const int hv = H / 8;  // vectors per row
+  const int r0 = b * rows_per_block;
+  const int r1 = min(rows, r0 + rows_per_block);
+  const int64_t c0 = (int64_t)r0 * hv, c1 = (int64_t)r1 * hv;
+  bf16x8* my_stage = reinterpret_cast<bf16x8*>(mine + buf_off);
+  const bf16x8* src = reinterpret_cast<const bf16x8*>(in);
+  for (int64_t i = c0 + tid; i < c1; i += blockDim.x) my_stage[i] = src[i];
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  ar_exchange(P, 0, flags, err, b, rank, world, epoch);
+  const bf16x8* wv = reinterpret_cast<const bf16x8*>(w);
+  bf16x8* res = reinterpret_cast<bf16x8*>(residual);
+  bf16x8* outv = reinterpret_cast<bf16x8*>(normed);
+  const int lane = tid & 63, wid = tid >> 6;
+  for (int row = r0; row < r1; ++row) {
+    float ss = 0.f;
+    for (int j = tid; j < hv; j += blockDim.x) {
+      const int64_t i = (int64_t)row * hv + j;
+      float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      for (int q = 0; q < world; ++q) {
+        const bf16x8 v = reinterpret_cast<const bf16x8*>(P.base[q] + buf_off)[i];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] += bf2f(v[e]);
+      }
+      const bf16x8 rv = res[i];
+      bf16x8 hsum;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float o = bf2f(f2bf(acc[e]));  // the all-reduce result, rounded once
+        hsum[e] = f2bf(o + bf2f(rv[e]));
+        const float hf = bf2f(hsum[e]);
+        ss += hf * hf;
+      }
+      res[i] = hsum;
+    }
+    ss = wave_sum(ss);
+    if (lane == 0) s_red[wid] = ss;
+    __syncthreads();
+    float tot = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) tot += s_red[k];
+    const float rstd = rsqrtf(tot / (float)H + eps);
+    for (int j = tid; j < hv; j += blockDim.x) {
+      const int64_t i = (int64_t)row * hv + j;
+      const bf16x8 hsum = res[i];  // this thread wrote it above
+      const bf16x8 ww = wv[j];
+      bf16x8 o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        o[e] = f2bf(bf2f(hsum[e]) * rstd * (bf2f(ww[e]) + (gemma ? 1.f : 0.f)));
+      outv[i] = o;
+    }
+    __syncthreads();  // s_red reuse
+  }
+}
+
+int launch_custom_ar_rmsnorm(void* normed, void* residual, const void* in, const void* w,
+                             int rows, int H, float eps, int gemma, const ArPeers& peers,
+                             int rank, int world, int64_t stage_elems, hipStream_t st) {
+  if (rows == 0) return 0;
+  if (world < 1 || world > kArMaxRanks || rank < 0 || rank >= world || H % 8 != 0 || H > 16384 ||
+      (int64_t)rows * H > stage_elems)
+    return -1;
+  const int64_t chunk = (stage_elems / 8 + kArMaxBlocks - 1) / kArMaxBlocks;  // vectors
+  const int rpb = (int)(chunk / (H / 8));
+  if (rpb < 1) return -1;  // a row does not fit one block's fixed chunk
+  const int nb = (rows + rpb - 1) / rpb;
+  if (nb > kArMaxBlocks) return -1;
+  hipLaunchKernelGGL(custom_ar_rmsnorm_kernel, dim3(nb), dim3(512), 0, st, (bf16_t*)normed,
+                     (bf16_t*)residual, (const bf16_t*)in, (const bf16_t*)w, peers, rank, world,
+                     rows, H, eps, gemma, stage_elems, rpb);
+  return (int)hipGetLastError();
+}
+
 // header + input staging and result staging, each 2 parities x stage_elems bf16
 int64_t custom_ar_buffer_bytes(int64_t stage_elems) { return kArHeader + 8 * stage_elems; }
 

@@ -94,6 +94,16 @@ PYBIND11_MODULE(_hipk, m) {
     return drtc::launch_custom_allreduce(P<void>(out), P<const void>(in), n, p, rank,
                                          (int)bases.size(), stage_elems, two_shot, S(st));
   });
+  m.def("custom_ar_rmsnorm", [](u64 normed, u64 residual, u64 in, u64 w, int rows, int H,
+                                float eps, bool gemma, const std::vector<u64>& bases, int rank,
+                                int64_t stage_elems, u64 st) {
+    drtc::ArPeers p{};
+    if (bases.size() > 8) return -1;
+    for (size_t i = 0; i < bases.size(); ++i) p.base[i] = P<char>(bases[i]);
+    return drtc::launch_custom_ar_rmsnorm(P<void>(normed), P<void>(residual), P<const void>(in),
+                                          P<const void>(w), rows, H, eps, gemma ? 1 : 0, p, rank,
+                                          (int)bases.size(), stage_elems, S(st));
+  });
   m.def("ar_alloc", [](int64_t bytes) {
     void* p = nullptr;
     const int rc = drtc::ar_alloc(&p, bytes);

@@ -314,7 +314,43 @@ __global__ __launch_bounds__(kThreads) void gemm256_kernel(GemmParams p) {
     issue(0);
     if (Q > 1) issue(1);
     if (Q > 2) issue(2);
-    if constexpr (V == 5) {
+    if constexpr (V == 6) {
+      // V5 with the DMA of phase q+3 issued from the COMPUTE segment of phase q,
+      // one 1-KiB piece after every 8 MFMAs (an LDS-DMA issue costs ~60 cycles
+      // among bare MFMAs, 100-185 inside a load segment already carrying 12
+      // ds_reads: MI355X_MICROARCH.md cycle constants).  Region (q+3)&3 held
+      // phase q-1, whose last reader (G1) finished it in I(2q) <= this segment;
+      // the load segment of phase q waits for phase q+1 (issued in the compute
+      // segment of q-2) with one younger phase (q+2) in flight.
+      wait_vm<8>();  // phase 0 landed
+      barrier_raw();
+      if (wr == 1) barrier_raw();
+      for (int q = 0; q < Q; ++q) {
+        bf16x8 fa[8], fb[4];
+        read(q, fa, fb);
+        if (q + 2 < Q) wait_vm<4>();
+        else wait_vm<0>();
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        barrier_raw();
+        const bool dma = q + 3 < Q;
+        bf16_t* dbase = lds + ((q + 3) & 3) * REG + 64 * wv * 32;
+        const int koff = ((q + 3) >> 1) * kBK + ((q + 3) & 1) * 32;
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(fb[j], fa[i], acc[i][j]);
+          if ((i & 1) && dma) {
+            __builtin_amdgcn_sched_barrier(0);
+            glds16(src[i >> 1] + koff, dbase + 16 * (i >> 1) * 32);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        }
+        __builtin_amdgcn_s_setprio(0);
+        barrier_raw();
+      }
+      if (wr == 0) barrier_raw();
+    } else if constexpr (V == 5) {
       // Ping-pong: wave group G0 (wr = 0) and G1 (wr = 1) run the same
       // load | barrier | compute | barrier program, G1 one barrier behind, so on
       // every SIMD (one wave of each group) one wave's 32 MFMAs overlap the other
@@ -626,6 +662,7 @@ int launch_e(const GemmParams& p, int variant, hipStream_t st) {
     case 3: return launch_t<EPI, 3>(p, st);
     case 4: return launch_t<EPI, 4>(p, st);
     case 5: return launch_t<EPI, 5>(p, st);
+    case 6: return launch_t<EPI, 6>(p, st);
     default: return -1;
   }
 }
@@ -640,6 +677,7 @@ int cfg_one() {
 template <int EPI>
 int cfg_epi() {
   return cfg_one<EPI, 1>() | cfg_one<EPI, 2>() | cfg_one<EPI, 3>() | cfg_one<EPI, 5>() |
+         cfg_one<EPI, 6>() |
          (int)hipFuncSetAttribute((const void*)gemm256w4_kernel<EPI>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 4 * 512 * 32 * 2);
 }

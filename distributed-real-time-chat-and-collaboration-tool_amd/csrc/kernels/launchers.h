@@ -63,6 +63,10 @@ int ar_ipc_get(void* p, char* handle);  // 64-byte handle
 int ar_ipc_open(const char* handle, void** p);
 int ar_ipc_close(void* p);
 int ar_error(void* base);
+// One-shot all-reduce + residual add + RMSNorm (decode sublayer epilogue under TP).
+int launch_custom_ar_rmsnorm(void* normed, void* residual, const void* in, const void* w,
+                             int rows, int H, float eps, int gemma, const ArPeers& peers,
+                             int rank, int world, int64_t stage_elems, hipStream_t st);
 int ar_set_epoch(void* base, uint64_t epoch);
 
 // Tuned hipBLASLt projection GEMM y[M,N] = x[M,K] @ W[N,K]^T, bf16 (gemm_lt.cpp).

@@ -9,8 +9,16 @@ MI355X-first layout decisions
   * tensor parallel over RCCL: heads / intermediate columns sharded, one
     all-reduce after o_proj and one after down_proj (or the MoE combine),
     vocab-parallel LM head + all-gather;
-  * expert parallel for MoE: each rank owns E/ep experts, partial expert
-    outputs are summed by the EP all-reduce;
+  * sequence parallel TP prefill (ParallelContext.sequence_parallel): the
+    o / down partial sums are reduce-scattered over tokens, norms and the
+    residual stream live on T/tp rows per rank, and rows are all-gathered
+    only in front of the column-parallel QKV / gate_up GEMMs;
+  * expert parallel for MoE: each rank owns E/ep experts; tokens are
+    dispatched to the expert owners and combined back over all-to-all
+    (parallel/expert_parallel.py: exact splits in prefill, where the rows are
+    already sequence-sharded; decode keeps replicated tokens + the EP
+    all-reduce unless DRTC_EP_DECODE=a2a selects the static-capacity,
+    graph-capturable all-to-all);
   * decode is static-shaped (persistent metadata buffers) so the whole step
     is hipGraph-capturable by the engine.
 
@@ -22,12 +30,17 @@ from __future__ import annotations
 import math
 from dataclasses import dataclass
 
+import os
+
 import torch
 import torch.nn.functional as F
 
 from .. import ops
-from ..parallel.comm import ParallelContext
+from ..parallel.comm import ParallelContext, all_gather_into_tensor
 from .config import ModelConfig
+
+
+_EP_DECODE_A2A = os.environ.get("DRTC_EP_DECODE", "allreduce") == "a2a"
 
 
 @dataclass
@@ -211,14 +224,16 @@ class TransformerLM:
             h = h * float(torch.tensor(math.sqrt(self.cfg.hidden_size), dtype=h.dtype))
         return h
 
-    def _mlp(self, L: dict, x: ops.PendingNorm) -> torch.Tensor:
+    def _mlp(self, L: dict, x: ops.PendingNorm, decode: bool = False) -> torch.Tensor:
         if self.cfg.is_moe:
-            return self._moe(L, x.materialize()), False
+            return self._moe(L, x.materialize(), decode), False
         gu = ops.norm_linear(x, L["gate_up"])
         res = self._fusable_residual(gu, x)
         if res is not None:
             return ops.linear_residual(ops.act_glu(gu, self.cfg.act), L["down"], res), True
         y = ops.glu_linear(gu, L["down"], self.cfg.act)
+        if decode and self.pc.tp_size > 1:
+            return y, False, True  # reduced by the next norm (fused all-reduce + add + norm)
         return self.pc.all_reduce_tp(y), False
 
     def _fusable_residual(self, a: torch.Tensor, x: ops.PendingNorm) -> torch.Tensor | None:
@@ -230,14 +245,37 @@ class TransformerLM:
         res = x.stream()
         return res if ops.residual_fusable(a, res) else None
 
-    def _moe(self, L: dict, x: torch.Tensor) -> torch.Tensor:
+    def _moe_ep_a2a(self, L: dict, x_rows: torch.Tensor, static: bool) -> torch.Tensor:
+        """This rank's token rows through the EP group's experts over
+        all-to-all (dispatch to the expert owners, combine back)."""
+        from ..parallel import expert_parallel as ep
+
+        cfg, pc = self.cfg, self.pc
+        topi, w = ep.route(x_rows, L["router"], cfg.experts_per_token)
+        fn = ep.ep_moe_a2a_static if static else ep.ep_moe_a2a
+        return fn(x_rows, topi, w, L["gate_up"], L["down"], cfg.act, pc.ep_group,
+                  cfg.num_experts, self.moe_ws)
+
+    def _moe(self, L: dict, x: torch.Tensor, decode: bool = False) -> torch.Tensor:
         """Top-k routed experts (Mixtral: softmax over the top-2 logits).
 
         GPU: the fused HIP MoE (ops/moe.py: device-side routing + grouped
         MFMA GEMMs, static launch shapes -> the same code runs eagerly in
         prefill and inside the decode hipGraphs).  CPU: per-expert gather
-        (reference semantics)."""
-        cfg, sh = self.cfg, self.sh
+        (reference semantics).  With EP, tokens replicated over the group
+        (decode / non-SP prefill) are split into per-rank slices for the
+        all-to-all form and all-gathered afterwards."""
+        cfg, sh, pc = self.cfg, self.sh, self.pc
+        T = x.shape[0]
+        a2a = (pc.ep_size > 1 and T % pc.ep_size == 0 and
+               (pc.ep_combine == "a2a" if not decode else _EP_DECODE_A2A))
+        if a2a:
+            t = T // pc.ep_size
+            rows = x[pc.ep_rank * t:(pc.ep_rank + 1) * t]
+            y = self._moe_ep_a2a(L, rows, static=decode)
+            out = x.new_empty((T, x.shape[1]))
+            all_gather_into_tensor(out, y.contiguous(), group=pc.ep_group)
+            return out
         if ops.on_gpu(x):
             out = ops.fused_moe(x, F.linear(x, L["router"]), L["gate_up"], L["down"],
                                 cfg.experts_per_token, cfg.act, cfg.num_experts,
@@ -263,7 +301,7 @@ class TransformerLM:
             return self.pc.all_reduce_ep(out)
         return self.pc.all_reduce_tp(out)
 
-    def _layers(self, h: torch.Tensor, attn_fn) -> torch.Tensor:
+    def _layers(self, h: torch.Tensor, attn_fn, decode: bool = False) -> torch.Tensor:
         """Pre-norm residual stack.  Each sublayer receives its input as an
         ops.PendingNorm (norm(x + residual) not yet computed), so a small
         decode batch can fuse the norm into the first projection."""
@@ -271,14 +309,17 @@ class TransformerLM:
         x = ops.PendingNorm(h, None, self.layers[0]["ln_in"], cfg.rms_eps, cfg.gemma_norm)
         n = len(self.layers)
         for i, L in enumerate(self.layers):
-            # (o, added): added = the projection already added the residual
-            # stream in its GEMM epilogue, o IS the new stream
-            o, added = attn_fn(i, L, x)
+            # (o, added[, partial]): added = the projection already added the
+            # residual stream in its GEMM epilogue, o IS the new stream;
+            # partial = o is still a TP partial sum - the next norm runs the
+            # all-reduce fused with the residual add (ParallelContext.reduce_norm)
+            o, added, *part = attn_fn(i, L, x)
             x = ops.PendingNorm(o, None if added else x.stream(), L["ln_post"], cfg.rms_eps,
-                                cfg.gemma_norm)
-            m, added = self._mlp(L, x)
+                                cfg.gemma_norm, pc=self.pc if part and part[0] else None)
+            m, added, *part = self._mlp(L, x, decode)
             nxt = self.layers[i + 1]["ln_in"] if i + 1 < n else self.final_norm
-            x = ops.PendingNorm(m, None if added else x.stream(), nxt, cfg.rms_eps, cfg.gemma_norm)
+            x = ops.PendingNorm(m, None if added else x.stream(), nxt, cfg.rms_eps, cfg.gemma_norm,
+                                pc=self.pc if part and part[0] else None)
         return x.materialize()
 
     def _logits(self, x: torch.Tensor) -> torch.Tensor:
@@ -287,6 +328,8 @@ class TransformerLM:
 
     def forward_prefill(self, ids: torch.Tensor, meta: PrefillMeta, kv_caches) -> torch.Tensor:
         """Packed varlen prefill. Returns logits of each sequence's last token."""
+        if self.pc.sp_ok(ids.shape[0]):
+            return self._forward_prefill_sp(ids, meta, kv_caches)
         cfg, sh = self.cfg, self.sh
         D = cfg.head_dim
 
@@ -317,6 +360,81 @@ class TransformerLM:
         x = self._layers(self._embed(ids), attn)
         return self._logits(x)
 
+    def _attn_prefill(self, i: int, L: dict, xn: torch.Tensor, meta: PrefillMeta, kv_caches):
+        """QKV + RoPE/KV write + causal attention of a packed prefill chunk on
+        this rank's heads; returns the attention output [T, hq * D]."""
+        cfg, sh = self.cfg, self.sh
+        D = cfg.head_dim
+        qkv = ops.linear(xn, L["qkv"])
+        kc, vc = kv_caches[i] if kv_caches is not None else (None, None)
+        blockwise_v = kc is not None and meta.v_segs is not None
+        ops.rope_kv_(qkv, meta.positions, meta.slots if kc is not None else None,
+                     self.cos_sin, sh.hq, sh.hkv, D, kc, vc, ops.KV_BLOCK, write_v=not blockwise_v)
+        if blockwise_v:
+            ops.kv_write_v(vc, qkv, meta.v_segs, sh.hq, sh.hkv, D)
+        return ops.prefill_attention(qkv, meta.cu_seqlens, sh.hq, sh.hkv, D, cfg.attn_scale,
+                                     True, tiles=meta.tiles, cu_host=meta.cu_host)
+
+    def _forward_prefill_sp(self, ids: torch.Tensor, meta: PrefillMeta, kv_caches) -> torch.Tensor:
+        """Sequence-parallel TP prefill (tp | T).  Rank r holds rows
+        [r T/tp, (r+1) T/tp) of the residual stream; per layer:
+
+          norm(local rows) -> all-gather -> QKV (column-parallel) -> attention
+          on this rank's heads -> o_proj partial -> reduce-scatter -> + residual
+          norm(local rows) -> dense MLP: all-gather -> gate_up -> act -> down ->
+                              reduce-scatter;  MoE (EP): expert all-to-all of
+                              the local rows only (no gather at all)
+
+        i.e. the per-sublayer all-reduce of [T, H] becomes a reduce-scatter +
+        all-gather of the same bytes, while the norms, residual adds and the
+        MoE dispatch work on T/tp rows.  The last layer continues on each
+        sequence's last token only (replicated, all-reduce form)."""
+        cfg, pc = self.cfg, self.pc
+        tp, r = pc.tp_size, pc.tp_rank
+        T = ids.shape[0]
+        t = T // tp
+        n = len(self.layers)
+        moe_a2a = cfg.is_moe and pc.ep_size > 1 and pc.ep_combine == "a2a" and \
+            pc.ep_group is pc.tp_group
+        x = ops.PendingNorm(self._embed(ids[r * t:(r + 1) * t]), None, self.layers[0]["ln_in"],
+                            cfg.rms_eps, cfg.gemma_norm)
+        for i, L in enumerate(self.layers):
+            xn = pc.all_gather_rows(x.materialize())
+            a = self._attn_prefill(i, L, xn, meta, kv_caches)
+            if i == n - 1:
+                # every position is cached: only the last token of each sequence
+                # feeds the logits; finish this layer on those rows, replicated
+                a = a.index_select(0, meta.last_idx)
+                res = pc.all_gather_rows(x.stream()).index_select(0, meta.last_idx)
+                o = pc.all_reduce_tp(ops.linear(a, L["o"]))
+                xr = ops.PendingNorm(o, res, L["ln_post"], cfg.rms_eps, cfg.gemma_norm)
+                m, added = self._mlp(L, xr)
+                xf = ops.PendingNorm(m, None if added else xr.stream(), self.final_norm,
+                                     cfg.rms_eps, cfg.gemma_norm)
+                return self._logits(xf.materialize())
+            o_rows = pc.reduce_scatter_rows(ops.linear(a, L["o"]))
+            x = ops.PendingNorm(o_rows, x.stream(), L["ln_post"], cfg.rms_eps, cfg.gemma_norm)
+            if cfg.is_moe and moe_a2a:
+                m_rows = self._moe_ep_a2a(L, x.materialize(), static=False)
+            elif cfg.is_moe:
+                # experts TP-sharded over the intermediate dim: every rank needs
+                # every token, partial outputs are reduce-scattered
+                xg = pc.all_gather_rows(x.materialize())
+                part = ops.fused_moe(xg, F.linear(xg, L["router"]), L["gate_up"], L["down"],
+                                     cfg.experts_per_token, cfg.act, cfg.num_experts,
+                                     self.sh.expert_offset, workspace=self.moe_ws) \
+                    if ops.on_gpu(xg) else ops.fused_moe_ref(
+                        xg, F.linear(xg, L["router"]), L["gate_up"], L["down"],
+                        cfg.experts_per_token, cfg.act, self.sh.expert_offset)
+                m_rows = pc.reduce_scatter_rows(part)
+            else:
+                xg = pc.all_gather_rows(x.materialize())
+                gu = ops.linear(xg, L["gate_up"])
+                m_rows = pc.reduce_scatter_rows(ops.linear(ops.act_glu(gu, cfg.act), L["down"]))
+            x = ops.PendingNorm(m_rows, x.stream(), self.layers[i + 1]["ln_in"], cfg.rms_eps,
+                                cfg.gemma_norm)
+        raise AssertionError("unreachable")
+
     def forward_decode(self, ids: torch.Tensor, meta: DecodeMeta, kv_caches,
                        attn_out: torch.Tensor | None = None) -> torch.Tensor:
         """One token per sequence; static shapes (graph-capturable)."""
@@ -334,9 +452,12 @@ class TransformerLM:
                                            cfg.attn_scale, out=attn_out,
                                            blocks_per_part=meta.blocks_per_part,
                                            workspace=meta.workspace)
-            return self.pc.all_reduce_tp(ops.linear(a.view(B, sh.hq * D), L["o"])), False
+            o = ops.linear(a.view(B, sh.hq * D), L["o"])
+            if self.pc.tp_size > 1:
+                return o, False, True  # reduced by the next norm (fused all-reduce + add + norm)
+            return o, False
 
-        x = self._layers(self._embed(ids), attn)
+        x = self._layers(self._embed(ids), attn, decode=True)
         return self._logits(x)
 
     # ------------------------------------------------------------ reference

@@ -219,7 +219,7 @@ def norm_linear(p, w: torch.Tensor) -> torch.Tensor:
     the new residual stream is written by the GEMM.  Otherwise the norm is
     materialised and ``linear`` runs."""
     x, res = p.x, p.residual
-    if (_fuse_norm and p._out is None and on_gpu(x) and _enabled and x.dim() == 2
+    if (_fuse_norm and p._out is None and p.pc is None and on_gpu(x) and _enabled and x.dim() == 2
             and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and x.stride(1) == 1
             and w.is_contiguous() and p.w.is_contiguous()
             and (res is None or (res.stride(1) == 1 and res.shape == x.shape))):

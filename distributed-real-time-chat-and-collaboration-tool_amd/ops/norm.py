@@ -57,11 +57,15 @@ class PendingNorm:
     (x itself when there is no residual), which the next PendingNorm adds to.
     """
 
-    __slots__ = ("x", "residual", "w", "eps", "gemma", "_h", "_out")
+    __slots__ = ("x", "residual", "w", "eps", "gemma", "_h", "_out", "pc")
 
     def __init__(self, x: torch.Tensor, residual: torch.Tensor | None, w: torch.Tensor,
-                 eps: float, gemma: bool):
+                 eps: float, gemma: bool, pc=None):
+        """``pc``: a ParallelContext when ``x`` is still a tensor-parallel PARTIAL
+        sum: materialize() then runs the all-reduce fused with the residual add
+        and the norm (ParallelContext.reduce_norm)."""
         self.x, self.residual, self.w, self.eps, self.gemma = x, residual, w, eps, gemma
+        self.pc = pc
         self._h: torch.Tensor | None = None
         self._out: torch.Tensor | None = None
 
@@ -72,7 +76,11 @@ class PendingNorm:
     def materialize(self) -> torch.Tensor:
         if self._out is None:
             res = self.residual
-            self._out = rmsnorm(self.x, self.w, self.eps, self.gemma, residual=res)
+            if self.pc is not None:
+                self._out = self.pc.reduce_norm(self.x, res, self.w, self.eps, self.gemma)
+                self.pc = None
+            else:
+                self._out = rmsnorm(self.x, self.w, self.eps, self.gemma, residual=res)
             self._h = res if res is not None else self.x  # rmsnorm updated res in place
             self.x, self.residual = self._h, None
         return self._out

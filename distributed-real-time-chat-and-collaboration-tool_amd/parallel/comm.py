@@ -11,7 +11,7 @@ are the X1-X3 rows of SURVEY §2.3.
 from __future__ import annotations
 
 import os
-from dataclasses import dataclass
+from dataclasses import dataclass, field
 
 import torch
 import torch.distributed as dist
@@ -47,6 +47,46 @@ def init_distributed(backend: str | None = None, device: torch.device | None = N
     return rank, world
 
 
+# ------------------------------------------------------------ collectives
+# RCCL ("nccl") takes device tensors directly.  gloo implements all-to-all,
+# reduce-scatter and all-gather-into only for host tensors; the one-GPU
+# multi-rank rehearsals (DRTC_DIST_BACKEND=gloo, eager) stage device tensors
+# through host memory here.  Production TP/EP groups are RCCL and never stage.
+def _staged(group, *ts) -> bool:
+    return any(t.is_cuda for t in ts) and dist.get_backend(group) == "gloo"
+
+
+def all_to_all_single(out: torch.Tensor, inp: torch.Tensor, out_splits=None, in_splits=None,
+                      group=None) -> torch.Tensor:
+    if _staged(group, out, inp):
+        o = out.cpu()
+        dist.all_to_all_single(o, inp.cpu(), out_splits, in_splits, group=group)
+        out.copy_(o)
+    else:
+        dist.all_to_all_single(out, inp, out_splits, in_splits, group=group)
+    return out
+
+
+def reduce_scatter_tensor(out: torch.Tensor, inp: torch.Tensor, group=None) -> torch.Tensor:
+    if _staged(group, out, inp):
+        o = out.float().cpu()
+        dist.reduce_scatter_tensor(o, inp.float().cpu(), group=group)
+        out.copy_(o)
+    else:
+        dist.reduce_scatter_tensor(out, inp, group=group)
+    return out
+
+
+def all_gather_into_tensor(out: torch.Tensor, inp: torch.Tensor, group=None) -> torch.Tensor:
+    if _staged(group, out, inp):
+        o = out.cpu()
+        dist.all_gather_into_tensor(o, inp.cpu(), group=group)
+        out.copy_(o)
+    else:
+        dist.all_gather_into_tensor(out, inp, group=group)
+    return out
+
+
 @dataclass
 class ParallelContext:
     tp_size: int = 1
@@ -56,6 +96,14 @@ class ParallelContext:
     ep_rank: int = 0
     ep_group: object = None
     custom_ar: object = None     # CustomAllReduce over the TP group (decode-sized messages)
+    # sequence parallelism for TP prefill: after o/down projections the partial
+    # sums are reduce-scattered over tokens, norms/residuals run on T/tp rows,
+    # and the rows are all-gathered before the next column-parallel GEMM
+    sequence_parallel: bool = field(
+        default_factory=lambda: os.environ.get("DRTC_SEQUENCE_PARALLEL", "1") != "0")
+    # MoE with ep_size > 1: "a2a" = token dispatch/combine over all-to-all
+    # (parallel/expert_parallel.py); "allreduce" = replicated tokens + all-reduce
+    ep_combine: str = field(default_factory=lambda: os.environ.get("DRTC_EP_COMBINE", "a2a"))
 
     @staticmethod
     def single() -> "ParallelContext":
@@ -102,6 +150,19 @@ class ParallelContext:
             v = int(t.item())
         return int(v)
 
+    def reduce_norm(self, x: torch.Tensor, residual: torch.Tensor | None, w: torch.Tensor,
+                    eps: float, gemma: bool) -> torch.Tensor:
+        """norm(all_reduce_tp(x) + residual) * w, residual updated in place: one
+        fused launch (custom one-shot all-reduce + add + RMSNorm) when the
+        message qualifies, else the all-reduce followed by the norm kernel."""
+        from .. import ops
+
+        car = self.custom_ar
+        if (self.tp_size > 1 and car is not None and residual is not None
+                and car.can_fuse_norm(x, residual)):
+            return car.all_reduce_rmsnorm(x, residual, w, eps, gemma)
+        return ops.rmsnorm(self.all_reduce_tp(x), w, eps, gemma, residual=residual)
+
     def all_reduce_tp(self, x: torch.Tensor) -> torch.Tensor:
         if self.tp_size > 1:
             if self.custom_ar is not None and self.custom_ar.can(x):
@@ -116,6 +177,20 @@ class ParallelContext:
                 return self.custom_ar.all_reduce(x)
             dist.all_reduce(x, group=self.ep_group)
         return x
+
+    def sp_ok(self, T: int) -> bool:
+        """Whether a prefill pass of T tokens runs sequence-parallel."""
+        return self.tp_size > 1 and self.sequence_parallel and T % self.tp_size == 0
+
+    def reduce_scatter_rows(self, x: torch.Tensor) -> torch.Tensor:
+        """[T, H] partial sums -> this rank's [T / tp, H] rows of the sum."""
+        out = x.new_empty((x.shape[0] // self.tp_size, x.shape[1]))
+        return reduce_scatter_tensor(out, x.contiguous(), group=self.tp_group)
+
+    def all_gather_rows(self, x: torch.Tensor) -> torch.Tensor:
+        """This rank's [T / tp, H] rows -> [T, H] on every rank."""
+        out = x.new_empty((x.shape[0] * self.tp_size, x.shape[1]))
+        return all_gather_into_tensor(out, x.contiguous(), group=self.tp_group)
 
     def all_gather_tp_lastdim(self, x: torch.Tensor) -> torch.Tensor:
         if self.tp_size == 1:

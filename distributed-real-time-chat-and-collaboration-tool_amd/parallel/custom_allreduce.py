@@ -71,6 +71,31 @@ class CustomAllReduce:
               "custom_allreduce")
         return out
 
+    def can_fuse_norm(self, x: torch.Tensor, residual: torch.Tensor) -> bool:
+        """Whether all_reduce_rmsnorm takes [rows, H] (one-shot, rows whole in
+        one block's fixed staging chunk)."""
+        if not (self.can(x) and x.dim() == 2 and residual.is_contiguous()
+                and residual.shape == x.shape and residual.dtype == x.dtype):
+            return False
+        H = x.shape[1]
+        chunk = (self.stage_elems // 8 + 63) // 64
+        return H % 8 == 0 and H <= 16384 and chunk >= H // 8 and \
+            -(-x.shape[0] // (chunk // (H // 8))) <= 64
+
+    def all_reduce_rmsnorm(self, x: torch.Tensor, residual: torch.Tensor, w: torch.Tensor,
+                           eps: float, gemma: bool = False,
+                           out: torch.Tensor | None = None) -> torch.Tensor:
+        """One launch: residual += sum over ranks of x (rounded to bf16 once, as
+        all_reduce), returns rmsnorm(residual) * w.  Identical bits on every rank."""
+        assert self.can_fuse_norm(x, residual) and w.is_contiguous()
+        if out is None:
+            out = torch.empty_like(x)
+        check(hipk().custom_ar_rmsnorm(out.data_ptr(), residual.data_ptr(), x.data_ptr(),
+                                       w.data_ptr(), x.shape[0], x.shape[1], float(eps),
+                                       bool(gemma), self.bases, self.rank, self.stage_elems,
+                                       stream_ptr(x)), "custom_ar_rmsnorm")
+        return out
+
     def error(self) -> int:
         """Non-zero if a flag wait ever timed out (a peer missed a call)."""
         return hipk().ar_error(self.base)

@@ -63,6 +63,59 @@ def main():
             print(f"rank {rank}: graph mismatch it={it}", flush=True)
             sys.exit(4)
         it += 1
+    # fused all-reduce + residual add + RMSNorm (decode sublayer epilogue)
+    for rows, H, gemma in ((1, 4096, False), (7, 8192, True), (64, 2048, False)):
+        part = data(rank, it, rows * H).view(rows, H).cuda()
+        res0 = data(99, it, rows * H).view(rows, H)
+        w = (data(98, it, H) * 0.1 + 1.0).to(torch.bfloat16)
+        res = res0.cuda()
+        y = car.all_reduce_rmsnorm(part, res, w.cuda(), 1e-5, gemma)
+        torch.cuda.synchronize()
+        o = expected(world, it, rows * H).view(rows, H).float()
+        h = (o + res0.float()).to(torch.bfloat16)
+        ww = w.float() + (1.0 if gemma else 0.0)
+        ref = (h.float() * torch.rsqrt(h.float().pow(2).mean(-1, keepdim=True) + 1e-5) * ww)
+        if not torch.equal(res.cpu(), h):
+            print(f"rank {rank}: fused residual mismatch rows={rows}", flush=True)
+            sys.exit(6)
+        if (y.cpu().float() - ref).abs().max().item() > 0.02 * ref.abs().max().item():
+            print(f"rank {rank}: fused norm mismatch rows={rows}", flush=True)
+            sys.exit(7)
+        ys = [torch.empty_like(y.cpu()) for _ in range(world)]
+        dist.all_gather(ys, y.cpu())
+        if not all(torch.equal(ys[0], t) for t in ys):
+            print(f"rank {rank}: fused norm differs across ranks", flush=True)
+            sys.exit(8)
+        it += 1
+    # back-to-back calls of different sizes and kinds, no host sync in between
+    # (fixed per-block partition: parity reuse stays safe across sizes)
+    outs, wants = [], []
+    for k, n in enumerate((8 * 1001, 1 << 20, 64, 8 * 12345, 4096, 2 << 20, 8 * 3)):
+        x = data(rank, it, n).cuda()
+        outs.append(car.all_reduce(x, two_shot=(k % 3 == 1) and world > 2))
+        wants.append(expected(world, it, n))
+        it += 1
+    torch.cuda.synchronize()
+    for y, want in zip(outs, wants):
+        if not torch.equal(y.cpu(), want):
+            print(f"rank {rank}: mismatch in the unsynchronised mixed-size sequence", flush=True)
+            sys.exit(9)
+    # epochs far past the 32-bit range (64-bit counters and flags)
+    dist.barrier()
+    torch.cuda.synchronize()
+    for start in ((1 << 31) - 3, (1 << 32) - 2):
+        dist.barrier()
+        from drtc_amd.ops._ext import hipk
+        assert hipk().ar_set_epoch(car.base, start) == 0
+        dist.barrier()
+        for _ in range(5):
+            x = data(rank, it, 4096).cuda()
+            y = car.all_reduce(x)
+            torch.cuda.synchronize()
+            if not torch.equal(y.cpu(), expected(world, it, 4096)):
+                print(f"rank {rank}: mismatch after epoch {start}", flush=True)
+                sys.exit(10)
+            it += 1
     if car.error():
         print(f"rank {rank}: flag wait timed out", flush=True)
         sys.exit(5)

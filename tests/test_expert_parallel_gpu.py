@@ -1,9 +1,6 @@
-"""Custom one-/two-shot IPC all-reduce (csrc/kernels/allreduce.hip) with 2, 3
-and 4 ranks as separate processes sharing the box's GPU: exact (bitwise) sums
-vs a fixed-order fp32 reference, staging double-buffer reuse across both
-kernels, hipGraph replay, the fused all-reduce + residual + RMSNorm kernel
-(bit-identical on every rank), unsynchronised mixed-size call sequences and
-64-bit epochs started past 2^31 and 2^32."""
+"""Expert all-to-all (parallel/expert_parallel.py) with the fused HIP expert kernel:
+2 and 4 ranks as separate processes on the box's GPU, exact-split and
+static-capacity forms vs the single-process fp32-accumulated MoE reference."""
 import os
 import subprocess
 import sys
@@ -16,14 +13,14 @@ pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 
-@pytest.mark.parametrize("world", [2, 3, 4, 8])
-def test_custom_allreduce_multiprocess(hipk, world):
+@pytest.mark.parametrize("world", [2, 4])
+def test_ep_all_to_all_fused_experts_multiprocess(hipk, world):
     port = free_port()
     procs = []
     for r in range(world):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
                    MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
-        procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "ar_worker.py")],
+        procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "ep_worker.py")],
                                       env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
                                       text=True))
     outs = []

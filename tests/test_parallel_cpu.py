@@ -20,6 +20,8 @@ def _port():
 
 
 def _ep_worker(rank, world, port, q):
+    """Exact-split and static-capacity expert all-to-all on each rank's token
+    shard vs the single-process MoE over all experts."""
     sys.path.insert(0, ROOT)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -33,9 +35,13 @@ def _ep_worker(rank, world, port, q):
     x_all = torch.randn(world * 13, H, generator=g).to(torch.bfloat16)
     x = x_all[rank * 13:(rank + 1) * 13]
     el = E // world
-    y = ep_moe_forward(x, router, gu[rank * el:(rank + 1) * el], dn[rank * el:(rank + 1) * el], k)
     ref = moe_reference(x_all, router, gu, dn, k)[rank * 13:(rank + 1) * 13]
-    q.put((rank, (y.float() - ref.float()).abs().max().item()))
+    errs = []
+    for static in (False, True):
+        y = ep_moe_forward(x, router, gu[rank * el:(rank + 1) * el], dn[rank * el:(rank + 1) * el],
+                           k, static=static)
+        errs.append((y.float() - ref.float()).abs().max().item())
+    q.put((rank, errs))
     dist.destroy_process_group()
 
 
@@ -47,12 +53,37 @@ def _tp_worker(rank, world, port, q):
     from drtc_amd.parallel.comm import ParallelContext
 
     res = {}
-    for cfg in (TINY_LLAMA, TINY_GEMMA, TINY_MIXTRAL.replace(experts_per_token=4)):
-        pc = ParallelContext.from_world(tp=True, ep=cfg.is_moe)
-        m = TransformerLM(cfg, "cpu", pc=pc, seed=21)
-        out = m.forward_reference([list(range(3, 40))])[0]
-        full = TransformerLM(cfg, "cpu", seed=21).forward_reference([list(range(3, 40))])[0]
-        res[cfg.name] = (out.float() - full.float()).abs().max().item() / full.float().abs().max().item()
+    for cfg in (TINY_LLAMA, TINY_GEMMA, TINY_MIXTRAL.replace(experts_per_token=4),
+                TINY_MIXTRAL):
+        full_m = TransformerLM(cfg, "cpu", seed=21)
+        # 37 tokens: replicated TP path; 38 tokens: sequence-parallel prefill
+        # (+ expert all-to-all for the MoE model)
+        for ids, tag in ((list(range(3, 40)), "tp"), (list(range(3, 41)), "sp")):
+            for ep_mode in (("a2a", "allreduce") if cfg.is_moe else ("a2a",)):
+                pc = ParallelContext.from_world(tp=True, ep=cfg.is_moe)
+                pc.ep_combine = ep_mode
+                m = TransformerLM(cfg, "cpu", pc=pc, seed=21)
+                out = m.forward_reference([ids])[0]
+                full = full_m.forward_reference([ids])[0]
+                key = f"{cfg.name}/k{cfg.experts_per_token}/{tag}/{ep_mode}"
+                res[key] = ((out.float() - full.float()).abs().max().item()
+                            / full.float().abs().max().item())
+        assert pc.sp_ok(38) and not pc.sp_ok(37)
+        if cfg.is_moe:
+            # decode form: static-capacity (graph-capturable) all-to-all on
+            # replicated tokens == the replicated + all-reduce form
+            import drtc_amd.models.transformer as tr
+            x = torch.randn(6, cfg.hidden_size, generator=torch.Generator().manual_seed(1)).to(
+                torch.bfloat16)
+            L = m.layers[0]
+            tr._EP_DECODE_A2A = False
+            y_ar = m._moe(L, x, decode=True)
+            tr._EP_DECODE_A2A = True
+            y_a2a = m._moe(L, x, decode=True)
+            tr._EP_DECODE_A2A = False
+            res[f"{cfg.name}/k{cfg.experts_per_token}/decode_a2a"] = (
+                (y_a2a.float() - y_ar.float()).abs().max().item()
+                / y_ar.float().abs().max().item())
     q.put((rank, res))
     dist.destroy_process_group()
 
@@ -96,8 +127,8 @@ def _run(fn, world=2):
 
 
 def test_ep_all_to_all_matches_reference():
-    for rank, err in _run(_ep_worker):
-        assert err < 0.03, (rank, err)
+    for rank, errs in _run(_ep_worker):
+        assert max(errs) == 0.0, (rank, errs)  # same bf16 roundings, fp32 combine
 
 
 def test_tp_and_ep_model_forward_matches_single_process():
