@@ -58,6 +58,91 @@ def log(rank: int, *a) -> None:
         print("[bench]", *a, file=sys.stderr, flush=True)
 
 
+def _pct(xs, q):
+    xs = sorted(xs)
+    return xs[min(len(xs) - 1, int(round(q * (len(xs) - 1))))] if xs else 0.0
+
+
+def open_loop(args, eng, make_prompts, params, rank, world, tp, device, cfg) -> None:
+    """Open-loop serving: requests arrive as a Poisson process at
+    ``--arrival-rate`` req/s (per replica) whatever the engine's progress, the
+    way chat users issue smart-reply RPCs; latency counts from the SCHEDULED
+    arrival, so queueing behind a busy step is included.  Reports p50/p99 of
+    end-to-end latency, TTFT and TPOT (time per output token after the first)."""
+    import random
+
+    rate = args.arrival_rate
+    n_req = args.requests or int(rate * 20)
+    prompts = []
+    s = 0
+    while len(prompts) < n_req:
+        prompts += make_prompts(1000 + s)
+        s += 1
+    prompts = prompts[:n_req]
+    rng = random.Random(17 + rank)
+    arr, t = [], 0.0
+    for _ in range(n_req):
+        t += rng.expovariate(rate)
+        arr.append(t)
+    eng.stats.clear()
+    if world > 1:
+        dist.barrier()
+    if device.type == "cuda":
+        torch.cuda.synchronize()
+    reqs, i = [], 0
+    t0 = time.perf_counter()
+    while i < n_req or eng.has_work():
+        now = time.perf_counter() - t0
+        while i < n_req and arr[i] <= now:
+            r = Request(prompts[i], params)
+            r.arrival_time = t0 + arr[i]
+            reqs.append(eng.add_request(r))
+            i += 1
+        if eng.has_work():
+            eng.step()
+        elif i < n_req:
+            time.sleep(min(0.002, max(0.0, arr[i] - now)))
+    if device.type == "cuda":
+        torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    lat = [r.latency for r in reqs]
+    ttft = [r.ttft for r in reqs]
+    tpot = [(r.finish_time - r.first_token_time) / (len(r.output_ids) - 1)
+            for r in reqs if len(r.output_ids) > 1]
+    gen = sum(len(r.output_ids) for r in reqs)
+    st = torch.tensor([elapsed, gen, _pct(lat, .5), _pct(lat, .99), _pct(ttft, .5),
+                       _pct(ttft, .99), _pct(tpot, .5), _pct(tpot, .99)], dtype=torch.float64,
+                      device=device)
+    if world > 1:
+        g = st[1].clone()
+        dist.all_reduce(st, op=dist.ReduceOp.MAX)
+        if tp == 1:
+            dist.all_reduce(g)
+        st[1] = g
+    el, gen = float(st[0]), float(st[1])
+    if rank == 0:
+        ms = [round(1000 * float(v), 1) for v in st[2:]]
+        print(json.dumps({
+            "metric": f"{args.workload} open-loop latency at {rate:g} req/s per replica, "
+                      f"{cfg.name} TP={tp}",
+            "mode": "open-loop", "arrival": "poisson", "arrival_rate_per_replica": rate,
+            "n_gpus": world, "requests_per_replica": n_req,
+            "achieved_req_per_s": round(n_req * (world // tp) / el, 1),
+            "gen_tokens_per_s": round(gen / el, 1),
+            "p50_latency_ms": ms[0], "p99_latency_ms": ms[1],
+            "p50_ttft_ms": ms[2], "p99_ttft_ms": ms[3],
+            "p50_tpot_ms": ms[4], "p99_tpot_ms": ms[5],
+            "p99_over_p50_tpot": round(ms[5] / max(ms[4], 1e-9), 2),
+            "scheduler": ("mixed, %d prompt tokens/step" % eng.mixed_tokens) if eng.mixed
+            else "prefill-first",
+            "max_new_tokens": params.max_new_tokens, "dtype": "bf16",
+            "data": "synthetic chat logs, random-init weights",
+            "engine_stats": dict(eng.stats)}), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -77,8 +162,20 @@ def main() -> None:
                     help="record engine/graph spans (roctx + Chrome trace JSON at PATH)")
     ap.add_argument("--kv-fraction", type=float, default=0.85,
                     help="fraction of the free HBM (after weights) given to the paged KV cache")
-    ap.add_argument("--custom-allreduce", action="store_true",
-                    help="TP: one-shot IPC all-reduce for decode-sized messages (else RCCL)")
+    ap.add_argument("--custom-allreduce", dest="custom_allreduce", action="store_true",
+                    default=True,
+                    help="TP: one-shot IPC all-reduce (fused with the residual add + RMSNorm) "
+                         "for decode-sized messages, RCCL above the size threshold (default)")
+    ap.add_argument("--rccl-only", dest="custom_allreduce", action="store_false",
+                    help="TP: every all-reduce on RCCL")
+    ap.add_argument("--arrival-rate", type=float, default=0.0, metavar="REQ_PER_S",
+                    help="open-loop mode: Poisson arrivals at this rate per replica; reports "
+                         "p50/p99 latency, TTFT and TPOT instead of the closed-wave headline")
+    ap.add_argument("--requests", type=int, default=0,
+                    help="open-loop: requests per replica (default: 20 s of arrivals)")
+    ap.add_argument("--mixed-tokens", type=int, default=None,
+                    help="prompt-token budget of a mixed prefill+decode step")
+    ap.add_argument("--no-mixed", action="store_true", help="strict prefill-first scheduling")
     args = ap.parse_args()
     if args.trace:
         from drtc_amd.utils import tracing
@@ -111,6 +208,10 @@ def main() -> None:
     eng = LLMEngine(model, max_batch=args.batch, max_model_len=args.max_model_len,
                     max_prefill_tokens=max(16384, args.batch * 400),
                     kv_fraction=args.kv_fraction, use_graphs=not args.no_graphs, seed=dp_rank)
+    if args.no_mixed:
+        eng.mixed = False
+    if args.mixed_tokens:
+        eng.mixed_tokens = args.mixed_tokens
     if world > 1:
         dist.barrier()  # TP: the custom all-reduce's flag waits are time-bounded
     eng.warmup(capture=True)
@@ -142,6 +243,9 @@ def main() -> None:
 
     for w in range(args.warmup):
         serve(make_prompts(-1 - w))
+    if args.arrival_rate > 0:
+        open_loop(args, eng, make_prompts, params, rank, world, tp, device, cfg)
+        return
     prompts = [make_prompts(s) for s in range(args.steps)]
     prompt_tokens = sum(len(p) for ps in prompts for p in ps)
 

@@ -35,7 +35,7 @@ import torch
 from .. import ops
 from ..utils import tracing
 from ..utils.metrics import METRICS
-from ..models.transformer import PrefillMeta, TransformerLM
+from ..models.transformer import DecodeMeta, PrefillMeta, TransformerLM
 from .decode_runner import DEFAULT_BUCKETS, DecodeRunner
 from .kv_cache import PagedKVCache
 from .request import Request, RequestState, SamplingParams
@@ -105,6 +105,12 @@ class LLMEngine:
         # request is admitted until some running request finishes
         self.watermark = max(1, self.kv.num_blocks // 100)
         self._pressure = False
+        # mixed steps: while requests are running, new prompts are prefilled
+        # INSIDE decode steps, at most ``mixed_tokens`` prompt tokens per step,
+        # so a new wave never stalls running decodes for a whole prefill
+        # (DRTC_MIXED=0: strict prefill-first)
+        self.mixed = os.environ.get("DRTC_MIXED", "1") != "0"
+        self.mixed_tokens = int(os.environ.get("DRTC_MIXED_TOKENS", "4096"))
 
     # ------------------------------------------------------------ API
     def add_request(self, req: Request) -> Request:
@@ -138,6 +144,22 @@ class LLMEngine:
 
     def step(self) -> list[Request]:
         """One scheduler iteration. Returns requests finished in it."""
+        if self.mixed and (self.running or self._inflight is not None) and self._could_admit():
+            done = self._process_inflight() if self._inflight is not None else []
+            with self.lock:
+                self._ensure_blocks()
+                batch = self._admit(self.mixed_tokens) if self.running else self._admit()
+            if batch and self.running:
+                with tracing.span("engine.mixed", seqs=len(batch), batch=len(self.running)):
+                    done += self._run_mixed(batch)
+            elif batch:
+                with tracing.span("engine.prefill", seqs=len(batch)):
+                    done += self._run_prefill(batch)
+            elif self.running:
+                with tracing.span("engine.decode", batch=len(self.running)):
+                    done += self._run_decode()
+            self._record(done)
+            return done
         if self._inflight is not None and self._could_admit():
             # a prefill changes the slot layout: read the in-flight step first
             done = self._process_inflight()
@@ -174,7 +196,8 @@ class LLMEngine:
         M.set_gauge("engine.waiting", len(self.waiting))
 
     # ------------------------------------------------------------ admission
-    def _admit(self) -> list[Request]:
+    def _admit(self, budget: int | None = None) -> list[Request]:
+        budget = self.max_prefill_tokens if budget is None else budget
         batch, tokens = [], 0
         if self._pressure and self.running:
             return batch
@@ -183,7 +206,7 @@ class LLMEngine:
             r = self.waiting[0]
             ids = r.all_ids  # recomputation after preemption includes outputs
             n = len(ids)
-            if batch and tokens + n > self.max_prefill_tokens:
+            if batch and tokens + n > budget:
                 break
             need = math.ceil((n + 1) / BS)
             busy = bool(self.running or batch)
@@ -275,7 +298,11 @@ class LLMEngine:
             finished += self._finish_prefill(reqs, lens, h_tok.numpy())
         return finished
 
-    def _launch_prefill(self, batch: list[Request]):
+    def _launch_prefill(self, batch: list[Request], n_dec: int = 0):
+        """Enqueue one packed prefill of ``batch``.  ``n_dec > 0`` makes it a
+        mixed step: one decode row per running slot 0..n_dec-1 (padded to the
+        decode bucket) rides in the same forward pass - same GEMM launches,
+        paged attention for those rows - and is sampled with the prefill rows."""
         dev = self.device
         cuda = dev.type == "cuda"
         # host metadata, vectorised over the batch (a 1024-prompt prefill is
@@ -292,7 +319,10 @@ class LLMEngine:
         # its kernels per GEMM shape, so stable shapes avoid re-heuristics and
         # first-use code-object loads on every prefill.  Padded rows carry
         # position 0 and slot -1 (no cache write) and are never attended.
-        Tp = _pad_tokens(T)
+        # mixed step: the prefill part is padded so that prefill + decode rows
+        # land on a token bucket (stable GEMM shapes)
+        Bb = self.runner.bucket(n_dec) if n_dec else 0
+        Tp = _pad_tokens(T + Bb) - Bb
         ids = np.zeros(Tp, dtype=np.int32)
         ids[:T] = np.fromiter(itertools.chain.from_iterable(seqs), dtype=np.int32, count=T)
         seq_of = np.repeat(np.arange(nseq), lens_a)
@@ -316,10 +346,33 @@ class LLMEngine:
         self._prefill_step += 1
         params = np.array([(r.params.temperature, r.params.top_p, r.params.top_k) for r in batch],
                           dtype=np.float64).reshape(nseq, 3)
+        dec_i32 = []
+        if n_dec:
+            # decode rows: exactly the staging of a decode step of bucket Bb
+            # (padding rows: context 0, no cache write, greedy)
+            n, MB = n_dec, self.max_blocks
+            d_pos = self.ctx[:n]
+            d_ids = np.zeros(Bb, np.int32); d_ids[:n] = self.last[:n]
+            d_p = np.zeros(Bb, np.int32); d_p[:n] = d_pos
+            d_slot = np.full(Bb, -1, np.int64)
+            d_slot[:n] = self.bt[np.arange(n), d_pos // BS].astype(np.int64) * BS + d_pos % BS
+            d_ctx = np.zeros(Bb, np.int32); d_ctx[:n] = d_pos + 1
+            d_bt = np.zeros((Bb, MB), np.int32); d_bt[:n] = self.bt[:n]
+            d_par = np.zeros((Bb, 3)); d_par[:, 1] = 1.0
+            d_par[:n, 0], d_par[:n, 1], d_par[:n, 2] = self.temp[:n], self.topp[:n], self.topk[:n]
+            ids = np.concatenate([ids, d_ids])
+            pos = np.concatenate([pos, d_p])
+            slots = np.concatenate([slots, d_slot])
+            last_idx = np.concatenate([last_idx, Tp + np.arange(Bb, dtype=np.int64)])
+            params = np.concatenate([params, d_par])
+            dec_i32 = [d_ctx, d_bt.reshape(-1)]
+            # the V of decode rows goes through rope_kv_'s own write
+            seg_tok = seg_len = seg_blk = np.zeros(0, np.int32)
+        R, ns_all = Tp + Bb, nseq + Bb
         h_i32 = torch.from_numpy(np.concatenate([
             ids, pos, np.asarray(cu, np.int32), np.asarray(ts, np.int32),
             np.asarray(tq, np.int32), seg_tok, seg_len, seg_blk,
-            params[:, 2].astype(np.int32)]))
+            params[:, 2].astype(np.int32)] + dec_i32))
         h_i64 = torch.from_numpy(np.concatenate([
             slots, last_idx, np.array([self._prefill_step + (1 << 40)], dtype=np.int64)]))
         h_f32 = torch.from_numpy(params[:, :2].T.astype(np.float32).reshape(-1))
@@ -330,21 +383,30 @@ class LLMEngine:
         t_f32 = h_f32.to(dev, non_blocking=True)
         nt, ns = len(ts), len(seg_tok)
         o = 0
-        d_ids = t_i32[o:o + Tp]; o += Tp
-        d_pos = t_i32[o:o + Tp]; o += Tp
+        d_ids = t_i32[o:o + R]; o += R
+        d_pos = t_i32[o:o + R]; o += R
         d_cu = t_i32[o:o + nseq + 1]; o += nseq + 1
         d_ts = t_i32[o:o + nt]; o += nt
         d_tq = t_i32[o:o + nt]; o += nt
         d_segs = (t_i32[o:o + ns], t_i32[o + ns:o + 2 * ns], t_i32[o + 2 * ns:o + 3 * ns])
         o += 3 * ns
-        topk = t_i32[o:o + nseq]
-        meta = PrefillMeta(positions=d_pos, slots=t_i64[:Tp], cu_seqlens=d_cu, cu_host=cu,
-                           tiles=(d_ts, d_tq), last_idx=t_i64[Tp:Tp + nseq], v_segs=d_segs)
-        step = t_i64[Tp + nseq:Tp + nseq + 1]
-        temp, topp = t_f32[:nseq], t_f32[nseq:]
+        topk = t_i32[o:o + ns_all]; o += ns_all
+        dmeta = None
+        if n_dec:
+            rm = self.runner._meta(Bb)  # decode partitioning + workspace of bucket Bb
+            ctx_d = t_i32[o:o + Bb]; o += Bb
+            bt_d = t_i32[o:o + Bb * self.max_blocks].view(Bb, self.max_blocks)
+            dmeta = DecodeMeta(positions=d_pos[Tp:], slots=t_i64[Tp:R], block_tables=bt_d,
+                               context_lens=ctx_d, blocks_per_part=rm.blocks_per_part,
+                               workspace=rm.workspace)
+        meta = PrefillMeta(positions=d_pos, slots=t_i64[:R], cu_seqlens=d_cu, cu_host=cu,
+                           tiles=(d_ts, d_tq), last_idx=t_i64[R:R + ns_all],
+                           v_segs=None if n_dec else d_segs, decode=dmeta, n_prefill=Tp)
+        step = t_i64[R + ns_all:R + ns_all + 1]
+        temp, topp = t_f32[:ns_all], t_f32[ns_all:]
         logits = self.model.forward_prefill(d_ids, meta, self.kv)
         toks = ops.sample(logits, temp, topk, topp, seed=self.seed, step=step)
-        h_tok = torch.empty(nseq, dtype=torch.int32, pin_memory=cuda)
+        h_tok = torch.empty(ns_all, dtype=torch.int32, pin_memory=cuda)
         h_tok.copy_(toks, non_blocking=cuda)
         ev = None
         if cuda:
@@ -373,6 +435,28 @@ class LLMEngine:
                 r.mark_finished(reason)
                 finished.append(r)
         return finished
+
+    def _run_mixed(self, batch: list[Request]) -> list[Request]:
+        """One forward over [prefill rows of ``batch`` | one decode row per
+        running request] (the running requests' next KV slots are already
+        allocated): the decode rows share the prefill's weight reads and GEMM
+        launches instead of waiting for the prefill to finish."""
+        n = len(self.running)
+        reqs = list(self.running)
+        _, lens, h_tok, ev = self._launch_prefill(batch, n_dec=n)
+        self.stats["mixed_steps"] += 1
+        self.stats["decode_tokens"] += n
+        self.ctx[:n] += 1
+        self.gen[:n] += 1
+        st = {"handle": None, "n": n, "reqs": reqs, "gen": self.gen[:n].copy(),
+              "ctx": self.ctx[:n].copy()}
+        if ev is not None:
+            ev.synchronize()
+        toks = h_tok.numpy()
+        nseq = len(batch)
+        st["toks"] = toks[nseq:nseq + n].copy()
+        done = self._process(st, later_inflight=False)
+        return done + self._finish_prefill(batch, lens, toks[:nseq])
 
     # ------------------------------------------------------------ decode
     def _ensure_blocks(self) -> None:
@@ -480,7 +564,7 @@ class LLMEngine:
         """Read a launched step's tokens; finish requests.  With a later step
         in flight a finished request keeps its slot (its next token is
         discarded) until that step is read."""
-        toks = self.runner.wait(st["handle"])
+        toks = st["toks"] if st.get("handle") is None else self.runner.wait(st["handle"])
         n, reqs = st["n"], st["reqs"]
         live = np.fromiter((r.state != RequestState.FINISHED for r in reqs), dtype=bool, count=n)
         for r, tok, ok in zip(reqs, toks.tolist(), live.tolist()):

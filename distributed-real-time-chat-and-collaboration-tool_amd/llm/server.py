@@ -85,8 +85,11 @@ def main(argv=None):
     ap.add_argument("--model", default="llama-3-8b")
     ap.add_argument("--gpus", type=int, default=1, help="data-parallel replicas (1 process/GPU)")
     ap.add_argument("--tp", type=int, default=1, help="tensor-parallel degree")
-    ap.add_argument("--custom-allreduce", action="store_true",
-                    help="one-shot IPC all-reduce for decode-sized TP messages (else RCCL)")
+    ap.add_argument("--custom-allreduce", dest="custom_allreduce", action="store_true",
+                    default=True,
+                    help="one-shot IPC all-reduce (+ fused residual/RMSNorm) for decode-sized "
+                         "TP messages, RCCL above the threshold (default)")
+    ap.add_argument("--rccl-only", dest="custom_allreduce", action="store_false")
     ap.add_argument("--max-batch", type=int, default=256)
     ap.add_argument("--max-model-len", type=int, default=4096)
     ap.add_argument("--no-graphs", action="store_true")

@@ -52,6 +52,11 @@ class PrefillMeta:
     tiles: tuple | None          # (tile_seq, tile_q0) int32 device tensors
     last_idx: torch.Tensor       # int64 [n] index of each sequence's last token
     v_segs: tuple | None = None  # (tok, len, block) int32: block-wise V write
+    # mixed step (engine/engine.py::_run_mixed): rows [n_prefill, T) are one
+    # decode token per running sequence, attended against the paged cache
+    # with ``decode``'s block tables / context lengths
+    decode: "DecodeMeta | None" = None
+    n_prefill: int = 0
 
 
 @dataclass
@@ -327,8 +332,10 @@ class TransformerLM:
         return self.pc.all_gather_tp_lastdim(logits)
 
     def forward_prefill(self, ids: torch.Tensor, meta: PrefillMeta, kv_caches) -> torch.Tensor:
-        """Packed varlen prefill. Returns logits of each sequence's last token."""
-        if self.pc.sp_ok(ids.shape[0]):
+        """Packed varlen prefill (optionally with decode rows appended, see
+        PrefillMeta.decode). Returns logits of the rows in ``meta.last_idx``:
+        each sequence's last token, then every decode row."""
+        if meta.decode is None and self.pc.sp_ok(ids.shape[0]):
             return self._forward_prefill_sp(ids, meta, kv_caches)
         cfg, sh = self.cfg, self.sh
         D = cfg.head_dim
@@ -342,8 +349,12 @@ class TransformerLM:
                          write_v=not blockwise_v)
             if blockwise_v:
                 ops.kv_write_v(vc, qkv, meta.v_segs, sh.hq, sh.hkv, D)
-            a = ops.prefill_attention(qkv, meta.cu_seqlens, sh.hq, sh.hkv, D, cfg.attn_scale,
-                                      True, tiles=meta.tiles, cu_host=meta.cu_host)
+            if meta.decode is None:
+                a = ops.prefill_attention(qkv, meta.cu_seqlens, sh.hq, sh.hkv, D,
+                                          cfg.attn_scale, True, tiles=meta.tiles,
+                                          cu_host=meta.cu_host)
+            else:
+                a = self._attn_mixed(qkv, meta, kc, vc)
             if i == last:
                 # Every position's K/V is cached and attended to by now; only
                 # each sequence's last token feeds the logits, so the last
@@ -359,6 +370,27 @@ class TransformerLM:
         last = len(self.layers) - 1
         x = self._layers(self._embed(ids), attn)
         return self._logits(x)
+
+    def _attn_mixed(self, qkv: torch.Tensor, meta: PrefillMeta, kc, vc) -> torch.Tensor:
+        """Attention of a mixed step: causal varlen attention over the prefill
+        rows, paged-cache attention for the decode rows (their K/V were just
+        written by rope_kv_), both into one [T, hq * D] buffer."""
+        cfg, sh = self.cfg, self.sh
+        D, Tp, dm = cfg.head_dim, meta.n_prefill, meta.decode
+        T = qkv.shape[0]
+        Bd = T - Tp
+        a = qkv.new_empty((T, sh.hq * D))
+        ap = ops.prefill_attention(qkv[:Tp], meta.cu_seqlens, sh.hq, sh.hkv, D, cfg.attn_scale,
+                                   True, tiles=meta.tiles, cu_host=meta.cu_host, out=a[:Tp])
+        if ap.data_ptr() != a.data_ptr():  # CPU reference returns a new tensor
+            a[:Tp].copy_(ap)
+        if meta.cu_host[-1] < Tp:
+            a[meta.cu_host[-1]:Tp].zero_()  # shape-padding rows: never written by the kernel
+        q = qkv[Tp:].as_strided((Bd, sh.hq, D), (qkv.stride(0), D, 1))
+        ops.paged_decode_attention(q, kc, vc, dm.block_tables, dm.context_lens, cfg.attn_scale,
+                                   out=a[Tp:].view(Bd, sh.hq, D),
+                                   blocks_per_part=dm.blocks_per_part, workspace=dm.workspace)
+        return a
 
     def _attn_prefill(self, i: int, L: dict, xn: torch.Tensor, meta: PrefillMeta, kv_caches):
         """QKV + RoPE/KV write + causal attention of a packed prefill chunk on

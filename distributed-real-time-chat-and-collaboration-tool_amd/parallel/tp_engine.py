@@ -33,7 +33,7 @@ def _free_port() -> int:
 
 
 def tp_worker(rank: int, world: int, port: int, model_name: str, engine_kw: dict, inq, outq,
-              custom_ar: bool = False):
+              custom_ar: bool = True):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
     import torch
@@ -113,7 +113,7 @@ class TPEngineGroup:
     """Front-end handle: generate() on a TP group of ``world`` GPUs."""
 
     def __init__(self, model_name: str, world: int, engine_kw: dict, tokenizer,
-                 start_timeout: float = 1800, custom_allreduce: bool = False):
+                 start_timeout: float = 1800, custom_allreduce: bool = True):
         ctx = mp.get_context("spawn")
         self.inq, self.outq = ctx.Queue(), ctx.Queue()
         port = _free_port()

@@ -137,6 +137,7 @@ def main():
     ap.add_argument("--splitk", default="auto", help="'auto' or comma list tried for every shape")
     ap.add_argument("--only", default="", help="comma list of gemm names")
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--group-ms", default="8", help="comma list of row-tile group sizes")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--no-check", action="store_true")
     ap.add_argument("--smoke", action="store_true", help="tiny-shape launch checks first")
@@ -167,9 +168,11 @@ def main():
         else:
             sks = [int(s) for s in a.splitk.split(",") if (K // 64) % int(s) == 0]
         arms = {"lib": None}
+        gms = [int(g) for g in a.group_ms.split(",")]
         for v in variants:
             for sk in sks:
-                arms[f"v{v}_sk{sk}"] = (v, sk)
+                for gm_ in gms:
+                    arms[f"v{v}_sk{sk}" + (f"_g{gm_}" if len(gms) > 1 else "")] = (v, sk, gm_)
         # correctness
         ref = None if a.no_check else reference(x, w, epi, res)
         status = {}
@@ -177,11 +180,11 @@ def main():
         for arm, cfg in arms.items():
             if cfg is None:
                 continue
-            v, sk = cfg
+            v, sk, gm_ = cfg
             o = torch.empty(M, nout, device=dev, dtype=torch.bfloat16)
             r_in = res.clone() if res is not None else None
             print(f"# check {name} M={M} {arm}", flush=True)
-            G.mfma_gemm(x, w, epi, residual=r_in, out=o, variant=v, splitk=sk)
+            G.mfma_gemm(x, w, epi, residual=r_in, out=o, variant=v, splitk=sk, group_m=gm_)
             torch.cuda.synchronize()  # a fault ends the run here, naming the arm above
             if ref is not None:
                 err = (o.float() - ref).abs().max().item() / max(ref.abs().max().item(), 1e-6)
@@ -202,13 +205,13 @@ def main():
             if cfg is None:
                 fn = lib_fn(x, w, epi, rr, o)
             else:
-                v, sk = cfg
+                v, sk, gm_ = cfg
                 if epi == "residual":
-                    fn = (lambda v=v, sk=sk, rr=rr: G.mfma_gemm(x, w, epi, residual=rr, out=rr,
-                                                                variant=v, splitk=sk))
+                    fn = (lambda v=v, sk=sk, rr=rr, gm_=gm_: G.mfma_gemm(
+                        x, w, epi, residual=rr, out=rr, variant=v, splitk=sk, group_m=gm_))
                 else:
-                    fn = (lambda v=v, sk=sk, o=o: G.mfma_gemm(x, w, epi, out=o, variant=v,
-                                                              splitk=sk))
+                    fn = (lambda v=v, sk=sk, o=o, gm_=gm_: G.mfma_gemm(
+                        x, w, epi, out=o, variant=v, splitk=sk, group_m=gm_))
             runners[arm] = (graph_time if a.graphs else eager_time)(fn, a.iters)
         times = {arm: [] for arm in runners}
         for _ in range(a.rounds):

@@ -50,3 +50,22 @@ def test_bench_two_ranks_gloo():
     p = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, p.stderr[-2000:]
     _check(_json_line(p.stdout), 2)
+
+
+def test_bench_open_loop_poisson():
+    """--arrival-rate: Poisson arrivals, latency from the scheduled arrival,
+    p50/p99 latency / TTFT / TPOT; mixed prefill+decode steps happen."""
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    args = ["--steps", "1", "--warmup", "0", "--model", "tiny-llama", "--batch", "8",
+            "--max-new-tokens", "6", "--max-model-len", "1024", "--arrival-rate", "200",
+            "--requests", "24", "--mixed-tokens", "512"]
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], cwd=ROOT,
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-2000:]
+    r = _json_line(p.stdout)
+    assert r["mode"] == "open-loop" and r["requests_per_replica"] == 24
+    for k in ("p50_latency_ms", "p99_latency_ms", "p50_ttft_ms", "p99_ttft_ms",
+              "p50_tpot_ms", "p99_tpot_ms"):
+        assert r[k] > 0, k
+    assert r["p99_latency_ms"] >= r["p50_latency_ms"]
+    assert r["engine_stats"]["mixed_steps"] > 0

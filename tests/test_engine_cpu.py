@@ -106,6 +106,36 @@ def test_pipelined_decode_matches_synchronous():
     assert st_pipe["decode_steps_pipelined"] > 0 and st_sync["decode_steps_pipelined"] == 0
 
 
+@pytest.mark.parametrize("cfg", [TINY_LLAMA, TINY_MIXTRAL], ids=lambda c: c.name)
+def test_mixed_steps_match_prefill_first(cfg):
+    """Mixed scheduling (late prompts prefilled inside decode steps under a
+    token budget, decode rows attended against the paged cache in the same
+    forward) produces the prefill-first engine's tokens, with finishes, block
+    growth and a budget that splits one arrival wave over several steps."""
+    from drtc_amd.engine import Request
+
+    m = TransformerLM(cfg, "cpu", seed=5)
+    prompts = [list(range(1, 10 + 7 * i)) for i in range(7)]
+
+    def run(mixed: bool):
+        eng = LLMEngine(m, max_batch=8, max_model_len=256, num_blocks=64, use_graphs=False)
+        eng.mixed, eng.mixed_tokens = mixed, 40
+        params = [SamplingParams.greedy(10 + 4 * i, ignore_eos=True) for i in range(7)]
+        reqs = [eng.add_request(Request(list(p), prm)) for p, prm in zip(prompts[:2], params[:2])]
+        for _ in range(3):
+            eng.step()
+        reqs += [eng.add_request(Request(list(p), prm)) for p, prm in zip(prompts[2:], params[2:])]
+        while eng.has_work():
+            eng.step()
+        assert eng.alloc.num_used == 0 and not eng.running
+        return [r.output_ids for r in reqs], eng.stats
+
+    ref, st_ref = run(False)
+    got, st = run(True)
+    assert st["mixed_steps"] >= 2 and st_ref["mixed_steps"] == 0
+    assert got == ref
+
+
 def test_tp2_matches_tp1_logits():
     """TP sharding math (head/column split + reductions) on one process by
     summing the shards' partial outputs by hand."""
