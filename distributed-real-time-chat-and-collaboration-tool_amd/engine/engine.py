@@ -110,7 +110,7 @@ class LLMEngine:
         # so a new wave never stalls running decodes for a whole prefill
         # (DRTC_MIXED=0: strict prefill-first)
         self.mixed = os.environ.get("DRTC_MIXED", "1") != "0"
-        self.mixed_tokens = int(os.environ.get("DRTC_MIXED_TOKENS", "4096"))
+        self.mixed_tokens = int(os.environ.get("DRTC_MIXED_TOKENS", "2048"))
 
     # ------------------------------------------------------------ API
     def add_request(self, req: Request) -> Request:

@@ -112,6 +112,57 @@ def run_load(target, n_requests: int, threads: int, seed: int):
     return lat, errors, t_start, time.time()
 
 
+def run_open_loop(target, n_requests: int, rate: float, seed: int):
+    """Open loop: RPCs issued as a Poisson process at ``rate`` req/s (gRPC
+    futures, one dispatcher thread), whatever the service's progress; latency
+    counts from each request's SCHEDULED send time.  Returns (latencies s,
+    errors, wall start, wall end)."""
+    mode, address, token = target
+    rng = random.Random(seed)
+    if mode == "raft":
+        stubs = [make_stub(grpc.insecure_channel(address), RAFT_SERVICE) for _ in range(8)]
+
+        def req(stub):
+            return stub.GetSmartReply.future(
+                raft_pb.SmartReplyRequest(token=token, channel_id="general"), timeout=120)
+    else:
+        histories = [[llm_pb.Message(sender=m.sender, content=m.content)
+                      for m in channel_history(rng, 5)] for _ in range(64)]
+        stubs = [make_stub(grpc.insecure_channel(address), LLM_SERVICE) for _ in range(8)]
+
+        def req(stub):
+            return stub.GetSmartReply.future(llm_pb.SmartReplyRequest(
+                recent_messages=histories[rng.randrange(len(histories))]), timeout=120)
+    lat, errors, lock = [], [], threading.Lock()
+    done = threading.Semaphore(0)
+
+    def on_done(fut, t_sched):
+        try:
+            r = fut.result()
+            ok = len(r.suggestions) == 3 and (mode != "raft" or r.success)
+            with lock:
+                (lat.append(time.perf_counter() - t_sched) if ok
+                 else errors.append("bad response"))
+        except grpc.RpcError as e:
+            with lock:
+                errors.append(repr(e)[:200])
+        done.release()
+
+    t_start = time.time()
+    t0 = time.perf_counter()
+    t = 0.0
+    for i in range(n_requests):
+        t += rng.expovariate(rate)
+        d = t0 + t - time.perf_counter()
+        if d > 0:
+            time.sleep(d)
+        f = req(stubs[i % len(stubs)])
+        f.add_done_callback(lambda fut, ts=t0 + t: on_done(fut, ts))
+    for _ in range(n_requests):
+        done.acquire()
+    return lat, errors, t_start, time.time()
+
+
 def _client_main(target, n_requests, threads, seed, q):
     q.put(run_load(target, n_requests, threads, seed))
 
@@ -127,6 +178,9 @@ def main():
     ap.add_argument("--requests", type=int, default=1024)
     ap.add_argument("--concurrency", type=int, default=256)
     ap.add_argument("--max-batch", type=int, default=512)
+    ap.add_argument("--arrival-rate", type=float, default=0.0, metavar="REQ_PER_S",
+                    help="open loop: Poisson arrivals at this rate (instead of --concurrency "
+                         "closed-loop clients); reports p50/p99 latency and engine TPOT")
     args = ap.parse_args()
 
     backend, eng = build_backend(args)
@@ -155,7 +209,11 @@ def main():
         run_load(target, 16, 16, 0)
         if eng is not None:
             eng.stats.clear()
-        if args.client_procs > 0:  # clients outside this process (no shared GIL)
+        METRICS.reset()
+        if args.arrival_rate > 0:
+            lat, errors, t_s, t_e = run_open_loop(target, args.requests, args.arrival_rate, 1)
+            dt = t_e - t_s
+        elif args.client_procs > 0:  # clients outside this process (no shared GIL)
             ctx = mp.get_context("spawn")
             q = ctx.Queue()
             k = args.client_procs
@@ -178,8 +236,15 @@ def main():
             dt = t_e - t_s
         lat.sort()
         gen_tokens = (len(lat) * fp.smart.max_new_tokens) if args.backend != "scripted" else 0
+        hist = METRICS.snapshot()["histograms"]
+        tpot = hist.get("engine.tpot_s", {})
         out = {
-            "metric": f"service smart-reply ({args.mode}) requests/s + latency",
+            "metric": f"service smart-reply ({args.mode}) requests/s + latency" +
+                      (f", open loop at {args.arrival_rate:g} req/s" if args.arrival_rate else ""),
+            "load": (f"open-loop poisson {args.arrival_rate:g} req/s" if args.arrival_rate
+                     else f"closed-loop, {args.concurrency} clients"),
+            "p50_tpot_ms": round(1000 * tpot["p50"], 1) if "p50" in tpot else None,
+            "p99_tpot_ms": round(1000 * tpot["p99"], 1) if "p99" in tpot else None,
             "backend": args.backend, "model": args.model if args.backend != "scripted" else None,
             "client_procs": args.client_procs,
             "requests": len(lat), "errors": len(errors), "concurrency": args.concurrency, "seconds": round(dt, 3),

@@ -41,6 +41,22 @@ def main():
         g = (b[0] - a[1]) / 1e3
         if g > min_us:
             print(f"idle {g:.0f} us at {(a[1] - s0) / 1e6:.1f} ms: {a[2]} -> {b[2]}")
+    # idle attribution: summed gap per (previous kernel -> next kernel), split
+    # into the prefill phase (before the first decode attention) and decode
+    t_dec = dec[0][0] if dec else st[-1][1] + 1
+    for phase, sel in (("prefill", lambda t: t < t_dec), ("decode", lambda t: t >= t_dec)):
+        agg, n_gap, tot = {}, {}, 0.0
+        for a, b in zip(st, st[1:]):
+            if not sel(b[0]):
+                continue
+            g = max(0, b[0] - a[1]) / 1e3
+            k = f"{a[2]} -> {b[2]}"
+            agg[k] = agg.get(k, 0.0) + g
+            n_gap[k] = n_gap.get(k, 0) + 1
+            tot += g
+        print(f"\n{phase}: idle between kernels {tot / 1e3:.1f} ms; top transitions:")
+        for k, v in sorted(agg.items(), key=lambda kv: -kv[1])[:12]:
+            print(f"  {v / 1e3:8.2f} ms  {n_gap[k]:6d} x  mean {v / n_gap[k]:7.1f} us  {k}")
 
 
 if __name__ == "__main__":

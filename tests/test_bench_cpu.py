@@ -69,3 +69,15 @@ def test_bench_open_loop_poisson():
         assert r[k] > 0, k
     assert r["p99_latency_ms"] >= r["p50_latency_ms"]
     assert r["engine_stats"]["mixed_steps"] > 0
+
+
+def test_service_bench_open_loop_scripted():
+    """scripts/service_bench.py --arrival-rate: open-loop Poisson RPCs against
+    the LLM gRPC service (scripted backend), latency from the scheduled send."""
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "service_bench.py"),
+                        "--backend", "scripted", "--requests", "40", "--arrival-rate", "150"],
+                       cwd=ROOT, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-2000:]
+    r = _json_line(p.stdout)
+    assert r["load"].startswith("open-loop") and r["requests"] == 40 and r["errors"] == 0
+    assert r["p99_latency_ms"] >= r["p50_latency_ms"] > 0

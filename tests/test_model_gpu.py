@@ -96,6 +96,34 @@ def test_pipelined_decode_with_graphs_matches_synchronous(hipk):
     assert stats[1].get("decode_steps_pipelined", 0) > 0
 
 
+@pytest.mark.parametrize("cfg", [TINY_LLAMA, TINY_GEMMA, TINY_MIXTRAL], ids=lambda c: c.name)
+def test_mixed_prefill_decode_steps_match_reference(hipk, cfg):
+    """Late arrivals are prefilled inside decode steps (HIP varlen attention on
+    the prompt rows + paged decode attention on the running rows, one
+    forward, graphs on for the pure decode steps): every generated token is a
+    maximiser of the full-sequence reference forward."""
+    from drtc_amd.engine import Request
+
+    m = TransformerLM(cfg, "cuda", seed=13)
+    eng = LLMEngine(m, max_batch=16, max_model_len=512, num_blocks=128, use_graphs=True)
+    eng.mixed_tokens = 96
+    prompts = [list(range(1, 30 + 11 * i)) for i in range(8)]
+    prm = SamplingParams.greedy(14, ignore_eos=True)
+    reqs = [eng.add_request(Request(list(p), prm)) for p in prompts[:3]]
+    for _ in range(4):
+        eng.step()
+    reqs += [eng.add_request(Request(list(p), prm)) for p in prompts[3:]]
+    while eng.has_work():
+        eng.step()
+    assert eng.stats["mixed_steps"] >= 2 and eng.alloc.num_used == 0
+    for p, r in zip(prompts, reqs):
+        assert len(r.output_ids) == 14
+        ref = m.forward_reference([p + r.output_ids[:-1]])[0].float()
+        for j, tok in enumerate(r.output_ids):
+            row = ref[len(p) - 1 + j]
+            assert row[tok] >= row.max() - 0.05 * max(1.0, row.abs().max().item()), (j, tok)
+
+
 @pytest.mark.parametrize("cfg", [TINY_LLAMA, TINY_GEMMA], ids=lambda c: c.name)
 def test_prefill_residual_in_gemm_epilogue(hipk, cfg, monkeypatch):
     """o / down projections adding the residual stream in the GEMM epilogue
