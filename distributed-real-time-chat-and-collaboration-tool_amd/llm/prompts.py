@@ -17,6 +17,9 @@ SMART_REPLY_EMPTY = ["Hello!", "How can I help?", "What's on your mind?"]
 SMART_REPLY_PAD = ["I agree", "Interesting point"]
 ANSWER_ERROR = ("I apologize, but I'm having trouble processing your request. "
                 "Please try again.")
+# ref llm_server.py:180 (empty response after every retry)
+ANSWER_EMPTY = ("I'm having trouble generating a response. "
+                "Please try rephrasing your question.")
 SUMMARY_ERROR = "Unable to generate summary at this time."
 SUGGEST_ERROR = ["sounds interesting", "tell me more", "I see"]
 

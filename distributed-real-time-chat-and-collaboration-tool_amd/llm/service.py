@@ -36,10 +36,15 @@ class FeatureParams:
 
 
 class LLMServicer:
-    def __init__(self, backend, params: FeatureParams | None = None, timeout: float = 60.0):
+    def __init__(self, backend, params: FeatureParams | None = None, timeout: float = 60.0,
+                 answer_retries: int = 3, answer_backoff: float = 1.0):
         self.backend = backend
         self.p = params or FeatureParams()
         self.timeout = timeout
+        # Ask-AI retries a failed or empty generation with exponential backoff
+        # (answer_backoff * 2**attempt: 1 s, 2 s), as ref llm_server.py:164-208
+        self.answer_retries = max(1, answer_retries)
+        self.answer_backoff = answer_backoff
 
     def _gen(self, feature: str, prompt: str, params: SamplingParams) -> str:
         t0 = time.perf_counter()
@@ -49,13 +54,35 @@ class LLMServicer:
         return text
 
     def GetLLMAnswer(self, request, context):
-        try:
-            text = self._gen("answer", P.answer_prompt(request.query, list(request.context)), self.p.answer)
-            return llm_pb.LLMResponse(request_id=request.request_id, answer=P.parse_answer(text),
-                                      confidence=0.95)
-        except Exception as e:
-            log.error("LLM answer failed: %s", e)
-            return llm_pb.LLMResponse(request_id=request.request_id, answer=P.ANSWER_ERROR, confidence=0.0)
+        """Ask-AI with retry + exponential backoff (ref llm_server.py:164-208):
+        an exception or an empty answer is retried up to ``answer_retries``
+        attempts, never sleeping past the RPC deadline; the final failure maps
+        to the reference's fallback strings (confidence 0)."""
+        prompt = P.answer_prompt(request.query, list(request.context))
+        empty = False
+        for attempt in range(self.answer_retries):
+            try:
+                answer = P.parse_answer(self._gen("answer", prompt, self.p.answer))
+                if answer:
+                    return llm_pb.LLMResponse(request_id=request.request_id, answer=answer,
+                                              confidence=0.95)
+                empty = True
+                log.warning("empty LLM answer (attempt %d)", attempt + 1)
+            except Exception as e:
+                empty = False
+                log.warning("LLM answer attempt %d/%d failed: %s", attempt + 1,
+                            self.answer_retries, str(e)[:120])
+            if attempt + 1 < self.answer_retries:
+                wait = self.answer_backoff * (2 ** attempt)
+                left = context.time_remaining() if context is not None else None
+                if left is not None and left < wait + 1.0:
+                    break  # no time for another attempt before the caller's deadline
+                METRICS.inc("llm.answer.retries")
+                time.sleep(wait)
+        log.error("LLM answer failed after retries")
+        return llm_pb.LLMResponse(request_id=request.request_id,
+                                  answer=P.ANSWER_EMPTY if empty else P.ANSWER_ERROR,
+                                  confidence=0.0)
 
     def GetSmartReply(self, request, context):
         msgs = list(request.recent_messages)

@@ -15,6 +15,16 @@ MAX_CANDIDATES = 1024
 def sample_ref(logits: torch.Tensor, temperature: torch.Tensor | None = None,
                top_k: torch.Tensor | None = None, top_p: torch.Tensor | None = None,
                generator: torch.Generator | None = None) -> torch.Tensor:
+    """Reference semantics of the HIP sampler (draws differ: torch RNG).
+
+    * temperature <= 0: argmax.
+    * 0 < top_k < V: the tokens whose logit is >= the k-th largest (k capped
+      at MAX_CANDIDATES; ties with the k-th value kept), softmax(l / T) over
+      them, cut at the first sorted position whose inclusive mass reaches
+      top_p, draw.
+    * top_k == 0 (or >= V): exact top-p over the whole vocabulary: token i is
+      kept iff the probability mass of tokens STRICTLY more likely than i is
+      < top_p (so tied tokens are kept or dropped together)."""
     B, V = logits.shape
     out = torch.empty(B, dtype=torch.int32, device=logits.device)
     lf = logits.float()
@@ -23,15 +33,32 @@ def sample_ref(logits: torch.Tensor, temperature: torch.Tensor | None = None,
         if t <= 0:
             out[b] = int(torch.argmax(lf[b]))
             continue
-        k = int(top_k[b]) if top_k is not None and int(top_k[b]) > 0 else MAX_CANDIDATES
-        k = min(k, MAX_CANDIDATES, V)
-        vals, idx = torch.topk(lf[b], k)
-        p = torch.softmax(vals / t, dim=-1)
         pp = float(top_p[b]) if top_p is not None and 0 < float(top_p[b]) < 1 else 1.0
-        cum = torch.cumsum(p, 0)
-        cut = int(torch.searchsorted(cum, torch.tensor(pp * float(cum[-1]))))
-        cut = min(cut, k - 1)
-        p = p[: cut + 1]
+        k = int(top_k[b]) if top_k is not None else 0
+        if 0 < k < V:
+            k = min(k, MAX_CANDIDATES)
+            kth = torch.topk(lf[b], k).values[-1]
+            idx = torch.nonzero(lf[b] >= kth).flatten()
+            vals = lf[b, idx]
+            order = torch.argsort(-vals, stable=True)
+            vals, idx = vals[order], idx[order]
+            p = torch.softmax(vals / t, dim=-1)
+            cum = torch.cumsum(p, 0)
+            cut = int(torch.searchsorted(cum, torch.tensor(pp * float(cum[-1]))))
+            cut = min(cut, len(idx) - 1)
+            p = p[: cut + 1]
+            j = int(torch.multinomial(p / p.sum(), 1, generator=generator))
+            out[b] = int(idx[j])
+            continue
+        vals, idx = torch.sort(lf[b], descending=True, stable=True)
+        p = torch.softmax(vals / t, dim=-1)
+        if pp < 1.0:
+            # mass strictly above each token: the exclusive cumsum at the first
+            # position holding its value
+            excl = torch.cumsum(p, 0) - p
+            first = torch.searchsorted(-vals, -vals, right=False)
+            keep = excl[first] < pp
+            p = p * keep
         j = int(torch.multinomial(p / p.sum(), 1, generator=generator))
         out[b] = int(idx[j])
     return out

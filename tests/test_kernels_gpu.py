@@ -280,6 +280,77 @@ def test_sample_distribution(hipk):
     assert (f - e).abs().max() < 0.04, (f, e)
 
 
+def _nucleus_mask(logits, temp, top_p):
+    """[B, V] bool: token kept by exact top-p (mass strictly above < top_p)."""
+    lf = logits.float() / temp
+    vals, idx = torch.sort(lf, dim=-1, descending=True, stable=True)
+    p = torch.softmax(vals, dim=-1)
+    excl = torch.cumsum(p, -1) - p
+    first = torch.searchsorted(-vals.contiguous(), -vals.contiguous(), right=False)
+    keep_sorted = excl.gather(1, first) < top_p
+    keep = torch.zeros_like(keep_sorted)
+    keep.scatter_(1, idx, keep_sorted)
+    return keep
+
+
+def test_sample_top_p_full_vocab_exact(hipk):
+    """top_k = 0: every draw lies in the exact nucleus of the full 128k vocab,
+    and most draws are ranked below 1024 (nothing is truncated to a candidate
+    list) on a flat distribution."""
+    torch.manual_seed(5)
+    B, V = 256, 128256
+    logits = (torch.randn(B, V, device=DEV) * 0.5).to(torch.bfloat16)
+    logits[:8] *= 8.0  # a few peaked rows (rejection + bisection rounds)
+    temp = torch.full((B,), 1.0, device=DEV)
+    k0 = torch.zeros(B, dtype=torch.int32, device=DEV)
+    pp = torch.full((B,), 0.9, device=DEV)
+    keep = _nucleus_mask(logits, 1.0, 0.9)
+    rank = logits.float().argsort(-1, descending=True).argsort(-1)
+    step = torch.zeros(1, dtype=torch.int64, device=DEV)
+    deep = 0
+    for i in range(6):
+        step.fill_(i)
+        out = ops.sample(logits, temp, k0, pp, seed=11, step=step).long()
+        assert keep.gather(1, out[:, None]).all()
+        deep += int((rank.gather(1, out[:, None])[8:] >= 1024).sum())
+    assert deep > 0.5 * 6 * (B - 8)
+
+
+def test_sample_top_p_distribution_with_ties(hipk):
+    """Exact nucleus frequencies; tied tokens at the cut are kept together."""
+    V, R = 50000, 8192
+    base = torch.full((V,), -30.0)
+    base[7], base[100], base[4000], base[49999] = 2.0, 1.0, 1.0, 0.0
+    logits = base.to(torch.bfloat16).to(DEV).repeat(R, 1)
+    temp = torch.ones(R, device=DEV)
+    out = ops.sample(logits, temp, torch.zeros(R, dtype=torch.int32, device=DEV),
+                     torch.full((R,), 0.6, device=DEV), seed=5).long().cpu()
+    f = torch.bincount(out, minlength=V).float() / R
+    w = torch.tensor([2.0, 1.0, 1.0]).exp()
+    e = w / w.sum()
+    assert abs(f[[7, 100, 4000]].sum().item() - 1.0) < 1e-6  # token 49999 is outside
+    assert (f[[7, 100, 4000]] - e).abs().max() < 0.03, (f[[7, 100, 4000]], e)
+    # top_k = 2 over the same rows: {7, and the lower-index tie... both ties kept}
+    out = ops.sample(logits, temp, torch.full((R,), 2, dtype=torch.int32, device=DEV),
+                     torch.ones(R, device=DEV), seed=6).long().cpu()
+    f = torch.bincount(out, minlength=V).float() / R
+    assert abs(f[[7, 100, 4000]].sum().item() - 1.0) < 1e-6
+    assert (f[[7, 100, 4000]] - e).abs().max() < 0.03
+
+
+def test_sample_top_k_heavy_ties_fallback(hipk):
+    """All-equal rows overflow the candidate gather (radix fallback); rows with
+    three distinct leaders take the fast path; both stay inside the top-k."""
+    B, V = 64, 32000
+    logits = torch.zeros(B, V, device=DEV, dtype=torch.bfloat16)
+    logits[32:, 5], logits[32:, 900], logits[32:, 31999] = 5.0, 4.0, 3.0
+    temp = torch.ones(B, device=DEV)
+    k = torch.full((B,), 3, dtype=torch.int32, device=DEV)
+    out = ops.sample(logits, temp, k, torch.ones(B, device=DEV), seed=2).long().cpu()
+    assert ((out[:32] >= 0) & (out[:32] < V)).all()
+    assert torch.isin(out[32:], torch.tensor([5, 900, 31999])).all()
+
+
 def _moe_inputs(T, H, I, E, seed=0):
     g = torch.Generator(device=DEV).manual_seed(seed)
     x = torch.randn(T, H, device=DEV, generator=g).to(torch.bfloat16)

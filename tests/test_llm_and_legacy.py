@@ -111,6 +111,44 @@ def test_llm_service_fallbacks_on_backend_error():
         srv.stop(0)
 
 
+def test_ask_ai_retries_with_backoff():
+    """GetLLMAnswer retries failures and empty answers with exponential backoff
+    (ref llm_server.py:164-208) and stops retrying when the deadline is near."""
+    from drtc_amd.llm.service import LLMServicer
+
+    class Flaky:
+        def __init__(self, script):
+            self.script, self.calls = list(script), 0
+
+        def generate(self, prompts, params, timeout=None):
+            self.calls += 1
+            item = self.script.pop(0)
+            if isinstance(item, Exception):
+                raise item
+            return [item]
+
+    class Ctx:
+        def __init__(self, left):
+            self.left = left
+
+        def time_remaining(self):
+            return self.left
+
+    req = llm_pb.LLMRequest(request_id="q1", query="what is raft?")
+    b = Flaky([RuntimeError("busy"), "", "Raft is a consensus protocol."])
+    r = LLMServicer(b, answer_backoff=0.01).GetLLMAnswer(req, Ctx(None))
+    assert b.calls == 3 and r.answer == "Raft is a consensus protocol." and r.confidence > 0.9
+    b = Flaky(["", "", ""])
+    r = LLMServicer(b, answer_backoff=0.01).GetLLMAnswer(req, Ctx(None))
+    assert b.calls == 3 and r.answer == P.ANSWER_EMPTY and r.confidence == 0.0
+    b = Flaky([RuntimeError("down")] * 3)
+    r = LLMServicer(b, answer_backoff=0.01).GetLLMAnswer(req, Ctx(None))
+    assert r.answer == P.ANSWER_ERROR and r.request_id == "q1"
+    b = Flaky([RuntimeError("down")] * 3)  # 0.5 s left: no retry fits
+    r = LLMServicer(b, answer_backoff=1.0).GetLLMAnswer(req, Ctx(0.5))
+    assert b.calls == 1 and r.answer == P.ANSWER_ERROR
+
+
 @pytest.mark.slow
 def test_tp2_engine_group_over_gloo():
     """Two lockstep TP ranks (gloo, CPU) produce the same greedy text as TP=1."""
