@@ -402,6 +402,234 @@ __global__ __launch_bounds__(256, D >= 256 ? 1 : 2) void paged_decode_wave_kerne
   }
 }
 
+// Block loads that skip the tokens of a partial last block (nvalid < 32):
+// a K row (256 B at D = 128) or a 4-token V group is not fetched when all of
+// its tokens are past the context; the registers are zeroed instead (their
+// probabilities are exactly 0, zeros keep 0 * V finite).
+template <int D>
+DRTC_DEVICE void load_kv_block_n(KVRegs<D>& r, const bf16_t* kb, const bf16_t* vb, int lane,
+                                 int nvalid) {
+  if (nvalid >= kBS) {
+    load_kv_block<D>(r, kb, vb, lane);
+    return;
+  }
+  const int t = lane & 15, g = lane >> 4;
+  bf16x8 z8;
+  bf16x4 z4;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) z8[j] = f2bf(0.f);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) z4[j] = f2bf(0.f);
+#pragma unroll
+  for (int s = 0; s < D / 32; ++s) {
+    r.k0[s] = z8;
+    r.k1[s] = z8;
+  }
+#pragma unroll
+  for (int i = 0; i < D / 16; ++i) {
+    r.vlo[i] = z4;
+    r.vhi[i] = z4;
+  }
+  if (t < nvalid) {
+#pragma unroll
+    for (int s = 0; s < D / 32; ++s) r.k0[s] = load_bf16x8(kb + t * D + 32 * s + 8 * g);
+  }
+  if (16 + t < nvalid) {
+#pragma unroll
+    for (int s = 0; s < D / 32; ++s) r.k1[s] = load_bf16x8(kb + (16 + t) * D + 32 * s + 8 * g);
+  }
+  if (4 * g < nvalid) {
+#pragma unroll
+    for (int i = 0; i < D / 16; ++i) r.vlo[i] = load_bf16x4(vb + g * (4 * D) + (16 * i + t) * 4);
+  }
+  if (16 + 4 * g < nvalid) {
+#pragma unroll
+    for (int i = 0; i < D / 16; ++i)
+      r.vhi[i] = load_bf16x4(vb + (4 + g) * (4 * D) + (16 * i + t) * 4);
+  }
+}
+
+// Variant 3: persistent waves.  The grid holds ~2 workgroups per CU; wave w
+// of the grid takes work items w, w + W, w + 2W, ... (item = (partition,
+// sequence, kv head), partition slowest) and streams their cache blocks back
+// to back through one register double buffer: the NEXT item's Q and
+// block-table row are loaded when the current item starts, and its first K/V
+// block is issued while the current item's last block is computed, so a
+// wave never pays the ctx -> table -> K/V load chain between items (variant 2
+// pays it once per ~6-block chat context).  Tokens past the context in a
+// partial last block are not fetched (load_kv_block_n).  Math per block is
+// variant 2's; per-item outputs / partials likewise.
+template <int D>
+__global__ __launch_bounds__(256, 2) void paged_decode_persist_kernel(
+    bf16_t* __restrict__ out, float* __restrict__ part_o,
+    float* __restrict__ part_ml, const bf16_t* __restrict__ q, int q_stride,
+    const bf16_t* __restrict__ k_cache, const bf16_t* __restrict__ v_cache,
+    const int* __restrict__ block_tables, int bt_stride,
+    const int* __restrict__ context_lens, int B, int Hq, int Hkv, float scale_log2e,
+    int max_parts, int blocks_per_part) {
+  constexpr int NT = D / 16;
+  constexpr int KS = D / 32;
+  const int lane = threadIdx.x & 63;
+  const int W = gridDim.x * 4;
+  const int BH = B * Hkv;
+  const int n_items = BH * max_parts;
+  const int G = Hq / Hkv;
+  const int col = lane & 15, g = lane >> 4;
+  const int64_t blk_elems = (int64_t)kBS * D;
+
+  struct Item {
+    int it, b, h, ctx, begin, end, nparts;
+  };
+  // first item >= it (stride W) with work; padded sequences get their zeros
+  auto next_item = [&](int it) -> Item {
+    for (; it < n_items; it += W) {
+      const int p = it / BH, bh = it - p * BH;
+      const int b = bh / Hkv, h = bh - b * Hkv;
+      const int ctx = __builtin_amdgcn_readfirstlane(context_lens[b]);
+      if (ctx <= 0) {
+        if (p == 0) {
+          bf16x8 z;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) z[j] = f2bf(0.f);
+          for (int i = lane; i < G * D / 8; i += 64)
+            store_bf16x8(out + ((int64_t)b * Hq + h * G) * D + 8 * i, z);
+        }
+        continue;
+      }
+      const int nblk = (ctx + kBS - 1) / kBS;
+      const int nparts = (nblk + blocks_per_part - 1) / blocks_per_part;
+      if (p >= nparts) continue;
+      const int begin = p * blocks_per_part;
+      return Item{it, b, h, ctx, begin, min(nblk, begin + blocks_per_part), nparts};
+    }
+    return Item{n_items, 0, 0, 0, 0, 0, 0};
+  };
+  auto load_q = [&](bf16x8* qf, const Item& A) {
+    const bf16_t* qrow = q + (int64_t)A.b * q_stride + (int64_t)(A.h * G + col) * D;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      if (col < G) qf[s] = load_bf16x8(qrow + 32 * s + 8 * g);
+      else for (int j = 0; j < 8; ++j) qf[s][j] = f2bf(0.f);
+    }
+  };
+  auto load_bt = [&](const Item& A, int chunk) -> int {
+    const int* bt = block_tables + (int64_t)A.b * bt_stride;
+    return (chunk + lane < A.end) ? bt[chunk + lane] : 0;
+  };
+  auto load_blk = [&](KVRegs<D>& r, const Item& A, int64_t phys, int blk) {
+    load_kv_block_n<D>(r, k_cache + (phys * Hkv + A.h) * blk_elems,
+                       v_cache + (phys * Hkv + A.h) * blk_elems, lane, A.ctx - blk * kBS);
+  };
+
+  Item A = next_item(blockIdx.x * 4 + wave_id_uniform());
+  if (A.it >= n_items) return;
+  bf16x8 qf[KS], qn[KS];
+  load_q(qf, A);
+  int chunk = A.begin;  // block-table slice [chunk, chunk + 64) of item A in bt_reg
+  int bt_reg = load_bt(A, chunk);
+  KVRegs<D> cur, nxt;
+  load_blk(cur, A, __builtin_amdgcn_readlane(bt_reg, 0), A.begin);
+  while (true) {
+    const Item Bn = next_item(A.it + W);
+    const bool have_next = Bn.it < n_items;
+    int bt_n = 0;
+    if (have_next) {
+      load_q(qn, Bn);
+      bt_n = load_bt(Bn, Bn.begin);
+    }
+    f32x4 o[NT];
+#pragma unroll
+    for (int i = 0; i < NT; ++i) o[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    float m = kNegBig, lsum = 0.f;
+    for (int blk = A.begin; blk < A.end; ++blk) {
+      const bool more = blk + 1 < A.end;
+      if (more) {
+        if (blk + 1 - chunk >= 64) {
+          chunk += 64;
+          bt_reg = load_bt(A, chunk);
+        }
+        load_blk(nxt, A, __builtin_amdgcn_readlane(bt_reg, blk + 1 - chunk), blk + 1);
+      } else if (have_next) {
+        load_blk(nxt, Bn, __builtin_amdgcn_readlane(bt_n, 0), Bn.begin);
+      }
+      f32x4 s0 = {0.f, 0.f, 0.f, 0.f}, s1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        s0 = mfma16(cur.k0[s], qf[s], s0);
+        s1 = mfma16(cur.k1[s], qf[s], s1);
+      }
+      const int tok0 = blk * kBS + 4 * g;
+      float bmax = kNegBig;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        s0[r] = (tok0 + r < A.ctx) ? s0[r] * scale_log2e : kNegBig;
+        s1[r] = (tok0 + 16 + r < A.ctx) ? s1[r] * scale_log2e : kNegBig;
+        bmax = fmaxf(bmax, fmaxf(s0[r], s1[r]));
+      }
+      bmax = fmaxf(bmax, __shfl_xor(bmax, 16, 64));
+      bmax = fmaxf(bmax, __shfl_xor(bmax, 32, 64));
+      const float m_new = fmaxf(m, bmax);
+      const float alpha = fast_exp2(m - m_new);
+      m = m_new;
+      bf16x8 pf;
+      float psum = 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float p0 = fast_exp2(s0[r] - m_new);
+        const float p1 = fast_exp2(s1[r] - m_new);
+        psum += p0 + p1;
+        pf[r] = f2bf(p0);
+        pf[4 + r] = f2bf(p1);
+      }
+      lsum = lsum * alpha + psum;
+#pragma unroll
+      for (int i = 0; i < NT; ++i) {
+        o[i] *= alpha;
+        bf16x8 a;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          a[j] = cur.vlo[i][j];
+          a[4 + j] = cur.vhi[i][j];
+        }
+        o[i] = mfma16(a, pf, o[i]);
+      }
+      if (more || have_next) cur = nxt;
+    }
+    lsum += __shfl_xor(lsum, 16, 64);
+    lsum += __shfl_xor(lsum, 32, 64);
+    if (col < G) {
+      const int hq = A.h * G + col;
+      const int p = A.it / BH;
+      if (A.nparts == 1) {
+        const float inv = 1.f / lsum;
+        bf16_t* orow = out + ((int64_t)A.b * Hq + hq) * D + 4 * g;
+#pragma unroll
+        for (int i = 0; i < NT; ++i) {
+          bf16x4 v;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = f2bf(o[i][r] * inv);
+          *reinterpret_cast<bf16x4*>(orow + 16 * i) = v;
+        }
+      } else {
+        const int64_t pi = ((int64_t)A.b * Hq + hq) * max_parts + p;
+        float* po = part_o + pi * D + 4 * g;
+#pragma unroll
+        for (int i = 0; i < NT; ++i) *reinterpret_cast<f32x4*>(po + 16 * i) = o[i];
+        if (g == 0) {
+          part_ml[pi * 2 + 0] = m;
+          part_ml[pi * 2 + 1] = lsum;
+        }
+      }
+    }
+    if (!have_next) break;
+    A = Bn;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) qf[s] = qn[s];
+    chunk = A.begin;
+    bt_reg = bt_n;
+  }
+}
+
 // Merge the per-partition partials of sequences that span > 1 partition.
 __global__ __launch_bounds__(256) void decode_reduce_kernel(
     bf16_t* __restrict__ out, const float* __restrict__ part_o,
@@ -437,6 +665,36 @@ int launch_paged_decode(void* out, float* part_o, float* part_ml, int* counters,
   if (Hkv <= 0 || Hq % Hkv != 0 || Hq / Hkv > 16) return -1;
   if (max_parts > 1 && (!part_o || !part_ml)) return -2;
   const float sl2 = scale * kLog2e;
+  // variant 3 holds two K/V blocks + two Q fragments in registers: at D = 256
+  // that spills, so head_dim 256 (Gemma-2B) runs variant 1
+  if (variant == 3 && D > 128) variant = 1;
+  if (variant == 3) {
+    static int n_cu = 0;
+    if (n_cu == 0) {
+      int dev = 0;
+      (void)hipGetDevice(&dev);
+      if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+          n_cu <= 0)
+        n_cu = 256;
+    }
+    const int items = B * Hkv * max_parts;
+    const dim3 pgrid(std::max(1, std::min((items + 3) / 4, 2 * n_cu))), pblock(256);
+    switch (D) {
+      case 64:
+        hipLaunchKernelGGL(paged_decode_persist_kernel<64>, pgrid, pblock, 0, st, (bf16_t*)out, part_o, part_ml, (const bf16_t*)q, q_stride, (const bf16_t*)k_cache, (const bf16_t*)v_cache, block_tables, bt_stride, context_lens, B, Hq, Hkv, sl2, max_parts, blocks_per_part);
+        break;
+      case 128:
+        hipLaunchKernelGGL(paged_decode_persist_kernel<128>, pgrid, pblock, 0, st, (bf16_t*)out, part_o, part_ml, (const bf16_t*)q, q_stride, (const bf16_t*)k_cache, (const bf16_t*)v_cache, block_tables, bt_stride, context_lens, B, Hq, Hkv, sl2, max_parts, blocks_per_part);
+        break;
+      default:
+        return -1;
+    }
+    if (max_parts > 1)
+      hipLaunchKernelGGL(decode_reduce_kernel, dim3(B * Hq), dim3(256), 0, st,
+                         (bf16_t*)out, (const float*)part_o, (const float*)part_ml,
+                         context_lens, Hq, D, max_parts, blocks_per_part);
+    return (int)hipGetLastError();
+  }
   if (variant == 2) {
     const dim3 wgrid((B * Hkv * max_parts + 3) / 4), wblock(256);
     switch (D) {

@@ -89,7 +89,8 @@ class DecodeRunner:
         m = self._metas.get(Bb)
         if m is None:
             sh = self.model.sh
-            bpp, max_parts = ops.decode_partitioning(Bb, sh.hkv, self.max_blocks)
+            bpp, max_parts = ops.decode_partitioning(Bb, sh.hkv, self.max_blocks,
+                                                     D=self.model.cfg.head_dim)
             ws = ops.DecodeWorkspace(Bb, sh.hq, self.model.cfg.head_dim, max_parts, self.device)
             m = DecodeMeta(positions=self.positions[:Bb], slots=self.slots[:Bb],
                            block_tables=self.bt[:Bb], context_lens=self.ctx[:Bb],

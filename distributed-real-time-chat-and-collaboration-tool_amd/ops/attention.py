@@ -94,14 +94,32 @@ def prefill_attention(qkv: torch.Tensor, cu_seqlens: torch.Tensor, Hq: int, Hkv:
 # 4-wave LDS merge (default); 2 = one wave per (seq, kv head, partition), no
 # merge.  Measured on MI355X (scripts/decode_attn_bench.py, Llama-3-8B heads):
 # equal at batch 1024 (4.8 TB/s), v1 ahead at long contexts.
-DECODE_VARIANT = int(os.environ.get("DRTC_DECODE_VARIANT", "1"))
+# 0 = pick per shape (decode_variant); 1 / 2 / 3 force a kernel variant
+DECODE_VARIANT = int(os.environ.get("DRTC_DECODE_VARIANT", "0"))
+
+
+def decode_variant(batch: int, Hkv: int, D: int, max_blocks: int) -> int:
+    """Kernel variant per decode shape (profiles/r2g_decode_persistent.md):
+    3 (persistent waves, next item prefetched) when there are >= 4096
+    (sequence, kv head) items and D <= 128 - the serving batches (B 1024 x 8
+    kv heads: 141 vs 150 us); 2 (wave per item) when the context must be
+    split over partitions to fill the chip (B 8 x 4k tokens: 30 vs 53 us for
+    variant 1, whose in-kernel merge pays an agent-scope fence per workgroup
+    across the 8 XCD L2s); 1 otherwise (B 256 x ~1k tokens: 196 vs 206 us)."""
+    if DECODE_VARIANT:
+        return DECODE_VARIANT
+    if batch * Hkv >= 4096 and D <= 128:
+        return 3
+    if batch * Hkv < 256 and max_blocks > 8:
+        return 2
+    return 1
 # variant 1 merges split-K partitions inside the attention kernel (last
 # workgroup to finish) instead of a separate decode_reduce launch
 FUSED_SPLIT_MERGE = os.environ.get("DRTC_DECODE_FUSED_MERGE", "1") != "0"
 
 
 def decode_partitioning(batch: int, Hkv: int, max_blocks: int, target_wgs: int = 256,
-                        variant: int | None = None):
+                        variant: int | None = None, D: int = 128):
     """Static (graph-capturable) split of the context into partitions.
 
     Returns (blocks_per_part, max_parts).  Split-K only pays when the batch
@@ -110,7 +128,8 @@ def decode_partitioning(batch: int, Hkv: int, max_blocks: int, target_wgs: int =
     8 kv heads: 84 us unsplit vs 96 us in 4 parts at ~1.7k-token contexts), and
     partitions shorter than ~8 blocks losing to the merge overhead (batch 8 at
     4k tokens: 28 us with 32-block parts vs 40 us with 4-block parts)."""
-    per_wg = 4 if (variant or DECODE_VARIANT) == 2 else 1
+    variant = variant or decode_variant(batch, Hkv, D, max_blocks)
+    per_wg = 4 if variant in (2, 3) else 1
     parts_wanted = max(1, math.ceil(target_wgs * per_wg / max(1, batch * Hkv)))
     bpp = max(8, math.ceil(max_blocks / parts_wanted))
     bpp = ((bpp + 3) // 4) * 4
@@ -179,9 +198,9 @@ def paged_decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torc
     assert block_tables.dtype == torch.int32 and block_tables.stride(1) == 1
     assert context_lens.dtype == torch.int32 and context_lens.numel() >= B
     max_blocks = block_tables.shape[1]
-    variant = variant or DECODE_VARIANT
+    variant = variant or decode_variant(B, Hkv, D, block_tables.shape[1])
     if blocks_per_part is None or workspace is None:
-        blocks_per_part, max_parts = decode_partitioning(B, Hkv, max_blocks, variant=variant)
+        blocks_per_part, max_parts = decode_partitioning(B, Hkv, max_blocks, variant=variant, D=D)
         workspace = DecodeWorkspace(B, Hq, D, max_parts, q.device)
     if out is None:
         out = torch.empty((B, Hq, D), dtype=q.dtype, device=q.device)

@@ -43,6 +43,9 @@ def timeit(fn, iters=50):
     return s.elapsed_time(e) * 1000 / iters
 
 
+VARIANTS = tuple(int(v) for v in (sys.argv[1] if len(sys.argv) > 1 else "1,2,3").split(","))
+
+
 def main():
     rng = random.Random(0)
     cases = [("B1024 ctx150-200", 1024, lambda: rng.randint(150, 200)),
@@ -57,7 +60,7 @@ def main():
         res = []
         outs = []
         maxb = bt.shape[1]
-        for v in (1, 2):
+        for v in VARIANTS:
             bpp0, _ = ops.decode_partitioning(B, 8, maxb, variant=v)
             sweep = sorted({bpp0} | {max(4, -(-maxb // n)) for n in (1, 2, 4, 8, 16)})
             for bpp in sweep:

@@ -113,7 +113,7 @@ def _paged_setup(B, Hq, Hkv, D, ctx_lens, nb_total=None, seed=0):
 @pytest.mark.parametrize("D,Hq,Hkv", [(128, 32, 8), (128, 64, 8), (256, 8, 1), (64, 4, 2),
                                       (128, 16, 16)])
 @pytest.mark.parametrize("ctx_lens", [[1, 31, 32, 33, 100, 257], [513, 1000, 2048], [5]])
-@pytest.mark.parametrize("variant", [1, 2])
+@pytest.mark.parametrize("variant", [1, 2, 3])
 def test_paged_decode(hipk, D, Hq, Hkv, ctx_lens, variant):
     B = len(ctx_lens)
     q, kc, vc, bt, cl = _paged_setup(B, Hq, Hkv, D, ctx_lens)
@@ -166,19 +166,54 @@ def test_paged_decode_fused_split_merge(hipk):
         attn_ops.FUSED_SPLIT_MERGE = saved
 
 
-def test_paged_decode_wave_long_partition(hipk):
-    """Variant 2 with a partition longer than 64 blocks (block-table slice reload)."""
+@pytest.mark.parametrize("variant", [2, 3])
+def test_paged_decode_wave_long_partition(hipk, variant):
+    """Variants 2/3 with a partition longer than 64 blocks (block-table slice reload)."""
     Hq, Hkv, D = 32, 8, 128
     ctx = [4100, 2049, 70]
     q, kc, vc, bt, cl = _paged_setup(3, Hq, Hkv, D, ctx)
     ref = ops.paged_decode_ref(q, kc, vc, bt, cl, D ** -0.5)
     ws = ops.DecodeWorkspace(3, Hq, D, 1, DEV)
     out = ops.paged_decode_attention(q, kc, vc, bt, cl, D ** -0.5, blocks_per_part=bt.shape[1],
-                                     workspace=ws, variant=2)
+                                     workspace=ws, variant=variant)
     _close(out, ref, 2e-2, 2e-2, "long partition")
 
 
-@pytest.mark.parametrize("variant", [1, 2])
+def test_paged_decode_persistent_many_items(hipk):
+    """Variant 3 at a headline-like batch: every wave streams several
+    (sequence, kv head) items (next item prefetched under the current one),
+    padded slots (context 0) in between, partial last blocks of every length;
+    equals variant 1 within bf16 rounding, the reference on a sample, and
+    replays bitwise from a hipGraph."""
+    Hq, Hkv, D = 32, 8, 128
+    rng = torch.Generator().manual_seed(9)
+    B = 1536  # 12288 items > 2 workgroups x 4 waves x 256 CUs
+    ctx = torch.randint(1, 300, (B,), generator=rng)
+    ctx[::97] = 0
+    ctx = ctx.tolist()
+    q, kc, vc, bt, cl = _paged_setup(B, Hq, Hkv, D, ctx, seed=4)
+    v1 = ops.paged_decode_attention(q, kc, vc, bt, cl, D ** -0.5, variant=1)
+    v3 = ops.paged_decode_attention(q, kc, vc, bt, cl, D ** -0.5, variant=3)
+    _close(v3, v1, 1e-2, 1e-2, "v3 vs v1")
+    assert torch.equal(v3[::97], torch.zeros_like(v3[::97]))
+    sel = [1, 2, 500, 1000, B - 1]
+    ref = ops.paged_decode_ref(q[sel], kc, vc, bt[sel], cl[sel], D ** -0.5)
+    _close(v3[sel], ref, 2e-2, 2e-2, "v3 vs ref")
+    bpp, mp = ops.decode_partitioning(B, Hkv, bt.shape[1], variant=3)
+    ws = ops.DecodeWorkspace(B, Hq, D, mp, DEV)
+    out = torch.empty_like(v3)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        ops.paged_decode_attention(q, kc, vc, bt, cl, D ** -0.5, out=out, blocks_per_part=bpp,
+                                   workspace=ws, variant=3)
+    for _ in range(2):
+        out.fill_(7.0)
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(out, v3)
+
+
+@pytest.mark.parametrize("variant", [1, 2, 3])
 def test_paged_decode_strided_q_and_padding(hipk, variant):
     Hq, Hkv, D = 32, 8, 128
     ctx = [40, 0, 77]
@@ -194,7 +229,7 @@ def test_paged_decode_strided_q_and_padding(hipk, variant):
     assert ctx
 
 
-@pytest.mark.parametrize("variant", [1, 2])
+@pytest.mark.parametrize("variant", [1, 2, 3])
 def test_paged_decode_spike(hipk, variant):
     """One key dominating forces the online-softmax rescale branch."""
     Hq, Hkv, D = 8, 2, 128
