@@ -148,7 +148,7 @@ class LLMEngine:
             done = self._process_inflight() if self._inflight is not None else []
             with self.lock:
                 self._ensure_blocks()
-                batch = self._admit(self.mixed_tokens) if self.running else self._admit()
+                batch = self._admit(self._mixed_budget()) if self.running else self._admit()
             if batch and self.running:
                 with tracing.span("engine.mixed", seqs=len(batch), batch=len(self.running)):
                     done += self._run_mixed(batch)
@@ -196,6 +196,17 @@ class LLMEngine:
         M.set_gauge("engine.waiting", len(self.waiting))
 
     # ------------------------------------------------------------ admission
+    def _mixed_budget(self) -> int:
+        """Prompt tokens a mixed step may add: ``mixed_tokens`` (keeps the
+        decode rows' TPOT near a pure decode step) while the queue is short,
+        growing to a quarter of the waiting prompt tokens (at most one prefill
+        chunk) under a backlog, so sustained overload is drained in
+        efficient large chunks - with the decode rows still riding along -
+        instead of throttling admission (closed-loop service load: 309 req/s
+        with the fixed budget vs 370 prefill-first)."""
+        waiting = sum(len(r.prompt_ids) + len(r.output_ids) for r in self.waiting)
+        return max(self.mixed_tokens, min(self.prefill_chunk_tokens, waiting // 4))
+
     def _admit(self, budget: int | None = None) -> list[Request]:
         budget = self.max_prefill_tokens if budget is None else budget
         batch, tokens = [], 0

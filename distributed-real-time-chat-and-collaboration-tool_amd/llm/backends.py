@@ -119,10 +119,16 @@ def _worker_main(rank: int, device: str, model_name: str, engine_kw: dict, inq, 
         outq.put(("fatal", rank, repr(e)))
         return
     pending = {}
+    parent = os.getppid()
 
     def watcher():
         last_hb = 0.0
         while True:
+            if os.getppid() != parent:
+                # the parent died without closing the pool (os._exit, SIGKILL):
+                # do not stay behind holding the GPU and its KV cache
+                log.error("engine replica %d: parent process gone, exiting", rank)
+                os._exit(0)
             for rid, r in list(pending.items()):
                 if r._done.is_set():
                     pending.pop(rid, None)
@@ -333,6 +339,10 @@ class ReplicaRouter:
         self.tok = tokenizer
         self.max_model_len = max_model_len
         self.max_redispatch = max_redispatch
+
+    def close(self):
+        """Stop the engine worker processes (and free their GPUs)."""
+        self.pool.close()
 
     def generate(self, prompts, params, timeout=None):
         if isinstance(params, SamplingParams):

@@ -15,3 +15,5 @@ run() {  # tag, args
 run direct_inproc --mode direct --requests 2048 --concurrency 1024 --max-batch 1024 || exit 1
 run direct_pool --backend pool --client-procs 8 --mode direct --requests 2048 --concurrency 1024 --max-batch 1024 || exit 1
 run raft_pool --backend pool --client-procs 8 --mode raft --requests 2048 --concurrency 1024 --max-batch 1024 || exit 1
+# open loop (Poisson) through the Raft leader: latency from the scheduled send
+run raft_pool_open300 --backend pool --mode raft --requests 4500 --arrival-rate 300 --max-batch 1024 || exit 1

@@ -295,3 +295,34 @@ def test_fit_prompt_keeps_instruction_head_and_tail():
     assert out.startswith("Summarize this conversation concisely in under 200 characters")
     assert "Key Points:" in out and "message number 399" in out and "message number 0 " not in out
     assert fit_prompt(tok, "short prompt", 300) == tok.encode("short prompt")
+
+
+def test_pool_workers_exit_when_parent_dies():
+    """A parent that dies without closing its WorkerPool (os._exit, SIGKILL)
+    must not leave engine workers behind holding the device and its KV cache."""
+    import subprocess
+    import sys as _sys
+
+    code = r"""
+import os, sys
+sys.path.insert(0, %r)
+from drtc_amd.llm.backends import WorkerPool
+pool = WorkerPool("tiny-llama", ["cpu"], dict(max_batch=2, max_model_len=128, num_blocks=16,
+                  use_graphs=False), hb_interval=0.2)
+print(pool.procs[0].pid, flush=True)
+os._exit(0)
+""" % os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    p = subprocess.run([_sys.executable, "-c", code], capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stderr[-2000:]
+    pid = int(p.stdout.strip().splitlines()[-1])
+    deadline = time.time() + 30
+    while time.time() < deadline:
+        try:
+            os.kill(pid, 0)
+        except ProcessLookupError:
+            return
+        with open(f"/proc/{pid}/stat") as f:  # reaped zombie counts as gone
+            if f.read().split()[2] == "Z":
+                return
+        time.sleep(0.2)
+    raise AssertionError(f"engine worker {pid} outlived its parent")
