@@ -63,11 +63,11 @@ PYBIND11_MODULE(_hipk, m) {
   m.def("prefill_attn",
         [](u64 out, int out_stride, u64 qkv, int qkv_stride, int Hq, int Hkv,
            int D, u64 cu_seqlens, u64 tile_seq, u64 tile_q0, int ntiles,
-           float scale, int causal, u64 st) {
+           float scale, int causal, int persist, u64 st) {
           return drtc::launch_prefill_attn(
               P<void>(out), out_stride, P<const void>(qkv), qkv_stride, Hq, Hkv, D,
               P<const int>(cu_seqlens), P<const int>(tile_seq),
-              P<const int>(tile_q0), ntiles, scale, causal, S(st));
+              P<const int>(tile_q0), ntiles, scale, causal, persist, S(st));
         });
   m.def("moe", [](u64 out, u64 x, u64 logits, u64 w_gu, u64 w_dn, int T, int H, int I, int E,
                   int k, int e_off, int e_local, int act, u64 ws, int64_t ws_bytes, int variant,

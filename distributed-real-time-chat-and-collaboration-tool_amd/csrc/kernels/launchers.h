@@ -38,7 +38,7 @@ int launch_paged_decode(void* out, float* part_o, float* part_ml, int* counters,
 int launch_prefill_attn(void* out, int out_stride, const void* qkv,
                         int qkv_stride, int Hq, int Hkv, int D,
                         const int* cu_seqlens, const int* tile_seq,
-                        const int* tile_q0, int ntiles, float scale, int causal,
+                        const int* tile_q0, int ntiles, float scale, int causal, int persist,
                         hipStream_t st);
 
 int launch_sample(int* out_tokens, const void* logits, int B, int V, int ld,

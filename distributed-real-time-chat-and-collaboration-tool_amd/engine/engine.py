@@ -412,7 +412,8 @@ class LLMEngine:
                                workspace=rm.workspace)
         meta = PrefillMeta(positions=d_pos, slots=t_i64[:R], cu_seqlens=d_cu, cu_host=cu,
                            tiles=(d_ts, d_tq), last_idx=t_i64[R:R + ns_all],
-                           v_segs=None if n_dec else d_segs, decode=dmeta, n_prefill=Tp)
+                           v_segs=None if n_dec else d_segs, decode=dmeta, n_prefill=Tp,
+                           max_len=int(lens_a.max()))
         step = t_i64[R + ns_all:R + ns_all + 1]
         temp, topp = t_f32[:ns_all], t_f32[ns_all:]
         logits = self.model.forward_prefill(d_ids, meta, self.kv)

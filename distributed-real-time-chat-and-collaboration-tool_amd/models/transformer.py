@@ -57,6 +57,7 @@ class PrefillMeta:
     # with ``decode``'s block tables / context lengths
     decode: "DecodeMeta | None" = None
     n_prefill: int = 0
+    max_len: int | None = None   # longest sequence (prefill attention launch form)
 
 
 @dataclass
@@ -352,7 +353,7 @@ class TransformerLM:
             if meta.decode is None:
                 a = ops.prefill_attention(qkv, meta.cu_seqlens, sh.hq, sh.hkv, D,
                                           cfg.attn_scale, True, tiles=meta.tiles,
-                                          cu_host=meta.cu_host)
+                                          cu_host=meta.cu_host, max_len=meta.max_len)
             else:
                 a = self._attn_mixed(qkv, meta, kc, vc)
             if i == last:
@@ -381,7 +382,8 @@ class TransformerLM:
         Bd = T - Tp
         a = qkv.new_empty((T, sh.hq * D))
         ap = ops.prefill_attention(qkv[:Tp], meta.cu_seqlens, sh.hq, sh.hkv, D, cfg.attn_scale,
-                                   True, tiles=meta.tiles, cu_host=meta.cu_host, out=a[:Tp])
+                                   True, tiles=meta.tiles, cu_host=meta.cu_host,
+                                   max_len=meta.max_len, out=a[:Tp])
         if ap.data_ptr() != a.data_ptr():  # CPU reference returns a new tensor
             a[:Tp].copy_(ap)
         if meta.cu_host[-1] < Tp:
@@ -405,7 +407,8 @@ class TransformerLM:
         if blockwise_v:
             ops.kv_write_v(vc, qkv, meta.v_segs, sh.hq, sh.hkv, D)
         return ops.prefill_attention(qkv, meta.cu_seqlens, sh.hq, sh.hkv, D, cfg.attn_scale,
-                                     True, tiles=meta.tiles, cu_host=meta.cu_host)
+                                     True, tiles=meta.tiles, cu_host=meta.cu_host,
+                                     max_len=meta.max_len)
 
     def _forward_prefill_sp(self, ids: torch.Tensor, meta: PrefillMeta, kv_caches) -> torch.Tensor:
         """Sequence-parallel TP prefill (tp | T).  Rank r holds rows

@@ -11,6 +11,7 @@ them is fused here.
 from ._ext import on_gpu, reference_mode
 from .activation import act_glu, act_glu_ref
 from .attention import (KV_BLOCK, DecodeWorkspace, decode_partitioning, paged_decode_attention,
+                        set_prefill_persist,
                         paged_decode_ref, prefill_attention, prefill_attention_ref, prefill_tiles)
 from .gemm import glu_linear, linear, linear_residual, norm_linear, residual_fusable
 from .moe import fused_moe, fused_moe_ref

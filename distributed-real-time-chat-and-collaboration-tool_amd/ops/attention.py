@@ -14,6 +14,22 @@ from .rope import v_block_tokens
 
 KV_BLOCK = 32  # tokens per cache block (fixed by the decode kernel)
 PREFILL_QTILE = 64
+# Prefill attention launch form (profiles/r2j_prefill_persistent.md): persistent
+# workgroups win 9-10 % on chat-length prompts, one workgroup per (query tile,
+# head group) wins on long prompts (4k tokens: 8 %); parity around 430 tokens.
+PERSIST_MAX_LEN = 1024
+_prefill_persist = [{"1": True, "0": False}.get(os.environ.get("DRTC_PREFILL_PERSIST", ""))]
+
+
+def set_prefill_persist(on: bool | None) -> None:
+    """Force the prefill attention launch form (None: per call, by the
+    longest sequence of the batch)."""
+    _prefill_persist[0] = None if on is None else bool(on)
+
+
+def prefill_persist_for(max_len: int) -> bool:
+    forced = _prefill_persist[0]
+    return forced if forced is not None else max_len <= PERSIST_MAX_LEN
 
 
 # ----------------------------------------------------------------- prefill
@@ -57,7 +73,8 @@ def prefill_attention(qkv: torch.Tensor, cu_seqlens: torch.Tensor, Hq: int, Hkv:
                       D: int, scale: float, causal: bool = True,
                       tiles: tuple[torch.Tensor, torch.Tensor] | None = None,
                       cu_host: list[int] | None = None,
-                      out: torch.Tensor | None = None) -> torch.Tensor:
+                      out: torch.Tensor | None = None,
+                      max_len: int | None = None) -> torch.Tensor:
     """Packed varlen attention reading q/k/v from the fused QKV buffer.
 
     qkv: [T, >= (Hq + 2Hkv) * D] bf16 (RoPE already applied);
@@ -82,10 +99,13 @@ def prefill_attention(qkv: torch.Tensor, cu_seqlens: torch.Tensor, Hq: int, Hkv:
         tiles = (torch.tensor(ts, dtype=torch.int32, device=dev),
                  torch.tensor(tq, dtype=torch.int32, device=dev))
     ntiles = tiles[0].numel()
+    if max_len is None and _prefill_persist[0] is None:
+        max_len = max(b - a for a, b in zip(cu, cu[1:]))
+    persist = prefill_persist_for(max_len or 0)
     check(hipk().prefill_attn(out.data_ptr(), out.stride(0), qkv.data_ptr(), qkv.stride(0),
                               Hq, Hkv, D, cu_seqlens.data_ptr(), tiles[0].data_ptr(),
                               tiles[1].data_ptr(), ntiles, float(scale), int(causal),
-                              stream_ptr(qkv)), "prefill_attn")
+                              int(persist), stream_ptr(qkv)), "prefill_attn")
     return out
 
 

@@ -2,8 +2,10 @@
 """Time the packed varlen prefill attention kernel on chat-shaped batches.
 
 Prints one JSON line per shape: us per call and effective TFLOP/s (causal
-FLOPs = 4 * sum(n^2)/2 * Hq * D).  Run with DRTC_PREFILL_ATTN_V1=1 in the
-environment to time the previous per-head kernel for an A/B comparison.
+FLOPs = 4 * sum(n^2)/2 * Hq * D) for both launch forms - persistent
+workgroups and one workgroup per (query tile, head group) - timed in
+interleaved rounds in one process, and checks that both forms give bitwise
+identical outputs (same per-tile math and order).
 """
 import json
 import os
@@ -18,6 +20,7 @@ from drtc_amd import ops  # noqa: E402
 
 SHAPES = [  # (name, nseq, mean len, Hq, Hkv, D)
     ("llama8b_smart_reply", 1024, 148, 32, 8, 128),
+    ("llama8b_smart_reply_16k_chunk", 110, 148, 32, 8, 128),
     ("llama8b_summarize", 512, 432, 32, 8, 128),
     ("llama8b_long", 16, 4096, 32, 8, 128),
     ("gemma2b_smart_reply", 1024, 148, 8, 1, 256),
@@ -29,7 +32,6 @@ def main():
     only = sys.argv[sys.argv.index("--only") + 1] if "--only" in sys.argv else None
     dev = torch.device("cuda")
     rng = random.Random(0)
-    variant = "v1" if os.environ.get("DRTC_PREFILL_ATTN_V1") else "v2"
     for name, nseq, mean, Hq, Hkv, D in SHAPES:
         if only and name != only:
             continue
@@ -43,23 +45,35 @@ def main():
         ts, tq = ops.prefill_tiles(cu)
         tiles = (torch.tensor(ts, dtype=torch.int32, device=dev),
                  torch.tensor(tq, dtype=torch.int32, device=dev))
-        out = torch.empty(T, Hq * D, device=dev, dtype=torch.bfloat16)
-        f = lambda: ops.prefill_attention(qkv, cu_d, Hq, Hkv, D, D ** -0.5, True, tiles=tiles,
-                                          cu_host=cu, out=out)
-        for _ in range(3):
-            f()
-        torch.cuda.synchronize()
+        outs = {}
+        times = {}
+        for form in ("persist", "per_item"):
+            outs[form] = torch.empty(T, Hq * D, device=dev, dtype=torch.bfloat16)
+            times[form] = []
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         it = 20
-        e0.record()
-        for _ in range(it):
-            f()
-        e1.record()
-        torch.cuda.synchronize()
-        us = 1000 * e0.elapsed_time(e1) / it
+        for _ in range(5):
+            for form in ("persist", "per_item"):
+                ops.set_prefill_persist(form == "persist")
+                o = outs[form]
+                f = lambda: ops.prefill_attention(qkv, cu_d, Hq, Hkv, D, D ** -0.5, True,
+                                                  tiles=tiles, cu_host=cu, out=o)
+                f()
+                torch.cuda.synchronize()
+                e0.record()
+                for _ in range(it):
+                    f()
+                e1.record()
+                torch.cuda.synchronize()
+                times[form].append(1000 * e0.elapsed_time(e1) / it)
+        ops.set_prefill_persist(None)
+        same = torch.equal(outs["persist"], outs["per_item"])
         flops = 4 * sum(n * (n + 1) / 2 for n in lens) * Hq * D
-        print(json.dumps({"variant": variant, "shape": name, "tokens": T, "us": round(us, 1),
-                          "TFLOPs": round(flops / us / 1e6, 1)}), flush=True)
+        for form, ts in times.items():
+            us = sorted(ts)[len(ts) // 2]
+            print(json.dumps({"form": form, "shape": name, "tokens": T, "us": round(us, 1),
+                              "TFLOPs": round(flops / us / 1e6, 1), "bitwise_equal": same}),
+                  flush=True)
 
 
 if __name__ == "__main__":

@@ -242,7 +242,9 @@ def test_paged_decode_spike(hipk, variant):
 
 @pytest.mark.parametrize("D,Hq,Hkv", [(128, 32, 8), (256, 8, 1), (64, 4, 4), (64, 8, 2), (128, 64, 8), (256, 4, 4)])
 @pytest.mark.parametrize("lens", [[1], [7, 64, 65, 200], [513, 3]])
-def test_prefill_attention(hipk, D, Hq, Hkv, lens):
+@pytest.mark.parametrize("persist", [True, False])
+def test_prefill_attention(hipk, D, Hq, Hkv, lens, persist):
+    ops.set_prefill_persist(persist)
     torch.manual_seed(2)
     T = sum(lens)
     qkv = torch.randn(T, (Hq + 2 * Hkv) * D, device=DEV).to(torch.bfloat16)
@@ -252,8 +254,37 @@ def test_prefill_attention(hipk, D, Hq, Hkv, lens):
     cu_d = torch.tensor(cu, dtype=torch.int32, device=DEV)
     scale = D ** -0.5
     out = ops.prefill_attention(qkv, cu_d, Hq, Hkv, D, scale, True, cu_host=cu)
+    ops.set_prefill_persist(None)
     ref = ops.prefill_attention_ref(qkv, cu, Hq, Hkv, D, scale, True)
     _close(out, ref, 2e-2, 2e-2, "prefill")
+
+
+@pytest.mark.parametrize("D,Hq,Hkv", [(128, 32, 8), (256, 8, 1), (64, 8, 2)])
+def test_prefill_persistent_many_items(hipk, D, Hq, Hkv):
+    """Persistent workgroups at a chat-batch scale (many more (tile, head
+    group) items than resident workgroups, so each loops over several with
+    the next item prefetched): bitwise equal to one workgroup per item, and
+    equal to the reference on a sample of sequences."""
+    g = torch.Generator().manual_seed(6)
+    lens = torch.randint(1, 260, (700,), generator=g).tolist()
+    cu = [0]
+    for n in lens:
+        cu.append(cu[-1] + n)
+    T = cu[-1]
+    qkv = torch.randn(T, (Hq + 2 * Hkv) * D, generator=g).to(torch.bfloat16).to(DEV)
+    cu_d = torch.tensor(cu, dtype=torch.int32, device=DEV)
+    scale = D ** -0.5
+    ops.set_prefill_persist(False)
+    per_item = ops.prefill_attention(qkv, cu_d, Hq, Hkv, D, scale, True, cu_host=cu)
+    ops.set_prefill_persist(True)
+    persist = ops.prefill_attention(qkv, cu_d, Hq, Hkv, D, scale, True, cu_host=cu)
+    ops.set_prefill_persist(None)
+    torch.cuda.synchronize()
+    assert torch.equal(persist, per_item)
+    for s_ in (0, 1, 350, 699):
+        a, b = cu[s_], cu[s_ + 1]
+        ref = ops.prefill_attention_ref(qkv[a:b], [0, b - a], Hq, Hkv, D, scale, True)
+        _close(persist[a:b], ref, 2e-2, 2e-2, f"seq {s_}")
 
 
 def test_prefill_noncausal(hipk):
