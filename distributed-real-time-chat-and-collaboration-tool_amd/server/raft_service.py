@@ -113,7 +113,9 @@ class ChatNode:
     def __init__(self, cfg: NodeConfig):
         self.cfg = cfg
         self.sessions: dict[str, dict] = {}
-        self.revoked: set[str] = set()
+        # node-local fast path for logouts (token -> exp), pruned as tokens
+        # expire; the replicated REVOKE_TOKEN record is authoritative
+        self.revoked: dict[str, int] = {}
         self.local_lock = threading.Lock()
 
         def seed(state):
@@ -302,7 +304,10 @@ class ChatNode:
                                            "exp": int(p.get("exp", 0)), "ts": int(time.time())})
         with self.rt.state_lock:
             self.sessions.pop(request.token, None)
-            self.revoked.add(request.token)
+            now = int(time.time())
+            for t in [t for t, exp in self.revoked.items() if exp < now]:
+                del self.revoked[t]
+            self.revoked[request.token] = int(p.get("exp", 0)) or now + 86400
             u = self.st.users.get(name)
             if u is not None:
                 u["active_token"] = None
