@@ -112,6 +112,48 @@ def _tp_engine_worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
+def _tp_mixed_worker(rank, world, port, q):
+    """TP=2 (and TP=2 x EP=2 for the MoE model) engines driven in lockstep with
+    late arrivals: prompts that arrive while others decode are prefilled in
+    mixed prefill+decode steps (all-reduced partial sums over both row kinds).
+    Both ranks must agree, and the tokens must equal the same TP group run
+    prefill-first (and, for the dense model, a TP=1 engine; under EP a
+    near-tied top-2 routing can flip between TP=1 and TP=2 sums whatever the
+    scheduler)."""
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from drtc_amd.engine import LLMEngine, Request, SamplingParams
+    from drtc_amd.models import TINY_LLAMA, TINY_MIXTRAL, TransformerLM
+    from drtc_amd.parallel.comm import ParallelContext
+
+    res = {}
+    for cfg in (TINY_LLAMA, TINY_MIXTRAL):
+        prompts = [list(range(2 + i, 30 + 5 * i)) for i in range(6)]
+
+        def drive(eng, mixed=True):
+            eng.mixed, eng.mixed_tokens = mixed, 48
+            prm = SamplingParams.greedy(16, ignore_eos=True)
+            reqs = [eng.add_request(Request(list(p), prm)) for p in prompts[:2]]
+            for _ in range(3):
+                eng.step()
+            reqs += [eng.add_request(Request(list(p), prm)) for p in prompts[2:]]
+            while eng.has_work():
+                eng.step()
+            return [r.output_ids for r in reqs], eng.stats["mixed_steps"]
+
+        pc = ParallelContext.from_world(tp=True, ep=cfg.is_moe)
+        model = TransformerLM(cfg, "cpu", pc=pc, seed=8)
+        kw = dict(max_batch=8, max_model_len=256, num_blocks=64, use_graphs=False)
+        tp_out, mixed = drive(LLMEngine(model, **kw))
+        tp_pf, _ = drive(LLMEngine(model, **kw), mixed=False)
+        ref_out, _ = drive(LLMEngine(TransformerLM(cfg, "cpu", seed=8), **kw))
+        res[cfg.name] = {"tp": tp_out, "tp_prefill_first": tp_pf, "ref": ref_out,
+                         "mixed": mixed, "dense": not cfg.is_moe}
+    q.put((rank, res))
+    dist.destroy_process_group()
+
+
 def _run(fn, world=2):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -142,3 +184,14 @@ def test_tp_engines_agree_on_kv_blocks_under_preemption():
     assert res[0]["blocks"] == res[1]["blocks"] == 12
     assert res[0]["preempt"] == res[1]["preempt"] > 0
     assert res[0]["out"] == res[1]["out"]
+
+
+def test_tp_mixed_prefill_decode_steps_match_tp1():
+    res = dict(_run(_tp_mixed_worker))
+    for name in res[0]:
+        a, b = res[0][name], res[1][name]
+        assert a["mixed"] == b["mixed"] >= 2, name
+        assert a["tp"] == b["tp"], name
+        assert a["tp"] == a["tp_prefill_first"], name
+        if a["dense"]:
+            assert a["tp"] == a["ref"], name
