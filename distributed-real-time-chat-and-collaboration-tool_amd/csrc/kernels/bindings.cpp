@@ -127,6 +127,14 @@ PYBIND11_MODULE(_hipk, m) {
   });
   m.def("ar_ipc_close", [](u64 p) { return drtc::ar_ipc_close(P<void>(p)); });
   m.def("ar_error", [](u64 base) { return drtc::ar_error(P<void>(base)); });
+  m.def("midm_gemm", [](u64 y, u64 x, u64 w, u64 res, int M, int N, int K, int ldx, int ldy,
+                        int ldr, int epi, int splits, u64 slab, int64_t slab_bytes, u64 st) {
+    return drtc::launch_midm_gemm(P<void>(y), P<const void>(x), P<const void>(w),
+                                  P<const void>(res), M, N, K, ldx, ldy, ldr, epi, splits,
+                                  P<void>(slab), slab_bytes, S(st));
+  });
+  m.def("midm_slab_bytes",
+        [](int M, int N, int splits) { return drtc::midm_slab_bytes(M, N, splits); });
   m.def("ar_set_epoch", [](u64 base, uint64_t e) { return drtc::ar_set_epoch(P<void>(base), e); });
   m.def("lt_version", &drtc::lt_version);
   m.def("lt_gemm", [](u64 y, u64 x, u64 w, int64_t M, int64_t N, int64_t K, int64_t ldx,

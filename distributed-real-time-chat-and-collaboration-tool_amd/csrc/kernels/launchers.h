@@ -108,6 +108,11 @@ int64_t gemm_workspace_bytes(int64_t M, int64_t N, int splitk);
 int configure_kernels();
 int configure_decode();
 int configure_prefill();
+// medium-M decode GEMM (gemm_midm.hip)
+int64_t midm_slab_bytes(int M, int N, int S);
+int launch_midm_gemm(void* y, const void* x, const void* w, const void* res, int M, int N,
+                     int K, int ldx, int ldy, int ldr, int epi, int S, void* slab,
+                     int64_t slab_bytes, hipStream_t st);
 int configure_moe();
 int configure_gemm();
 

@@ -34,10 +34,13 @@ from ._ext import check, hipk, on_gpu, ptr, stream_ptr
 
 TUNED_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuned")
 _lock = threading.Lock()
-# (M, N, K, ldx) -> (hipBLASLt solution index or -1, skinny-kernel variant or 0)
-_table: dict[tuple[int, int, int, int], tuple[int, int]] | None = None
+# (M, N, K, ldx) -> (hipBLASLt solution index or -1, skinny-kernel variant or 0,
+#                   medium-M kernel K splits or 0)
+_table: dict[tuple[int, int, int, int], tuple[int, int, int]] | None = None
 _ready: set[tuple[int, int, int, int]] = set()               # entries with a native plan
 _enabled = os.environ.get("DRTC_TUNED_GEMM", "1") != "0"
+# medium-M decode kernel (gemm_midm.hip) where the tuning table measured a win
+_midm_enabled = os.environ.get("DRTC_MIDM_GEMM", "1") != "0"
 # decode batches up to this many rows may take the hand-written skinny kernel
 # (csrc/kernels/gemv.hip) instead of the library: the tuning table's choice
 # where the shape was measured, skinny_variant()'s default otherwise; 0
@@ -73,7 +76,8 @@ def _activate() -> dict:
             ver = str(hipk().lt_version())
             for ks, e in load_table().get(ver, {}).items():
                 M, N, K, ldx = (int(v) for v in ks.split(","))
-                tab[(M, N, K, ldx)] = (int(e.get("algo", -1)), int(e.get("skinny", 0)))
+                tab[(M, N, K, ldx)] = (int(e.get("algo", -1)), int(e.get("skinny", 0)),
+                                       int(e.get("midm", 0)) if _midm_enabled else 0)
         _ready.clear()
         _table = tab
     return _table
@@ -161,6 +165,8 @@ def linear(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
                 return skinny_linear(x, w, v)
         elif ent[1] and M <= SKINNY_MAX_M:
             return skinny_linear(x, w, ent[1])
+        elif ent[2] and M <= MIDM_MAX_M:
+            return midm_gemm(x, w, "store", splits=ent[2])
         elif ent[0] >= 0 and _plan(key):
             y = torch.empty((M, N), dtype=x.dtype, device=x.device)
             check(hipk().lt_gemm(y.data_ptr(), x.data_ptr(), w.data_ptr(), M, N, K, x.stride(0),
@@ -360,3 +366,63 @@ def save_entries(entries: dict[str, dict], path: str | None = None) -> str:
 
 
 __all__ = ["linear", "norm_linear", "glu_linear", "skinny_linear", "skinny_ok", "skinny_variant", "skinny_supports", "tune", "save_entries", "load_table", "reset", "set_enabled", "table_path"]
+
+
+# ------------------------------------------------------------------ medium-M decode GEMM
+MIDM_EPI = {"store": 0, "residual": 1, "silu": 2, "gelu_tanh": 3}
+MIDM_MAX_M = 128
+
+
+def midm_splits(M: int, N: int, K: int, target_wgs: int = 512) -> int:
+    """K splits of the medium-M GEMM: the largest S <= 16 with K a multiple of
+    256 S (whole 4-chunk register rings per split) and at most ~2 workgroups
+    per CU."""
+    nb = N // 128
+    ring = 64 * midm_depth(M)
+    best = 1
+    for s in range(1, 17):
+        if K % (ring * s) == 0 and nb * s <= target_wgs:
+            best = s
+    return best
+
+
+def midm_depth(M: int) -> int:
+    """Chunks of 64 k in flight per wave (gemm_midm.hip mid_depth)."""
+    return 4
+
+
+def midm_supported(M: int, N: int, K: int, epi: str = "store") -> bool:
+    return (1 <= M <= MIDM_MAX_M and N % 128 == 0 and K % (64 * midm_depth(M)) == 0
+            and epi in MIDM_EPI
+            and (epi not in ("silu", "gelu_tanh") or (N // 2) % 4 == 0))
+
+
+def midm_gemm(x: torch.Tensor, w: torch.Tensor, epi: str = "store",
+              residual: torch.Tensor | None = None, out: torch.Tensor | None = None,
+              splits: int | None = None) -> torch.Tensor:
+    """Medium-M (17..128 rows) decode GEMM, csrc/kernels/gemm_midm.hip:
+    y = x @ w^T with a store / residual (y = residual + x w^T, in place when
+    out is residual) / SiLU- or GELU-gated [gate | up] epilogue.  W streams
+    once from HBM into registers, x is shared through LDS, K is split over
+    workgroups and the fp32 partials summed by a second small kernel."""
+    M, K = x.shape
+    N = w.shape[0]
+    assert x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and x.is_cuda
+    assert x.stride(1) == 1 and w.is_contiguous() and w.shape[1] == K
+    assert midm_supported(M, N, K, epi), (M, N, K, epi)
+    S = splits or midm_splits(M, N, K)
+    while S > 1 and S * M * N * 4 > WS_SLAB_BYTES:
+        S //= 2
+    NO = N // 2 if epi in ("silu", "gelu_tanh") else N
+    if out is None:
+        out = residual if (epi == "residual" and residual is not None) else \
+            torch.empty((M, NO), dtype=x.dtype, device=x.device)
+    assert out.shape == (M, NO) and out.stride(1) == 1
+    if epi == "residual":
+        assert residual is not None and residual.shape == (M, N) and residual.stride(1) == 1
+    slab = gemm_workspace(x.device)[0]
+    check(hipk().midm_gemm(out.data_ptr(), x.data_ptr(), w.data_ptr(), ptr(residual), M, N, K,
+                           x.stride(0), out.stride(0),
+                           residual.stride(0) if residual is not None else 0, MIDM_EPI[epi], S,
+                           slab.data_ptr(), slab.numel() * 4, stream_ptr(x)), "midm_gemm")
+    return out

@@ -87,3 +87,76 @@ def test_mfma_gemm_rejects_bad_shapes(hipk):
     w = torch.randn(200, 128, device="cuda", dtype=torch.bfloat16)
     with pytest.raises(RuntimeError):
         G.mfma_gemm(x, w)  # N % 256 != 0
+
+
+# ---------------------------------------------------------------- medium-M decode GEMM
+def _rel(out, ref):
+    return (out.float() - ref).abs().max().item() / max(ref.abs().max().item(), 1e-6)
+
+
+@pytest.mark.parametrize("M", [17, 24, 33, 64, 100, 128])
+@pytest.mark.parametrize("N,K,S", [(4096, 4096, 8), (6144, 4096, 4), (2560, 2048, 8),
+                                   (4096, 14336, 7), (4096, 14336, 14), (1024, 1024, 1)])
+def test_midm_store_and_residual(hipk, M, N, K, S):
+    """gemm_midm.hip vs fp32: plain store and residual-add epilogues, ragged M
+    (column groups padded with zero rows), K splits summed by the reduce kernel."""
+    g = torch.Generator(device="cuda").manual_seed(M + N + S)
+    x = torch.randn(M, K, device="cuda", generator=g).to(torch.bfloat16)
+    w = (torch.randn(N, K, device="cuda", generator=g) * 0.02).to(torch.bfloat16)
+    ref = x.float() @ w.float().t()
+    y = G.midm_gemm(x, w, splits=S)
+    assert _rel(y, ref) < 1e-2
+    res = torch.randn(M, N, device="cuda", generator=g).to(torch.bfloat16)
+    ref_r = ref + res.float()
+    out = G.midm_gemm(x, w, "residual", residual=res, splits=S)  # in place
+    assert out.data_ptr() == res.data_ptr() and _rel(out, ref_r) < 1e-2
+
+
+@pytest.mark.parametrize("act", ["silu", "gelu_tanh"])
+@pytest.mark.parametrize("M", [24, 64, 128])
+def test_midm_glu_epilogue(hipk, act, M):
+    I, K = 2048, 2048
+    g = torch.Generator(device="cuda").manual_seed(M)
+    x = torch.randn(M, K, device="cuda", generator=g).to(torch.bfloat16)
+    w = (torch.randn(2 * I, K, device="cuda", generator=g) * 0.02).to(torch.bfloat16)
+    y = (x.float() @ w.float().t()).to(torch.bfloat16).float()
+    gte, up = y[:, :I], y[:, I:]
+    a = F.silu(gte) if act == "silu" else F.gelu(gte, approximate="tanh")
+    out = G.midm_gemm(x, w, act, splits=2)
+    assert out.shape == (M, I) and _rel(out, a * up) < 1e-2
+
+
+def test_midm_strided_input_and_graph_replay(hipk):
+    """x as a row-strided view (decode attention output / norm slices), the
+    kernel pair captured in a hipGraph and replayed bitwise."""
+    g = torch.Generator(device="cuda").manual_seed(3)
+    big = torch.randn(64, 6144, device="cuda", generator=g).to(torch.bfloat16)
+    x = big[:, :4096]
+    w = (torch.randn(4096, 4096, device="cuda", generator=g) * 0.02).to(torch.bfloat16)
+    eager = G.midm_gemm(x, w, splits=8)
+    assert _rel(eager, x.float() @ w.float().t()) < 1e-2
+    out = torch.empty_like(eager)
+    G.gemm_workspace(x.device)
+    G.midm_gemm(x, w, out=out, splits=8)
+    gr = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(gr):
+        G.midm_gemm(x, w, out=out, splits=8)
+    for _ in range(3):
+        out.zero_()
+        gr.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(out, eager)
+
+
+def test_linear_dispatches_midm_from_table(hipk):
+    """ops.linear takes the medium-M kernel for a shape the tuning table marks
+    (Llama-3-8B down at M = 64) and matches the library within bf16 rounding."""
+    G.reset()
+    ent = G._activate().get((64, 4096, 14336, 14336))
+    if ent is None or not ent[2]:
+        pytest.skip("no medium-M entry for this hipBLASLt version")
+    g = torch.Generator(device="cuda").manual_seed(4)
+    x = torch.randn(64, 14336, device="cuda", generator=g).to(torch.bfloat16)
+    w = (torch.randn(4096, 14336, device="cuda", generator=g) * 0.02).to(torch.bfloat16)
+    got = G.linear(x, w)
+    assert _rel(got, x.float() @ w.float().t()) < 1e-2
