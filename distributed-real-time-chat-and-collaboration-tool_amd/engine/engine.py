@@ -110,6 +110,7 @@ class LLMEngine:
         # so a new wave never stalls running decodes for a whole prefill
         # (DRTC_MIXED=0: strict prefill-first)
         self.mixed = os.environ.get("DRTC_MIXED", "1") != "0"
+        self._waiting_tokens = 0  # prompt (+ recompute) tokens queued in self.waiting
         self.mixed_tokens = int(os.environ.get("DRTC_MIXED_TOKENS", "2048"))
 
     # ------------------------------------------------------------ API
@@ -124,6 +125,7 @@ class LLMEngine:
         with self.lock:
             req.state = RequestState.WAITING
             self.waiting.append(req)
+            self._waiting_tokens += n
         return req
 
     def has_work(self) -> bool:
@@ -204,8 +206,7 @@ class LLMEngine:
         efficient large chunks - with the decode rows still riding along -
         instead of throttling admission (closed-loop service load: 309 req/s
         with the fixed budget vs 370 prefill-first)."""
-        waiting = sum(len(r.prompt_ids) + len(r.output_ids) for r in self.waiting)
-        return max(self.mixed_tokens, min(self.prefill_chunk_tokens, waiting // 4))
+        return max(self.mixed_tokens, min(self.prefill_chunk_tokens, self._waiting_tokens // 4))
 
     def _admit(self, budget: int | None = None) -> list[Request]:
         budget = self.max_prefill_tokens if budget is None else budget
@@ -224,10 +225,12 @@ class LLMEngine:
             if not self.alloc.can_allocate(need + (self.watermark if busy else 0)):
                 if not busy and need > self.alloc.num_blocks - 1:
                     self.waiting.popleft()
+                    self._waiting_tokens -= n
                     r.mark_finished("error: request exceeds KV-cache capacity")
                     continue
                 break
             self.waiting.popleft()
+            self._waiting_tokens -= n
             r.blocks = list(self.alloc.allocate(need))
             batch.append(r)
             tokens += n
@@ -500,6 +503,7 @@ class LLMEngine:
         r.num_preemptions += 1
         self.stats["preemptions"] += 1
         self.waiting.appendleft(r)
+        self._waiting_tokens += r.num_tokens
 
     def _could_admit(self) -> bool:
         return bool(self.waiting) and len(self.running) < self.max_batch and not (

@@ -187,6 +187,11 @@ class ChatNode:
     def _token(self, user_id: str, username: str) -> str:
         payload = {"user_id": user_id, "username": username,
                    "exp": _dt.datetime.now(_dt.timezone.utc) + _dt.timedelta(hours=self.cfg.token_ttl_hours)}
+        if self.cfg.token_mode != "reference":
+            # a random token id: logins within the same second (same exp) must not mint
+            # the token a logout just revoked (replicated revocation is by token hash);
+            # an extra claim, so reference verifiers (PyJWT) still accept it
+            payload["jti"] = uuid.uuid4().hex
         return auth.jwt_encode(payload, self.cfg.jwt_secret)
 
     def _verify(self, token: str) -> dict | None:

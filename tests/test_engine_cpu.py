@@ -56,6 +56,7 @@ def test_engine_preemption_and_recompute():
                                                                  top_k=20, top_p=0.9, ignore_eos=True))
     assert all(len(r.output_ids) == 40 for r in reqs)
     assert eng.stats["preemptions"] > 0 and eng.alloc.num_used == 0
+    assert eng._waiting_tokens == 0 and not eng.waiting  # incremental backlog count
 
 
 def test_engine_stop_conditions():

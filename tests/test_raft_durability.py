@@ -156,7 +156,8 @@ def test_logout_revocation_is_replicated_and_survives_failover(cluster):
     cluster.kill(L)
     L2 = cluster.leader()
     assert not cluster.stub(L2).GetChannels(raft_pb.GetChannelsRequest(token=tok)).success
-    tok2 = cluster.login(L2)  # a fresh login still works
+    tok2 = cluster.login(L2)  # a fresh login still works, even within the same second
+    assert tok2 != tok  # random jti: never the revoked token again
     assert cluster.stub(L2).GetChannels(raft_pb.GetChannelsRequest(token=tok2)).success
 
 
