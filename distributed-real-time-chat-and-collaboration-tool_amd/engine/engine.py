@@ -111,6 +111,7 @@ class LLMEngine:
         # (DRTC_MIXED=0: strict prefill-first)
         self.mixed = os.environ.get("DRTC_MIXED", "1") != "0"
         self._waiting_tokens = 0  # prompt (+ recompute) tokens queued in self.waiting
+        self._aborts: list[Request] = []  # abort() requests, applied at the next step
         self.mixed_tokens = int(os.environ.get("DRTC_MIXED_TOKENS", "2048"))
 
     # ------------------------------------------------------------ API
@@ -129,7 +130,46 @@ class LLMEngine:
         return req
 
     def has_work(self) -> bool:
-        return bool(self.running or self.waiting or self._inflight)
+        return bool(self.running or self.waiting or self._inflight or self._aborts)
+
+    def abort(self, req: Request) -> None:
+        """Cancel a request (its caller gave up, e.g. an RPC deadline): it is
+        dropped from the queue or finished with reason "abort" at the next
+        step boundary, freeing its batch slot and KV blocks.  Thread-safe;
+        a no-op for a request that already finished."""
+        with self.lock:
+            if req.state != RequestState.FINISHED:
+                self._aborts.append(req)
+
+    def _apply_aborts(self) -> list[Request]:
+        with self.lock:
+            aborts, self._aborts = self._aborts, []
+            done = []
+            for r in aborts:
+                if r.state == RequestState.WAITING:
+                    try:
+                        self.waiting.remove(r)
+                    except ValueError:
+                        continue
+                    self._waiting_tokens -= r.num_tokens
+                    r.mark_finished("abort")
+                    done.append(r)
+        live = [r for r in aborts if r.state == RequestState.RUNNING]
+        if live:
+            # a launched step still holds their slots: read it first
+            if self._inflight is not None:
+                done += self._process_inflight()
+            rel = sorted((r for r in live if r.state == RequestState.RUNNING and r.slot >= 0),
+                         key=lambda r: -r.slot)
+            with self.lock:
+                for r in rel:
+                    self._release_slot(r)
+                    r.mark_finished("abort")
+                    done.append(r)
+            if rel:
+                self._pressure = False
+        self.stats["aborted"] += len([r for r in done if r.finish_reason == "abort"])
+        return done
 
     def warmup(self, capture: bool = True, up_to: int | None = None) -> None:
         """Capture decode graphs up front (zeroed staging: no cache reads/writes)."""
@@ -146,6 +186,10 @@ class LLMEngine:
 
     def step(self) -> list[Request]:
         """One scheduler iteration. Returns requests finished in it."""
+        if self._aborts:
+            done = self._apply_aborts()
+            self._record(done)
+            return done
         if self.mixed and (self.running or self._inflight is not None) and self._could_admit():
             done = self._process_inflight() if self._inflight is not None else []
             with self.lock:

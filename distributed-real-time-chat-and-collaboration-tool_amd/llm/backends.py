@@ -82,6 +82,8 @@ class EngineBackend:
         for r in reqs:
             left = None if deadline is None else max(0.0, deadline - time.monotonic())
             if not r.wait(left):
+                for q in reqs:  # the caller gives up: free their slots and KV blocks
+                    self.engine.abort(q)
                 raise GenerationError("generation timed out")
             if r.finish_reason.startswith("error"):
                 raise GenerationError(r.finish_reason)
@@ -150,6 +152,11 @@ def _worker_main(rank: int, device: str, model_name: str, engine_kw: dict, inq, 
         msg = inq.get()
         if msg is None:
             break
+        if msg[0] == "abort":  # the caller gave up: free the slot / KV blocks
+            r = pending.get(msg[1])
+            if r is not None:
+                eng.abort(r)
+            continue
         rid, ids, prm = msg
         r = Request(ids, prm, request_id=rid)
         pending[rid] = r
@@ -307,7 +314,21 @@ class WorkerPool:
 
     def release(self, rid):
         with self._lock:
-            self.futures.pop(rid, None)
+            f = self.futures.pop(rid, None)
+            if f is not None and not f[1]:  # released before its result: not in flight any more
+                self.load[f[2]] -= 1
+
+    def abort(self, rid):
+        """Cancel an outstanding request on its replica, then release it."""
+        with self._lock:
+            f = self.futures.get(rid)
+            w = f[2] if f is not None and not f[1] else None
+        if w is not None and self.inqs[w] is not None:
+            try:
+                self.inqs[w].put(("abort", rid))
+            except (OSError, ValueError):
+                pass
+        self.release(rid)
 
     def health(self) -> list[dict]:
         with self._lock:
@@ -359,6 +380,8 @@ class ReplicaRouter:
                     rid, ev, slot = job[2]
                     left = None if deadline is None else max(0.0, deadline - time.monotonic())
                     if not ev.wait(left):
+                        for j in jobs:  # free the replicas' slots and KV blocks
+                            self.pool.abort(j[2][0])
                         raise GenerationError("generation timed out")
                     ids, reason = slot[0]
                     if reason.startswith(WorkerPool.LOST) and job[3] < self.max_redispatch:

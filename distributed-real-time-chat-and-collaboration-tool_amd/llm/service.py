@@ -46,9 +46,16 @@ class LLMServicer:
         self.answer_retries = max(1, answer_retries)
         self.answer_backoff = answer_backoff
 
-    def _gen(self, feature: str, prompt: str, params: SamplingParams) -> str:
+    def _gen(self, feature: str, prompt: str, params: SamplingParams, context=None) -> str:
+        """Generate under the service timeout, shortened to the caller's RPC
+        deadline: when the caller gives up, the backend aborts the request
+        (its batch slot and KV blocks are freed) instead of finishing it."""
         t0 = time.perf_counter()
-        text = self.backend.generate([prompt], [params], timeout=self.timeout)[0]
+        timeout = self.timeout
+        left = context.time_remaining() if context is not None else None
+        if left is not None:
+            timeout = min(timeout, max(0.05, left))
+        text = self.backend.generate([prompt], [params], timeout=timeout)[0]
         METRICS.observe(f"llm.{feature}.latency_s", time.perf_counter() - t0)
         METRICS.inc(f"llm.{feature}.requests")
         return text
@@ -62,7 +69,7 @@ class LLMServicer:
         empty = False
         for attempt in range(self.answer_retries):
             try:
-                answer = P.parse_answer(self._gen("answer", prompt, self.p.answer))
+                answer = P.parse_answer(self._gen("answer", prompt, self.p.answer, context))
                 if answer:
                     return llm_pb.LLMResponse(request_id=request.request_id, answer=answer,
                                               confidence=0.95)
@@ -89,7 +96,7 @@ class LLMServicer:
         if not msgs:
             return llm_pb.SmartReplyResponse(request_id=request.request_id, suggestions=P.SMART_REPLY_EMPTY)
         try:
-            text = self._gen("smart_reply", P.smart_reply_prompt(msgs), self.p.smart)
+            text = self._gen("smart_reply", P.smart_reply_prompt(msgs), self.p.smart, context)
             return llm_pb.SmartReplyResponse(request_id=request.request_id,
                                              suggestions=P.parse_smart_replies(text))
         except Exception as e:
@@ -104,7 +111,8 @@ class LLMServicer:
             return llm_pb.SummarizeResponse(request_id=request.request_id,
                                             summary="No messages to summarize", key_points=[])
         try:
-            text = self._gen("summarize", P.summarize_prompt(msgs, max_len), self.p.summary)
+            text = self._gen("summarize", P.summarize_prompt(msgs, max_len), self.p.summary,
+                             context)
             summary, points = P.parse_summary(text, msgs, max_len)
             return llm_pb.SummarizeResponse(request_id=request.request_id, summary=summary,
                                             key_points=points)
@@ -116,7 +124,8 @@ class LLMServicer:
     def GetContextSuggestions(self, request, context):
         msgs = list(request.context)
         try:
-            text = self._gen("suggest", P.suggestions_prompt(msgs, request.current_input), self.p.suggest)
+            text = self._gen("suggest", P.suggestions_prompt(msgs, request.current_input),
+                             self.p.suggest, context)
             s, t = P.parse_suggestions(text, request.current_input)
             return llm_pb.SuggestionsResponse(request_id=request.request_id, suggestions=s, topics=t)
         except Exception as e:

@@ -76,6 +76,7 @@ def tp_worker(rank: int, world: int, port: int, model_name: str, engine_kw: dict
 def _serve_loop(rank, eng, pc, cpu, inq, outq):
     import torch.distributed as dist
 
+    live: dict[str, Request] = {}  # request id -> Request, for aborts (same on every rank)
     while True:
         new = []
         if rank == 0:
@@ -91,13 +92,21 @@ def _serve_loop(rank, eng, pc, cpu, inq, outq):
         new = box[0]
         stop = any(m is None for m in new)
         for m in new:
-            if m is not None:
-                rid, ids, prm = m
-                eng.add_request(Request(ids, prm, request_id=rid))
+            if m is None:
+                continue
+            if m[0] == "abort":  # broadcast like a new request: every rank aborts at this step
+                r = live.get(m[1])
+                if r is not None:
+                    eng.abort(r)
+                continue
+            rid, ids, prm = m
+            live[rid] = eng.add_request(Request(ids, prm, request_id=rid))
         if stop:
             break
         if eng.has_work():
             done = eng.step()
+            for r in done:
+                live.pop(r.request_id, None)
             # a flag wait of the custom all-reduce that timed out means a peer
             # missed a call and this step summed stale staging: fail the whole
             # group (the supervisor starts fresh processes) instead of
@@ -155,7 +164,7 @@ class TPEngineGroup:
     def generate(self, prompts, params, timeout=None):
         if isinstance(params, SamplingParams):
             params = [params] * len(prompts)
-        hs = []
+        hs, rids = [], []
         for p, prm in zip(prompts, params):
             ids = fit_prompt(self.tok, p, self.max_model_len - prm.max_new_tokens - 1)
             rid = f"tp-{next(self._ids)}"
@@ -166,11 +175,18 @@ class TPEngineGroup:
                 self._futs[rid] = (ev, slot)
             self.inq.put((rid, ids, prm))
             hs.append((ev, slot))
+            rids.append((rid, ev, slot))
         deadline = None if timeout is None else time.monotonic() + timeout
         out = []
         for ev, slot in hs:
             left = None if deadline is None else max(0.0, deadline - time.monotonic())
             if not ev.wait(left):
+                with self._lock:  # the caller gives up: abort what is still running
+                    pending = [rid for rid, _, _ in rids if rid in self._futs]
+                    for rid in pending:
+                        self._futs.pop(rid, None)
+                for rid in pending:
+                    self.inq.put(("abort", rid))
                 raise TimeoutError("generation timed out")
             ids, reason = slot[0]
             if reason.startswith("error"):

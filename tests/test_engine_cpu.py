@@ -299,3 +299,58 @@ def test_moe_sorted_gemm_matches_reference():
         ref = moe_ops.fused_moe_ref(x, lg, wgu[e_off:e_off + n], wdn[e_off:e_off + n], k,
                                     e_off=e_off)
         assert (out.float() - ref.float()).abs().max() < 0.01
+
+
+def test_engine_abort_waiting_running_and_inflight():
+    """abort(): a queued request leaves the queue, running ones (one of them in
+    a pipelined in-flight step) finish with reason "abort" and free their slot
+    and KV blocks; the other requests produce exactly the tokens they produce
+    without the aborts."""
+    from drtc_amd.engine import Request
+
+    m = TransformerLM(TINY_LLAMA, "cpu", seed=6)
+    prompts = [list(range(1, 12 + 5 * i)) for i in range(6)]
+
+    def run(abort: bool):
+        eng = LLMEngine(m, max_batch=4, max_model_len=256, num_blocks=64, use_graphs=False)
+        prm = SamplingParams.greedy(24, ignore_eos=True)
+        reqs = [eng.add_request(Request(list(p), prm)) for p in prompts]  # 2 wait (max_batch 4)
+        for _ in range(4):
+            eng.step()
+        if abort:
+            assert eng._inflight is not None and len(eng.waiting) == 2
+            for i in (1, 3, 5):  # two running, one waiting
+                eng.abort(reqs[i])
+        while eng.has_work():
+            eng.step()
+        assert eng.alloc.num_used == 0 and not eng.running and eng._waiting_tokens == 0
+        return reqs, eng.stats
+
+    base, _ = run(False)
+    got, st = run(True)
+    assert st["aborted"] == 3
+    for i in (1, 3, 5):
+        assert got[i].finish_reason == "abort" and len(got[i].output_ids) < 24
+    for i in (0, 2, 4):
+        assert got[i].output_ids == base[i].output_ids
+    assert len(got[5].output_ids) == 0  # aborted while queued
+
+
+def test_backend_timeout_aborts_request():
+    import time
+
+    from drtc_amd.llm.backends import EngineBackend, GenerationError
+
+    m = TransformerLM(TINY_LLAMA, "cpu", seed=6)
+    eng = LLMEngine(m, max_batch=4, max_model_len=1024, num_blocks=64, use_graphs=False)
+    be = EngineBackend(eng, ChatTokenizer(TINY_LLAMA.vocab_size))
+    try:
+        with pytest.raises(GenerationError):
+            be.generate(["hello " * 20], SamplingParams.greedy(900, ignore_eos=True), timeout=0.05)
+        deadline = time.time() + 20
+        while (eng.running or eng.waiting) and time.time() < deadline:
+            time.sleep(0.01)
+        assert not eng.running and not eng.waiting and eng.stats["aborted"] == 1
+        assert eng.alloc.num_used == 0
+    finally:
+        be.close()

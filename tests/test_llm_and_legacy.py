@@ -163,6 +163,13 @@ if __name__ == '__main__':
     kw = dict(max_batch=8, max_model_len=512, num_blocks=64, use_graphs=False)
     g = TPEngineGroup('tiny-llama', 2, kw, tok)
     a = g.generate(['hello world', 'lunch tomorrow?'], SamplingParams.greedy(8, ignore_eos=True), timeout=120)
+    try:  # a caller that gives up: the abort is broadcast and applied by both ranks
+        g.generate(['hello ' * 30], SamplingParams.greedy(400, ignore_eos=True), timeout=0.3)
+        raise AssertionError('expected a timeout')
+    except TimeoutError:
+        pass
+    c = g.generate(['hello world'], SamplingParams.greedy(8, ignore_eos=True), timeout=120)
+    assert c[0] == a[0], (c, a)  # the group is still in lockstep and serving
     g.close()
     eng = LLMEngine(TransformerLM(TINY_LLAMA, 'cpu', seed=1234), seed=0, **kw)
     b = [tok.decode(r.output_ids) for r in eng.generate([tok.encode('hello world'), tok.encode('lunch tomorrow?')],
@@ -326,3 +333,31 @@ os._exit(0)
                 return
         time.sleep(0.2)
     raise AssertionError(f"engine worker {pid} outlived its parent")
+
+
+def test_pool_router_timeout_aborts_on_the_replica():
+    """A request whose caller times out is aborted on its replica (the engine
+    frees its slot and KV blocks) and the replica's load count comes back to
+    zero (it used to leak one per released-before-done request)."""
+    from drtc_amd.engine import SamplingParams
+    from drtc_amd.llm.backends import GenerationError, ReplicaRouter, WorkerPool
+
+    kw = dict(max_batch=4, max_model_len=1024, num_blocks=64, use_graphs=False)
+    pool = WorkerPool("tiny-llama", ["cpu"], kw, hb_interval=0.1)
+    try:
+        router = ReplicaRouter(pool, ChatTokenizer(TINY_LLAMA.vocab_size), 1024)
+        with pytest.raises(GenerationError):
+            router.generate(["hello " * 20], SamplingParams.greedy(900, ignore_eos=True),
+                            timeout=0.2)
+        assert pool.load == [0]
+        deadline = time.time() + 30
+        while time.time() < deadline:
+            h = pool.health()[0]
+            if h.get("aborted", 0) == 1 and h.get("running", 1) == 0:
+                break
+            time.sleep(0.1)
+        assert h.get("aborted") == 1 and h.get("running") == 0, h
+        out = router.generate(["hi"], SamplingParams.greedy(3, ignore_eos=True), timeout=60)
+        assert len(out) == 1 and pool.load == [0]
+    finally:
+        pool.close()
