@@ -149,3 +149,32 @@ def test_prefill_residual_in_gemm_epilogue(hipk, cfg, monkeypatch):
         scale = max(1.0, b.float().abs().max().item())
         assert (a.float() - b.float()).abs().max().item() < 0.05 * scale
         assert (a.float() - u.float()).abs().max().item() < 0.05 * scale
+
+
+def test_abort_with_graph_decode(hipk):
+    """abort() on the GPU path: hipGraph decode with a pipelined in-flight step;
+    survivors' tokens are unchanged, KV blocks all returned."""
+    from drtc_amd.engine import Request
+
+    prompts = [list(range(1, 12 + 5 * i)) for i in range(6)]
+
+    def run(abort):
+        m = TransformerLM(TINY_LLAMA, "cuda", seed=6)
+        eng = LLMEngine(m, max_batch=4, max_model_len=512, num_blocks=128, use_graphs=True)
+        prm = SamplingParams.greedy(24, ignore_eos=True)
+        reqs = [eng.add_request(Request(list(p), prm)) for p in prompts]
+        for _ in range(4):
+            eng.step()
+        if abort:
+            for i in (1, 3, 5):
+                eng.abort(reqs[i])
+        while eng.has_work():
+            eng.step()
+        assert eng.alloc.num_used == 0 and not eng.running
+        return reqs, eng.stats
+
+    base, _ = run(False)
+    got, st = run(True)
+    assert st["aborted"] == 3
+    for i in (0, 2, 4):
+        assert got[i].output_ids == base[i].output_ids
