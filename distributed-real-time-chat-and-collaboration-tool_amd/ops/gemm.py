@@ -71,7 +71,7 @@ def _activate() -> dict:
     with _lock:
         if _table is not None:
             return _table
-        tab: dict[tuple[int, int, int, int], tuple[int, int]] = {}
+        tab: dict[tuple[int, int, int, int], tuple[int, int, int]] = {}
         if _enabled and torch.cuda.is_available():
             ver = str(hipk().lt_version())
             for ks, e in load_table().get(ver, {}).items():
@@ -365,7 +365,9 @@ def save_entries(entries: dict[str, dict], path: str | None = None) -> str:
     return path
 
 
-__all__ = ["linear", "norm_linear", "glu_linear", "skinny_linear", "skinny_ok", "skinny_variant", "skinny_supports", "tune", "save_entries", "load_table", "reset", "set_enabled", "table_path"]
+__all__ = ["linear", "norm_linear", "glu_linear", "skinny_linear", "skinny_ok", "skinny_variant",
+           "skinny_supports", "mfma_gemm", "midm_gemm", "midm_supported", "tune", "save_entries",
+           "load_table", "reset", "set_enabled", "table_path"]
 
 
 # ------------------------------------------------------------------ medium-M decode GEMM
