@@ -460,7 +460,7 @@ DRTC_DEVICE void load_kv_block_n(KVRegs<D>& r, const bf16_t* kb, const bf16_t* v
 // partial last block are not fetched (load_kv_block_n).  Math per block is
 // variant 2's; per-item outputs / partials likewise.
 template <int D>
-__global__ __launch_bounds__(256, 2) void paged_decode_persist_kernel(
+__global__ __launch_bounds__(256, D >= 256 ? 1 : 2) void paged_decode_persist_kernel(
     bf16_t* __restrict__ out, float* __restrict__ part_o,
     float* __restrict__ part_ml, const bf16_t* __restrict__ q, int q_stride,
     const bf16_t* __restrict__ k_cache, const bf16_t* __restrict__ v_cache,
@@ -665,9 +665,6 @@ int launch_paged_decode(void* out, float* part_o, float* part_ml, int* counters,
   if (Hkv <= 0 || Hq % Hkv != 0 || Hq / Hkv > 16) return -1;
   if (max_parts > 1 && (!part_o || !part_ml)) return -2;
   const float sl2 = scale * kLog2e;
-  // variant 3 holds two K/V blocks + two Q fragments in registers: at D = 256
-  // that spills, so head_dim 256 (Gemma-2B) runs variant 1
-  if (variant == 3 && D > 128) variant = 1;
   if (variant == 3) {
     static int n_cu = 0;
     if (n_cu == 0) {
@@ -677,14 +674,20 @@ int launch_paged_decode(void* out, float* part_o, float* part_ml, int* counters,
           n_cu <= 0)
         n_cu = 256;
     }
+    // two K/V blocks + two Q fragments per wave: at D = 256 that is ~400 VGPRs,
+    // so one workgroup per CU (one wave per SIMD) instead of two
     const int items = B * Hkv * max_parts;
-    const dim3 pgrid(std::max(1, std::min((items + 3) / 4, 2 * n_cu))), pblock(256);
+    const int per_cu = D >= 256 ? 1 : 2;
+    const dim3 pgrid(std::max(1, std::min((items + 3) / 4, per_cu * n_cu))), pblock(256);
     switch (D) {
       case 64:
         hipLaunchKernelGGL(paged_decode_persist_kernel<64>, pgrid, pblock, 0, st, (bf16_t*)out, part_o, part_ml, (const bf16_t*)q, q_stride, (const bf16_t*)k_cache, (const bf16_t*)v_cache, block_tables, bt_stride, context_lens, B, Hq, Hkv, sl2, max_parts, blocks_per_part);
         break;
       case 128:
         hipLaunchKernelGGL(paged_decode_persist_kernel<128>, pgrid, pblock, 0, st, (bf16_t*)out, part_o, part_ml, (const bf16_t*)q, q_stride, (const bf16_t*)k_cache, (const bf16_t*)v_cache, block_tables, bt_stride, context_lens, B, Hq, Hkv, sl2, max_parts, blocks_per_part);
+        break;
+      case 256:
+        hipLaunchKernelGGL(paged_decode_persist_kernel<256>, pgrid, pblock, 0, st, (bf16_t*)out, part_o, part_ml, (const bf16_t*)q, q_stride, (const bf16_t*)k_cache, (const bf16_t*)v_cache, block_tables, bt_stride, context_lens, B, Hq, Hkv, sl2, max_parts, blocks_per_part);
         break;
       default:
         return -1;

@@ -125,12 +125,19 @@ def decode_variant(batch: int, Hkv: int, D: int, max_blocks: int) -> int:
     kv heads: 141 vs 150 us); 2 (wave per item) when the context must be
     split over partitions to fill the chip (B 8 x 4k tokens: 30 vs 53 us for
     variant 1, whose in-kernel merge pays an agent-scope fence per workgroup
-    across the 8 XCD L2s); 1 otherwise (B 256 x ~1k tokens: 196 vs 206 us)."""
+    across the 8 XCD L2s); 1 otherwise (B 256 x ~1k tokens: 196 vs 206 us).
+    r2l (profiles/r2l_decode_geometries.md): from 2048 items v3 also wins at
+    chat lengths (Mixtral / 70B heads at B 256: 38.4 vs 40.1 / 38.9 vs 41.2 us);
+    at D = 256 (Gemma-2B, one kv head) v2 wins from 1024 items (B 1024: 34.2 vs
+    49.5 us; v3 holds ~400 registers there and spills)."""
     if DECODE_VARIANT:
         return DECODE_VARIANT
-    if batch * Hkv >= 4096 and D <= 128:
+    items = batch * Hkv
+    if D <= 128 and items >= 2048:
         return 3
-    if batch * Hkv < 256 and max_blocks > 8:
+    if D > 128 and items >= 1024:
+        return 2
+    if items < 256 and max_blocks > 8:
         return 2
     return 1
 # variant 1 merges split-K partitions inside the attention kernel (last

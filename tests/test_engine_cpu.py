@@ -354,3 +354,23 @@ def test_backend_timeout_aborts_request():
         assert eng.alloc.num_used == 0
     finally:
         be.close()
+
+
+def test_decode_kernel_choice_per_geometry():
+    """The measured decode-attention variant table (profiles/r2g, r2l) at the
+    engine's decode buckets: static per graph, chosen from (batch, kv heads, D)
+    with the block-table width the runner passes (max_model_len / 32)."""
+    from drtc_amd.ops.attention import decode_partitioning, decode_variant
+
+    mb = 2048 // ops.KV_BLOCK
+    assert decode_variant(1024, 8, 128, mb) == 3      # Llama-3-8B headline
+    assert decode_variant(256, 8, 128, mb) == 3       # Mixtral / Llama-3-70B at batch 256
+    assert decode_variant(1024, 1, 256, mb) == 2      # Gemma-2B headline batch
+    assert decode_variant(256, 1, 256, mb) == 1
+    assert decode_variant(16, 8, 128, mb) == 2        # small batch: context split over waves
+    assert decode_variant(64, 8, 128, 4) == 1
+    # one partition whenever the batch fills the chip; split contexts never on variant 1
+    for B, hkv, D in ((1024, 8, 128), (256, 8, 128), (1024, 1, 256)):
+        assert decode_partitioning(B, hkv, mb, D=D) == (mb, 1)
+    bpp, parts = decode_partitioning(8, 8, mb)
+    assert parts > 1 and decode_variant(8, 8, 128, mb) == 2
