@@ -110,14 +110,22 @@ def open_loop(args, eng, make_prompts, params, rank, world, tp, device, cfg) -> 
     tpot = [(r.finish_time - r.first_token_time) / (len(r.output_ids) - 1)
             for r in reqs if len(r.output_ids) > 1]
     gen = sum(len(r.output_ids) for r in reqs)
+    # service rate in the steady part of the arrival window (30-90 % of it): the
+    # whole-run rate above also counts the ramp-up and the drain after the last
+    # arrival, so under overload it understates what the engine sustains
+    w0, w1 = t0 + 0.3 * arr[-1], t0 + 0.9 * arr[-1]
+    fin = [r for r in reqs if w0 <= r.finish_time < w1]
     st = torch.tensor([elapsed, gen, _pct(lat, .5), _pct(lat, .99), _pct(ttft, .5),
                        _pct(ttft, .99), _pct(tpot, .5), _pct(tpot, .99)], dtype=torch.float64,
                       device=device)
+    steady = torch.tensor([len(fin) / (w1 - w0), sum(len(r.output_ids) for r in fin) / (w1 - w0)],
+                          dtype=torch.float64, device=device)
     if world > 1:
         g = st[1].clone()
         dist.all_reduce(st, op=dist.ReduceOp.MAX)
         if tp == 1:
             dist.all_reduce(g)
+            dist.all_reduce(steady)
         st[1] = g
     el, gen = float(st[0]), float(st[1])
     if rank == 0:
@@ -129,6 +137,8 @@ def open_loop(args, eng, make_prompts, params, rank, world, tp, device, cfg) -> 
             "n_gpus": world, "requests_per_replica": n_req,
             "achieved_req_per_s": round(n_req * (world // tp) / el, 1),
             "gen_tokens_per_s": round(gen / el, 1),
+            "steady_req_per_s": round(float(steady[0]), 1),
+            "steady_gen_tokens_per_s": round(float(steady[1]), 1),
             "p50_latency_ms": ms[0], "p99_latency_ms": ms[1],
             "p50_ttft_ms": ms[2], "p99_ttft_ms": ms[3],
             "p50_tpot_ms": ms[4], "p99_tpot_ms": ms[5],

@@ -14,7 +14,7 @@ import csv, sys
 rows = []
 with open(sys.argv[1]) as f:
     for r in csv.DictReader(f):
-        rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"][:60]))
+        rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"][:160]))
 rows.sort()
 # the open-loop window: last 60 % of the trace (after warm-up / graph capture)
 t0 = rows[int(len(rows) * 0.4)][0]
@@ -31,6 +31,18 @@ for g, a, b in big:
     agg[k] = agg.get(k, 0) + g
 for k, v in sorted(agg.items(), key=lambda kv: -kv[1])[:10]:
     print(f"  {v / 1e3:8.1f} ms  {k}")
+# kernel-time breakdown of the window by kernel (GEMMs grouped by macro tile)
+import re
+tot = {}
+cnt = {}
+for a, b, n in rows:
+    m = re.search(r"MT\d+x\d+x\d+", n)
+    k = ("GEMM " + m.group(0)) if m else n
+    tot[k] = tot.get(k, 0) + (b - a)
+    cnt[k] = cnt.get(k, 0) + 1
+print("kernel time in the window:")
+for k, v in sorted(tot.items(), key=lambda kv: -kv[1])[:25]:
+    print(f"  {v / 1e6:8.1f} ms {100 * v / 1e6 / busy:5.1f} %  {cnt[k]:6d}x  {k}")
 PY
 cat gpurun_out/ol_idle.txt; tail -2 gpurun_out/prof_ol.log | cut -c1-400
 rm -rf gpurun_out/prof_ol

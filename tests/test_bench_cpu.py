@@ -69,6 +69,7 @@ def test_bench_open_loop_poisson():
         assert r[k] > 0, k
     assert r["p99_latency_ms"] >= r["p50_latency_ms"]
     assert r["engine_stats"]["mixed_steps"] > 0
+    assert r["steady_req_per_s"] >= 0 and r["steady_gen_tokens_per_s"] >= 0
 
 
 def test_service_bench_open_loop_scripted():

@@ -374,3 +374,72 @@ def test_decode_kernel_choice_per_geometry():
         assert decode_partitioning(B, hkv, mb, D=D) == (mb, 1)
     bpp, parts = decode_partitioning(8, 8, mb)
     assert parts > 1 and decode_variant(8, 8, 128, mb) == 2
+
+
+@pytest.mark.parametrize("mixed", [True, False], ids=["mixed", "prefill_first"])
+def test_slot_bound_admission_in_groups(mixed):
+    """With more queued requests than free batch slots, admission waits for
+    ``admit_group`` free slots and takes them in one step (the in-between
+    steps are pure decodes); tokens equal the trickle-admission engine's."""
+    from drtc_amd.engine import Request
+
+    m = TransformerLM(TINY_LLAMA, "cpu", seed=7)
+    prompts = [list(range(1, 8 + 3 * i)) for i in range(20)]
+
+    def run(group: int):
+        eng = LLMEngine(m, max_batch=8, max_model_len=256, num_blocks=96, use_graphs=False)
+        eng.mixed, eng.mixed_tokens, eng.admit_group = mixed, 4096, group
+        sizes = []
+        real = eng._admit
+
+        def spy(*a, **k):
+            b = real(*a, **k)
+            if b:
+                sizes.append((len(b), len(eng.running), len(eng.waiting)))
+            return b
+
+        eng._admit = spy
+        reqs = [eng.add_request(Request(list(p), SamplingParams.greedy(3 + (5 * i) % 11,
+                                                                       ignore_eos=True)))
+                for i, p in enumerate(prompts)]
+        while eng.has_work():
+            eng.step()
+        assert eng.alloc.num_used == 0 and not eng.running
+        return [r.output_ids for r in reqs], sizes
+
+    ref, trickle = run(1)
+    got, grouped = run(4)
+    assert got == ref
+    # first admission fills the batch; later ones are groups of >= 4 (or the whole queue)
+    assert grouped[0][0] == 8
+    for n, running, waiting in grouped[1:]:
+        assert n >= 4 or waiting == 0, grouped
+    assert len(grouped) < len(trickle)
+
+
+def test_pipelined_decode_continues_across_staggered_finishes():
+    """Requests finishing one or two per step (continuous traffic) no longer
+    drain the decode pipeline each time: they ride along as zombies (row
+    computed, token discarded) up to ``admit_group``; tokens equal the
+    synchronous engine's and every KV block comes back."""
+    from drtc_amd.engine import Request
+
+    m = TransformerLM(TINY_LLAMA, "cpu", seed=3)
+    prompts = [list(range(2, 9 + 2 * i)) for i in range(10)]
+
+    def run(pipeline: bool):
+        eng = LLMEngine(m, max_batch=16, max_model_len=256, num_blocks=96, use_graphs=False)
+        eng.pipeline, eng.admit_group = pipeline, 4
+        reqs = [eng.add_request(Request(list(p), SamplingParams.greedy(6 + 2 * i, ignore_eos=True)))
+                for i, p in enumerate(prompts)]
+        while eng.has_work():
+            eng.step()
+        assert eng.alloc.num_used == 0 and not eng.running and not eng._zombies
+        return [r.output_ids for r in reqs], eng.stats
+
+    sync, st_sync = run(False)
+    pipe, st_pipe = run(True)
+    assert pipe == sync
+    assert all(len(o) == 6 + 2 * i for i, o in enumerate(pipe))
+    # a finish every other step: most decode steps stay pipelined
+    assert st_pipe["decode_steps_pipelined"] >= st_pipe["decode_steps"] // 2, st_pipe
