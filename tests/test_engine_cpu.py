@@ -348,7 +348,9 @@ def test_backend_timeout_aborts_request():
         with pytest.raises(GenerationError):
             be.generate(["hello " * 20], SamplingParams.greedy(900, ignore_eos=True), timeout=0.05)
         deadline = time.time() + 20
-        while (eng.running or eng.waiting) and time.time() < deadline:
+        # (the request may be mid-prefill - neither queued nor running - when
+        # the wait gives up; the abort lands at the engine's next step)
+        while (eng.running or eng.waiting or eng.stats["aborted"] == 0) and time.time() < deadline:
             time.sleep(0.01)
         assert not eng.running and not eng.waiting and eng.stats["aborted"] == 1
         assert eng.alloc.num_used == 0
