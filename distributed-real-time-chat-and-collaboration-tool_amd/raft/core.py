@@ -402,6 +402,9 @@ class RaftCore:
             self._append_local(new[k:])
         if req.leader_commit > self.commit_index:
             self.commit_index = max(self.commit_index, min(req.leader_commit, prev + len(new)))
+        if self.last_applied < self.commit_index:
+            # also catches up a runtime that restarted with committed entries
+            # it has not re-applied yet
             self._apply()
         return AppendResp(self.term, True)
 

@@ -75,6 +75,10 @@ class SimCluster:
         self.storages[i].state["last_applied"] = -1
         ids = sorted(self.nodes)
         self._make(i, ids)
+        # boot replay of the committed entries, as raft/node.py does
+        n = self.nodes[i]
+        n.last_applied = n.snap_index
+        n._apply()
 
     # ------------------------------------------------------------- running
     def _post(self, when, item) -> None:
