@@ -138,8 +138,9 @@ PYBIND11_MODULE(_hipk, m) {
   m.def("ar_set_epoch", [](u64 base, uint64_t e) { return drtc::ar_set_epoch(P<void>(base), e); });
   m.def("lt_version", &drtc::lt_version);
   m.def("lt_gemm", [](u64 y, u64 x, u64 w, int64_t M, int64_t N, int64_t K, int64_t ldx,
-                      int64_t ldy, u64 st) {
-    return drtc::lt_gemm(P<void>(y), P<const void>(x), P<const void>(w), M, N, K, ldx, ldy, S(st));
+                      int64_t ldy, float beta, u64 st) {
+    return drtc::lt_gemm(P<void>(y), P<const void>(x), P<const void>(w), M, N, K, ldx, ldy, beta,
+                         S(st));
   });
   m.def("lt_set_algo", &drtc::lt_set_algo);
   m.def("skinny_glu_gemm", [](u64 y, u64 gu, u64 w, int M, int N, int K, int ldx, int ldy, int act,

@@ -84,8 +84,8 @@ Plan* get_plan(int dev, int64_t M, int64_t N, int64_t K, int64_t ldx, int64_t ld
 }
 
 int run(DeviceCtx* dc, Plan* p, const hipblasLtMatmulAlgo_t* algo, void* y, const void* x,
-        const void* w, hipStream_t st) {
-  const float alpha = 1.f, beta = 0.f;
+        const void* w, hipStream_t st, float beta = 0.f) {
+  const float alpha = 1.f;
   hipblasStatus_t s = hipblasLtMatmul(dc->handle, p->desc, &alpha, w, p->a, x, p->b, &beta, y,
                                       p->c, y, p->c, algo, dc->workspace, kWorkspaceBytes, st);
   return s == HIPBLAS_STATUS_SUCCESS ? 0 : -100 - int(s);
@@ -103,7 +103,7 @@ int lt_version() {
 }
 
 int lt_gemm(void* y, const void* x, const void* w, int64_t M, int64_t N, int64_t K, int64_t ldx,
-            int64_t ldy, hipStream_t st) {
+            int64_t ldy, float beta, hipStream_t st) {
   DeviceCtx* dc;
   Plan* p;
   {
@@ -115,7 +115,8 @@ int lt_gemm(void* y, const void* x, const void* w, int64_t M, int64_t N, int64_t
     if (!p) return -2;
   }
   // no tuned solution: hipBLASLt's own heuristic (algo == nullptr)
-  return run(dc, p, p->has_algo ? &p->algo : nullptr, y, x, w, st);
+  // beta = 1: y += x W^T in place (C = D = y; the residual stream of a prefill pass)
+  return run(dc, p, p->has_algo ? &p->algo : nullptr, y, x, w, st, beta);
 }
 
 int lt_set_algo(int64_t M, int64_t N, int64_t K, int64_t ldx, int64_t ldy, int algo_index) {

@@ -69,10 +69,10 @@ int launch_custom_ar_rmsnorm(void* normed, void* residual, const void* in, const
                              int rank, int world, int64_t stage_elems, hipStream_t st);
 int ar_set_epoch(void* base, uint64_t epoch);
 
-// Tuned hipBLASLt projection GEMM y[M,N] = x[M,K] @ W[N,K]^T, bf16 (gemm_lt.cpp).
+// Tuned hipBLASLt projection GEMM y[M,N] = x[M,K] @ W[N,K]^T + beta * y, bf16 (gemm_lt.cpp).
 int lt_version();
 int lt_gemm(void* y, const void* x, const void* w, int64_t M, int64_t N, int64_t K, int64_t ldx,
-            int64_t ldy, hipStream_t st);
+            int64_t ldy, float beta, hipStream_t st);
 int lt_set_algo(int64_t M, int64_t N, int64_t K, int64_t ldx, int64_t ldy, int algo_index);
 // (solution index, us per call) pairs; index -1 = hipBLASLt's heuristic pick
 std::vector<std::pair<int, float>> lt_tune(void* y, const void* x, const void* w, int64_t M,

@@ -4,8 +4,12 @@
 shapes listed in the tuning table (``ops/tuned/gemm_<arch>.json``: the
 decode GEMMs of each model at every hipGraph batch bucket) it calls
 hipBLASLt directly through ``csrc/kernels/gemm_lt.cpp`` with the solution
-that measured fastest on MI355X; every other shape (prefill, CPU) goes
-through ``torch.nn.functional.linear``.
+that measured fastest on MI355X.  Prefill-sized GEMMs (M above the decode
+buckets) take the solution tuned at the nearest measured M (entries flagged
+``prefill``, ``scripts/tune_prefill.py``) where it beat torch's own pick,
+for the plain GEMM (beta = 0) and for the in-place residual form (beta = 1)
+separately; every other shape (CPU, untuned) goes through
+``torch.nn.functional.linear`` / ``addmm_``.
 
 Why a table: a decode GEMM has a small fixed M (the batch bucket) and
 model-fixed N/K, where hipBLASLt's heuristic pick can be far from the best
@@ -24,6 +28,7 @@ per measured shape, whether a skinny variant beat the library
 from __future__ import annotations
 
 import json
+import math
 import os
 import threading
 
@@ -38,7 +43,14 @@ _lock = threading.Lock()
 #                   medium-M kernel K splits or 0)
 _table: dict[tuple[int, int, int, int], tuple[int, int, int]] | None = None
 _ready: set[tuple[int, int, int, int]] = set()               # entries with a native plan
+# (N, K, ldx) -> sorted [(tuned M, algo, beats F.linear, beats addmm_)]: prefill entries
+_prefill: dict[tuple[int, int, int], list[tuple[int, int, bool, bool]]] = {}
+# (M, N, K, ldx, beta) -> algo chosen for a prefill-sized call (-1: torch's path)
+_prefill_pick: dict[tuple[int, int, int, int, int], int] = {}
+DECODE_MAX_M = 1024  # decode buckets end here; larger M are prefill (or mixed) passes
 _enabled = os.environ.get("DRTC_TUNED_GEMM", "1") != "0"
+# prefill-sized entries (tuned at M = 2k..16k, scripts/tune_prefill.py)
+_prefill_enabled = os.environ.get("DRTC_PREFILL_TUNED", "1") != "0"
 # medium-M decode kernel (gemm_midm.hip) where the tuning table measured a win
 _midm_enabled = os.environ.get("DRTC_MIDM_GEMM", "1") != "0"
 # decode batches up to this many rows may take the hand-written skinny kernel
@@ -72,13 +84,24 @@ def _activate() -> dict:
         if _table is not None:
             return _table
         tab: dict[tuple[int, int, int, int], tuple[int, int, int]] = {}
+        pre: dict[tuple[int, int, int], list[tuple[int, int, bool, bool]]] = {}
         if _enabled and torch.cuda.is_available():
             ver = str(hipk().lt_version())
             for ks, e in load_table().get(ver, {}).items():
                 M, N, K, ldx = (int(v) for v in ks.split(","))
+                if e.get("prefill"):
+                    if _prefill_enabled:
+                        pre.setdefault((N, K, ldx), []).append(
+                            (M, int(e["algo"]), bool(e.get("beta0")), bool(e.get("beta1"))))
+                    continue
                 tab[(M, N, K, ldx)] = (int(e.get("algo", -1)), int(e.get("skinny", 0)),
                                        int(e.get("midm", 0)) if _midm_enabled else 0)
+        for v in pre.values():
+            v.sort()
         _ready.clear()
+        _prefill.clear()
+        _prefill.update(pre)
+        _prefill_pick.clear()
         _table = tab
     return _table
 
@@ -96,6 +119,28 @@ def _plan(key: tuple[int, int, int, int]) -> bool:
             return False
         _ready.add(key)
     return True
+
+
+def _prefill_algo(M: int, N: int, K: int, ldx: int, beta: int) -> int:
+    """Solution for a prefill-sized GEMM: the entry tuned at the M nearest
+    to this one (log scale) for the same (N, K, ldx), if that entry beat
+    torch's pick for this beta; -1 = use torch's path.  The native plan is
+    per exact M (registered on first use, outside graph capture: prefill
+    passes run eagerly)."""
+    key = (M, N, K, ldx, beta)
+    algo = _prefill_pick.get(key)
+    if algo is not None:
+        return algo
+    algo = -1
+    cands = _prefill.get((N, K, ldx))
+    if cands and M > DECODE_MAX_M:
+        Mt, a, b0, b1 = min(cands, key=lambda c: abs(math.log(c[0] / M)))
+        if (b1 if beta else b0) and abs(math.log(Mt / M)) <= math.log(2.0):
+            with _lock:
+                if hipk().lt_set_algo(M, N, K, ldx, N, a) == 0:
+                    algo = a
+    _prefill_pick[key] = algo
+    return algo
 
 
 def reset() -> None:
@@ -159,7 +204,13 @@ def linear(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
         N = w.shape[0]
         key = (M, N, K, x.stride(0))
         ent = _activate().get(key)
-        if ent is None:
+        if ent is None and M > DECODE_MAX_M:
+            if _prefill_algo(M, N, K, x.stride(0), 0) >= 0:
+                y = torch.empty((M, N), dtype=x.dtype, device=x.device)
+                check(hipk().lt_gemm(y.data_ptr(), x.data_ptr(), w.data_ptr(), M, N, K,
+                                     x.stride(0), N, 0.0, stream_ptr(x)), "lt_gemm")
+                return y
+        elif ent is None:
             v = skinny_variant(M, N, K, x.stride(0))
             if v:
                 return skinny_linear(x, w, v)
@@ -170,7 +221,7 @@ def linear(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
         elif ent[0] >= 0 and _plan(key):
             y = torch.empty((M, N), dtype=x.dtype, device=x.device)
             check(hipk().lt_gemm(y.data_ptr(), x.data_ptr(), w.data_ptr(), M, N, K, x.stride(0),
-                                 N, stream_ptr(x)), "lt_gemm")
+                                 N, 0.0, stream_ptr(x)), "lt_gemm")
             return y
     return F.linear(x, w)
 
@@ -200,6 +251,15 @@ def linear_residual(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor) ->
     the fp32 accumulator plus the residual) instead of two (GEMM output,
     then the add in the norm kernel)."""
     assert residual.shape == (x.shape[0], w.shape[0]) and w.dtype == x.dtype
+    M, K = x.shape
+    N = w.shape[0]
+    if (_enabled and x.stride(1) == 1 and w.is_contiguous() and residual.stride(0) == N
+            and x.dtype == torch.bfloat16):
+        _activate()
+        if _prefill_algo(M, N, K, x.stride(0), 1) >= 0:
+            check(hipk().lt_gemm(residual.data_ptr(), x.data_ptr(), w.data_ptr(), M, N, K,
+                                 x.stride(0), N, 1.0, stream_ptr(x)), "lt_gemm")
+            return residual
     return residual.addmm_(x, w.t())
 
 

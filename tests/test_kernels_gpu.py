@@ -505,6 +505,39 @@ def test_tuned_linear(hipk, M, N, K):
         gemm._table = saved
 
 
+@pytest.mark.parametrize("M,N,K", [(2304, 1024, 512), (4352, 2048, 1536)])
+def test_prefill_tuned_linear_and_residual(hipk, M, N, K):
+    """Prefill-sized tuned entries (ops.gemm._prefill): a solution tuned at a
+    nearby M runs the plain GEMM (beta = 0) and the in-place residual form
+    (beta = 1, y += x @ w.T) through hipBLASLt directly; both match fp32."""
+    from drtc_amd.ops import gemm
+
+    torch.manual_seed(2)
+    Mt = 4096  # entry tuned at another M, applied by nearest-M lookup
+    r = gemm.tune(Mt, N, K, torch.device(DEV), iters=3, max_candidates=4)
+    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=DEV) * 0.05).to(torch.bfloat16)
+    res = torch.randn(M, N, device=DEV).to(torch.bfloat16)
+    ref = x.float() @ w.float().t()
+    gemm._activate()
+    saved = dict(gemm._prefill)
+    try:
+        gemm._prefill[(N, K, K)] = [(Mt, r["algo"], True, True)]
+        gemm._prefill_pick.clear()
+        y = gemm.linear(x, w)
+        assert gemm._prefill_pick.get((M, N, K, K, 0), -1) >= 0, "tuned prefill path not taken"
+        _close(y, ref, 2e-2, 2e-2, "prefill tuned linear")
+        want = ref + res.float()
+        out = gemm.linear_residual(x, w, res)
+        assert out.data_ptr() == res.data_ptr()
+        assert gemm._prefill_pick.get((M, N, K, K, 1), -1) >= 0
+        _close(out, want, 3e-2, 2e-2, "prefill tuned residual")
+    finally:
+        gemm._prefill.clear()
+        gemm._prefill.update(saved)
+        gemm._prefill_pick.clear()
+
+
 @pytest.mark.parametrize("M", [1, 2, 3, 5, 8, 13, 16])
 @pytest.mark.parametrize("N,K,ldx", [(256, 512, 512), (1152, 1536, 1536), (128, 4096, 4224),
                                      (192, 14336, 14336), (96, 384, 392)])
