@@ -84,6 +84,11 @@ PYBIND11_MODULE(_hipk, m) {
                              P<void>(slab), slab_bytes, P<int>(counters), n_counters, S(st));
   });
   m.def("gemm_workspace_bytes", &drtc::gemm_workspace_bytes);
+  m.def("gemm_dec", [](u64 c, u64 a, u64 b, u64 r, int M, int N, int K, int lda, int ldb, int ldc,
+                       int ldr, int epi, int up_off, int nr, int group_m, u64 st) {
+    return drtc::launch_gemm_dec(P<void>(c), P<const void>(a), P<const void>(b), P<const void>(r),
+                                 M, N, K, lda, ldb, ldc, ldr, epi, up_off, nr, group_m, S(st));
+  });
   m.def("moe_workspace_bytes", &drtc::moe_workspace_bytes);
   m.def("custom_ar_buffer_bytes", &drtc::custom_ar_buffer_bytes);
   m.def("custom_allreduce", [](u64 out, u64 in, int64_t n, const std::vector<u64>& bases, int rank,

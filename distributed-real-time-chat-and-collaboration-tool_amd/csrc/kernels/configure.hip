@@ -9,6 +9,8 @@ int configure_kernels() {
   if (e) return e;
   e = configure_moe();
   if (e) return e;
-  return configure_gemm();
+  e = configure_gemm();
+  if (e) return e;
+  return configure_gemm_dec();
 }
 }  // namespace drtc

@@ -115,5 +115,11 @@ int launch_midm_gemm(void* y, const void* x, const void* w, const void* res, int
                      int64_t slab_bytes, hipStream_t st);
 int configure_moe();
 int configure_gemm();
+// Decode-batch GEMM (gemm_dec.hip): 128 x 128 tiles, intra-workgroup K split over two wave
+// groups; epi as launch_gemm (N = columns of C; gated: up_off == N); nr = LDS regions 4/6/8.
+int launch_gemm_dec(void* c, const void* a, const void* b, const void* r, int M, int N, int K,
+                    int lda, int ldb, int ldc, int ldr, int epi, int up_off, int nr, int group_m,
+                    hipStream_t st);
+int configure_gemm_dec();
 
 }  // namespace drtc

@@ -426,7 +426,8 @@ def save_entries(entries: dict[str, dict], path: str | None = None) -> str:
 
 
 __all__ = ["linear", "norm_linear", "glu_linear", "skinny_linear", "skinny_ok", "skinny_variant",
-           "skinny_supports", "mfma_gemm", "midm_gemm", "midm_supported", "tune", "save_entries",
+           "skinny_supports", "mfma_gemm", "midm_gemm", "midm_supported", "dec_gemm", "dec_supported",
+           "tune", "save_entries",
            "load_table", "reset", "set_enabled", "table_path"]
 
 
@@ -487,4 +488,43 @@ def midm_gemm(x: torch.Tensor, w: torch.Tensor, epi: str = "store",
                            x.stride(0), out.stride(0),
                            residual.stride(0) if residual is not None else 0, MIDM_EPI[epi], S,
                            slab.data_ptr(), slab.numel() * 4, stream_ptr(x)), "midm_gemm")
+    return out
+
+
+# ------------------------------------------------------------------ decode-batch GEMM
+DEC_EPI = {"store": 0, "residual": 1, "silu": 2, "gelu_tanh": 3}
+
+
+def dec_supported(M: int, N: int, K: int, epi: str = "store") -> bool:
+    """Shapes csrc/kernels/gemm_dec.hip covers: K % 64, N % 128 (N/2 % 64 gated)."""
+    glu = epi in ("silu", "gelu_tanh")
+    return (M >= 1 and K % 64 == 0 and epi in DEC_EPI
+            and ((N // 2) % 64 == 0 and N % 2 == 0 if glu else N % 128 == 0))
+
+
+def dec_gemm(x: torch.Tensor, w: torch.Tensor, epi: str = "store",
+             residual: torch.Tensor | None = None, out: torch.Tensor | None = None,
+             nr: int = 8, group_m: int = 8, pipe: int = 2) -> torch.Tensor:
+    """Decode-batch GEMM (csrc/kernels/gemm_dec.hip): y = epi(x @ w.T) on 128 x 128 tiles
+    with the K loop split over two wave groups of each workgroup (one tile per CU at
+    M = 1024, N = 4096; no cross-workgroup reduction).  ``epi`` as ``mfma_gemm``; ``nr``
+    = LDS regions (4: 64 KiB, two workgroups per CU; 6 / 8: 96 / 128 KiB, deeper
+    prefetch); ``pipe`` 1 = fragments read after each barrier, 2 = fragments double-
+    buffered in registers with the DMA spread over the MFMAs."""
+    M, K = x.shape
+    glu = epi in ("silu", "gelu_tanh")
+    N = w.shape[0] // 2 if glu else w.shape[0]
+    assert x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and x.is_cuda
+    assert x.stride(1) == 1 and w.is_contiguous() and w.shape[1] == K
+    assert dec_supported(M, w.shape[0], K, epi), (M, w.shape[0], K, epi)
+    if out is None:
+        out = residual if (epi == "residual" and residual is not None) else \
+            torch.empty((M, N), dtype=x.dtype, device=x.device)
+    assert out.shape == (M, N) and out.stride(1) == 1
+    if epi == "residual":
+        assert residual is not None and residual.shape == (M, N) and residual.stride(1) == 1
+    check(hipk().gemm_dec(out.data_ptr(), x.data_ptr(), w.data_ptr(), ptr(residual), M, N, K,
+                          x.stride(0), w.stride(0), out.stride(0),
+                          residual.stride(0) if residual is not None else 0, DEC_EPI[epi],
+                          N if glu else 0, 10 * pipe + nr, group_m, stream_ptr(x)), "gemm_dec")
     return out
