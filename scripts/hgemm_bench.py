@@ -86,7 +86,6 @@ def eager_time(fn, iters):
         e.synchronize()
         return s.elapsed_time(e) * 1e3 / iters  # us
 
-    run.keep = (fn, g)  # the graph writes into buffers fn's closure keeps alive
     return run
 
 
@@ -107,6 +106,7 @@ def graph_time(fn, iters):
         e.synchronize()
         return s.elapsed_time(e) * 1e3 / iters  # us
 
+    run.keep = (fn, g)  # the graph writes into buffers fn's closure keeps alive
     return run
 
 
