@@ -25,9 +25,11 @@ def short(name: str) -> str:
         return f"hipBLASLt GEMM MT{m.group(1) if m else '?'}"
     m = re.search(r"drtc::(\w+)", name) or re.search(r"drtc(\d+)(\w+?)E", name)
     if "drtc" in name:
-        for k in ("paged_decode_kernel", "decode_reduce_kernel", "prefill_attn_kernel",
-                  "rmsnorm_kernel", "act_glu_kernel", "rope_kv_kernel", "sample_kernel",
-                  "moe_", "allreduce"):
+        for k in ("paged_decode_persist_kernel", "paged_decode_wave_kernel", "paged_decode_kernel",
+                  "decode_reduce_kernel", "prefill_attn_persist_kernel", "prefill_attn_kernel",
+                  "kv_write_v_kernel", "midm_reduce_kernel", "midm_kernel", "gemm_dec_kernel",
+                  "gemm256", "skinny", "rmsnorm_kernel", "act_glu_kernel", "rope_kv_kernel",
+                  "sample_kernel", "moe_", "allreduce"):
             if k in name:
                 return "drtc::" + k
     if "at::native" in name:
@@ -62,8 +64,8 @@ def main():
         names = {x[2] for x in p}
         if any("distribution_" in n for n in names):
             return None  # random weight init before the first forward
-        return ("prefill" if "drtc::prefill_attn_kernel" in names else
-                "decode" if "drtc::paged_decode_kernel" in names else None)
+        return ("prefill" if any(n.startswith("drtc::prefill_attn") for n in names) else
+                "decode" if any(n.startswith("drtc::paged_decode") for n in names) else None)
 
     busy_max = collections.Counter()
     for p in passes:
