@@ -34,6 +34,7 @@ import torch.distributed as dist
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 from drtc_amd.engine import ChatTokenizer, LLMEngine, Request, SamplingParams  # noqa: E402
+from drtc_amd.engine.engine import freeze_gc  # noqa: E402
 from drtc_amd.llm import prompts as P  # noqa: E402
 from drtc_amd.llm.service import FeatureParams  # noqa: E402
 from drtc_amd.models import TransformerLM, get_config  # noqa: E402
@@ -254,10 +255,12 @@ def main() -> None:
     for w in range(args.warmup):
         serve(make_prompts(-1 - w))
     if args.arrival_rate > 0:
+        freeze_gc()
         open_loop(args, eng, make_prompts, params, rank, world, tp, device, cfg)
         return
     prompts = [make_prompts(s) for s in range(args.steps)]
     prompt_tokens = sum(len(p) for ps in prompts for p in ps)
+    freeze_gc()  # as a serving process after warm-up (DRTC_GC_FREEZE=0: off)
 
     if world > 1:
         dist.barrier()

@@ -50,6 +50,18 @@ def _pad_tokens(T: int) -> int:
     return -(-T // 256) * 256
 
 
+
+def freeze_gc() -> None:
+    """Move every object alive now (weights, captured graphs, caches, prepared inputs)
+    into the cyclic GC's permanent generation, once per serving process after warm-up:
+    full collections triggered in the request loop then walk only request-lifetime
+    objects instead of the whole long-lived heap.  ``DRTC_GC_FREEZE=0`` disables it."""
+    import gc
+
+    if os.environ.get("DRTC_GC_FREEZE", "1") != "0":
+        gc.collect()
+        gc.freeze()
+
 class LLMEngine:
     def __init__(self, model: TransformerLM, max_batch: int = 256, max_model_len: int = 4096,
                  max_prefill_tokens: int = 16384, num_blocks: int | None = None,

@@ -105,7 +105,7 @@ def _worker_main(rank: int, device: str, model_name: str, engine_kw: dict, inq, 
     detection: per-GPU replica eviction)."""
     import torch
 
-    from ..engine.engine import EngineLoop, LLMEngine
+    from ..engine.engine import EngineLoop, LLMEngine, freeze_gc
     from ..models import TransformerLM, get_config
 
     try:
@@ -115,6 +115,7 @@ def _worker_main(rank: int, device: str, model_name: str, engine_kw: dict, inq, 
         model = TransformerLM(cfg, device, seed=seed, full_then_shard=False)
         eng = LLMEngine(model, seed=rank, **engine_kw)
         eng.warmup(capture=True)
+        freeze_gc()  # this process only serves the engine from here on
         loop = EngineLoop(eng).start()
         outq.put(("ready", rank, None))
     except BaseException as e:  # report start-up failures to the parent

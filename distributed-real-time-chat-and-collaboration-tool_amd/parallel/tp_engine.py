@@ -57,6 +57,9 @@ def tp_worker(rank: int, world: int, port: int, model_name: str, engine_kw: dict
         # flag waits are time-bounded, so enter the captured warm-up together
         dist.barrier(group=cpu)
         eng.warmup(capture=True)
+        from ..engine.engine import freeze_gc
+
+        freeze_gc()  # this process only serves the engine from here on
         if rank == 0:
             outq.put(("ready", 0, None))
     except BaseException as e:
