@@ -24,6 +24,7 @@ import grpc
 from ..protos import RAFT_SERVICE, RAFT_SNAPSHOT_SERVICE, make_stub, raft_pb, raft_snap_pb
 from .core import (NOOP, AppendReq, AppendResp, Entry, NotLeaderError, RaftConfig, RaftCore,
                    SnapshotReq, SnapshotResp, VoteReq, VoteResp)
+from ..utils import pickle_compat
 from .state_machine import ChatState
 from .storage import data_dir, open_storage
 
@@ -70,6 +71,7 @@ class RaftRuntime:
         self.storage = open_storage(storage, self.dir, port, fsync)
         self.state = state or ChatState()
         self.state_lock = threading.RLock()
+        self._persist_lock = threading.Lock()
         self.core_lock = threading.RLock()
         self.tick_interval = tick
         self.persist_interval = persist_interval
@@ -217,10 +219,15 @@ class RaftRuntime:
 
     def _persist_loop(self) -> None:
         last_export = time.monotonic()
+        pause = self.persist_interval
         while self.running:
-            time.sleep(self.persist_interval)
+            time.sleep(pause)
             try:
-                self.persist()
+                # the app-state pickles are a cache (the log is the source of truth):
+                # under write load with a large state, pace them so that pickling under
+                # the state lock takes at most ~5 % of the time
+                held = self.persist()
+                pause = max(self.persist_interval, 20.0 * held)
                 if self.export_interval and time.monotonic() - last_export >= self.export_interval:
                     self.export_reference_log()
                     last_export = time.monotonic()
@@ -238,12 +245,19 @@ class RaftRuntime:
         with self.core_lock:
             self.storage.export_end(last)
 
-    def persist(self, all_files: bool = False) -> None:
-        with self.state_lock:
-            if all_files:
-                self.state.save_all(self.dir)
-            elif self.state.dirty:
-                self.state.save(self.dir)
+    def persist(self, all_files: bool = False) -> float:
+        """Write the dirty (or all) app-state pickles.  They are pickled under the
+        state lock (a consistent image) and written after it is released, so applies
+        and reads wait for the pickling only, never for file I/O.  Returns the
+        seconds the lock was held."""
+        with self._persist_lock:  # writes land in the order their images were taken
+            with self.state_lock:
+                t0 = time.perf_counter()
+                files = self.state.encode(self.dir, list(self.state.FILES) if all_files else None)
+                held = time.perf_counter() - t0
+            for path, data in files:
+                pickle_compat.write_bytes(data, path)
+        return held
 
     # ------------------------------------------------------------ apply
     def _apply(self, index: int, e: Entry) -> None:

@@ -250,9 +250,19 @@ class ChatState:
         raise KeyError(which)
 
     def save(self, data_dir: str, which=None, fsync: bool = False) -> None:
+        for path, data in self.encode(data_dir, which):
+            pickle_compat.write_bytes(data, path, fsync)
+
+    def encode(self, data_dir: str, which=None) -> list[tuple[str, bytes]]:
+        """Pickled images (reference layout) of the given or the dirty files, marked
+        clean: the caller holds the state lock for this step only and writes the
+        bytes after releasing it (``pickle_compat.write_bytes``)."""
+        out = []
         for w in (which or list(self.dirty)):
-            pickle_compat.dump(self.snapshot_obj(w), os.path.join(data_dir, self.FILES[w]), fsync)
+            out.append((os.path.join(data_dir, self.FILES[w]),
+                        pickle.dumps(self.snapshot_obj(w), protocol=pickle_compat.PROTOCOL)))
             self.dirty.discard(w)
+        return out
 
     def save_all(self, data_dir: str, fsync: bool = False) -> None:
         self.save(data_dir, list(self.FILES), fsync)

@@ -50,9 +50,14 @@ def _fsync_dir(d: str) -> None:
 
 def dump(obj, path: str, fsync: bool = False) -> None:
     """Atomic write (temp file + rename) of ``pickle.dumps(obj, protocol=4)``."""
+    write_bytes(pickle.dumps(obj, protocol=PROTOCOL), path, fsync)
+
+
+def write_bytes(data: bytes, path: str, fsync: bool = False) -> None:
+    """Atomic write (temp file + rename) of already-pickled bytes: lets a caller
+    pickle under its lock (a consistent image) and do the file I/O outside it."""
     d = os.path.dirname(os.path.abspath(path))
     os.makedirs(d, exist_ok=True)
-    data = pickle.dumps(obj, protocol=PROTOCOL)
     fd, tmp = tempfile.mkstemp(dir=d, prefix=".tmp_", suffix=".pkl")
     try:
         with os.fdopen(fd, "wb") as f:

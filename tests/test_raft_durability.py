@@ -24,6 +24,7 @@ import pytest
 
 from drtc_amd.protos import RAFT_SERVICE, make_stub, raft_pb
 from drtc_amd.raft.core import Entry
+from drtc_amd.raft.state_machine import ChatState
 from drtc_amd.raft.storage import NativeStorage
 from drtc_amd.utils import pickle_compat
 from drtc_amd.utils.cluster import LocalCluster, free_port
@@ -311,3 +312,26 @@ def test_sigkill_leader_mid_write_then_restart_from_disk(tmp_path):
             if p.poll() is None:
                 os.killpg(p.pid, signal.SIGKILL)
                 p.wait(timeout=10)
+
+
+def test_persist_writes_app_state_outside_the_state_lock(cluster, monkeypatch):
+    """App-state pickles are taken under the state lock and written after it is
+    released: applies never wait for file I/O (a large messages.pkl rewrite used to
+    block every apply for its whole duration).  The files still match the state."""
+    L, cid = _workload(cluster)
+    rt = cluster.nodes[L].rt
+    writes = []
+    real = pickle_compat.write_bytes
+
+    def probe(data, path, fsync=False):
+        if rt.state_lock._is_owned():  # only the leader's own state lock is of interest
+            writes.append(path)
+        return real(data, path, fsync)
+
+    monkeypatch.setattr(pickle_compat, "write_bytes", probe)
+    held = rt.persist(all_files=True)
+    monkeypatch.undo()
+    assert writes == [] and held >= 0.0, writes
+    st = ChatState()
+    st.load(rt.dir)
+    assert [m["content"] for m in st.channel_messages[cid]] == [f"m{k}" for k in range(5)]
