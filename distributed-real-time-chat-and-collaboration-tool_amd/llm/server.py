@@ -32,6 +32,23 @@ from .service import LLMServicer
 log = logging.getLogger("drtc_amd.llm.server")
 
 
+# Engine batch (max concurrent requests per replica) when --max-batch is not given: the
+# measured throughput knee on one MI355X that still answers inside the reference's
+# per-feature node->LLM deadlines (20 s smart reply / suggestions, 10 s summarize and
+# ask-AI: ref server/raft_node.py:2018,2084,2126,2187).  BASELINE.md: Llama-3-8B and
+# Gemma-2B smart reply at 1024 (p50 2.5 s / 0.8 s); Mixtral suggestions at 512 (p50 5.2 s,
+# +20 % over 256); Llama-3-70B ask-AI on one GPU at 192 (p50 9.45 s; 256 is over 10 s).
+DEFAULT_MAX_BATCH = {"llama-3-8b": 1024, "gemma-2b": 1024, "mixtral-8x7b": 512,
+                     "llama-3-70b": 192}
+
+
+def default_max_batch(model: str, tp: int = 1) -> int:
+    """Engine batch for ``model`` when the operator did not choose one (256 for
+    models without a measurement; a TP group has tp x the compute of one GPU)."""
+    b = DEFAULT_MAX_BATCH.get(model, 256)
+    return b if tp <= 1 else max(b, 256)
+
+
 def build_backend(args):
     if args.backend == "scripted":
         return ScriptedBackend()
@@ -90,7 +107,8 @@ def main(argv=None):
                     help="one-shot IPC all-reduce (+ fused residual/RMSNorm) for decode-sized "
                          "TP messages, RCCL above the threshold (default)")
     ap.add_argument("--rccl-only", dest="custom_allreduce", action="store_false")
-    ap.add_argument("--max-batch", type=int, default=256)
+    ap.add_argument("--max-batch", type=int, default=0,
+                    help="engine batch per replica (default: per model, DEFAULT_MAX_BATCH)")
     ap.add_argument("--max-model-len", type=int, default=4096)
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--in-process", action="store_true",
@@ -101,6 +119,8 @@ def main(argv=None):
     ap.add_argument("--log-level", default="INFO")
     args = parse_with_config(ap, argv)
     setup_logging(args.log_level)
+    if not args.max_batch:
+        args.max_batch = default_max_batch(args.model, args.tp)
     backend = build_backend(args)
     workers = args.workers or args.max_batch * max(1, args.gpus) + 16
     server = serve(backend, args.port, workers)

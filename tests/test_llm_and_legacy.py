@@ -361,3 +361,15 @@ def test_pool_router_timeout_aborts_on_the_replica():
         assert len(out) == 1 and pool.load == [0]
     finally:
         pool.close()
+
+
+def test_default_engine_batch_per_model():
+    """Without --max-batch the LLM server sizes the engine batch per model from the
+    BASELINE measurements that stay inside the reference's deadlines."""
+    from drtc_amd.llm.server import default_max_batch
+
+    assert default_max_batch("llama-3-8b") == 1024
+    assert default_max_batch("mixtral-8x7b") == 512
+    assert default_max_batch("llama-3-70b") == 192      # p50 9.45 s < 10 s ask-AI deadline
+    assert default_max_batch("llama-3-70b", tp=8) == 256
+    assert default_max_batch("tiny-llama") == 256
