@@ -360,10 +360,15 @@ class LLMEngine:
         prepares chunk i+1 while the GPU runs chunk i (only the first chunk's
         preparation is on the critical path); the sampled first tokens come
         back through pinned buffers and are read after the last launch."""
+        # greedy, not balanced: a chunk of 16,384 tokens fills whole waves of workgroups
+        # on 256 CUs in every projection GEMM (64 row tiles x 16 / 24 / 112 column tiles
+        # of 256), while "balanced" 10 x ~15.2k chunks measured 5.5 % slower end to end
+        # (profiles/r2o_decode_gemm_128tile.md, wave quantization)
+        limit = self.prefill_chunk_tokens
         chunks, cur, tok = [], [], 0
         for r in batch:
             n = r.num_tokens
-            if cur and tok + n > self.prefill_chunk_tokens:
+            if cur and tok + n > limit:
                 chunks.append(cur)
                 cur, tok = [], 0
             cur.append(r)

@@ -35,10 +35,11 @@ log = logging.getLogger("drtc_amd.llm.server")
 # Engine batch (max concurrent requests per replica) when --max-batch is not given: the
 # measured throughput knee on one MI355X that still answers inside the reference's
 # per-feature node->LLM deadlines (20 s smart reply / suggestions, 10 s summarize and
-# ask-AI: ref server/raft_node.py:2018,2084,2126,2187).  BASELINE.md: Llama-3-8B and
-# Gemma-2B smart reply at 1024 (p50 2.5 s / 0.8 s); Mixtral suggestions at 512 (p50 5.2 s,
-# +20 % over 256); Llama-3-70B ask-AI on one GPU at 192 (p50 9.45 s; 256 is over 10 s).
-DEFAULT_MAX_BATCH = {"llama-3-8b": 1024, "gemma-2b": 1024, "mixtral-8x7b": 512,
+# ask-AI: ref server/raft_node.py:2018,2084,2126,2187).  BASELINE.md: Llama-3-8B smart
+# reply at 1024 (p50 2.5 s; 1536 adds ~1 %), Gemma-2B at 2048 (p50 1.5 s, +7.7 % over 1024),
+# Mixtral suggestions at 1024 (p50 8.9 s, +11 % over 512, +40 % over 256), Llama-3-70B
+# ask-AI on one GPU at 192 (p50 9.45 s; 256 is over the 10 s deadline).
+DEFAULT_MAX_BATCH = {"llama-3-8b": 1024, "gemma-2b": 2048, "mixtral-8x7b": 1024,
                      "llama-3-70b": 192}
 
 

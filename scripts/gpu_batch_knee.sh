@@ -21,3 +21,5 @@ run mix512 --model mixtral-8x7b --workload suggest --batch 512 --steps 2 && \
 run gemma2048 --model gemma-2b --batch 2048 --steps 3 && \
 run gemma1024 --model gemma-2b --batch 1024 --steps 3 && \
 run smart1024 --steps 3
+[ "${BAL_AB:-0}" = "1" ] && DRTC_PREFILL_BALANCE=0 run smart_bal0 --steps 4 && run smart_bal1 --steps 4 && \
+  DRTC_PREFILL_BALANCE=0 run smart_bal0b --steps 4 && run smart_bal1b --steps 4
