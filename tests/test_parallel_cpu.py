@@ -154,14 +154,22 @@ def _tp_mixed_worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
+def _capped(fn, rank, world, port, q):
+    # each rank gets its share of the CPUs: 2 ranks x all cores oversubscribe
+    # the machine (and more so under pytest -n), which made the mixed-step test
+    # miss its queue deadline
+    torch.set_num_threads(max(1, (os.cpu_count() or 2) // (2 * world)))
+    fn(rank, world, port, q)
+
+
 def _run(fn, world=2):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    ps = [ctx.Process(target=fn, args=(r, world, port, q)) for r in range(world)]
+    ps = [ctx.Process(target=_capped, args=(fn, r, world, port, q)) for r in range(world)]
     for p in ps:
         p.start()
-    out = [q.get(timeout=240) for _ in ps]
+    out = [q.get(timeout=480) for _ in ps]
     for p in ps:
         p.join(timeout=60)
         assert p.exitcode == 0
