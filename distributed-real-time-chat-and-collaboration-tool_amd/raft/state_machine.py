@@ -171,7 +171,9 @@ class ChatState:
 
     def conversation(self, a: str, b: str) -> list:
         conv = list(self._dm_pair.get(tuple(sorted((a, b))), ()))
-        conv.sort(key=lambda m: m["timestamp"])
+        # a DM entry without a timestamp (hand-built or foreign log) sorts
+        # first instead of failing the read
+        conv.sort(key=lambda m: m.get("timestamp") or "")
         return conv
 
     def dms_of_user(self, user_id: str) -> list:
