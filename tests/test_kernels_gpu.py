@@ -259,6 +259,26 @@ def test_prefill_attention(hipk, D, Hq, Hkv, lens, persist):
     _close(out, ref, 2e-2, 2e-2, "prefill")
 
 
+@pytest.mark.parametrize("persist", [True, False])
+def test_prefill_attention_shape_padding_rows_zero(hipk, persist):
+    """A shape-padded chunk (T > cu[-1]): the op allocates its output, only the
+    padding rows are zeroed, the real rows equal the reference."""
+    Hq, Hkv, D, lens, pad = 32, 8, 128, [37, 100], 27
+    ops.set_prefill_persist(persist)
+    torch.manual_seed(5)
+    T = sum(lens) + pad
+    qkv = torch.randn(T, (Hq + 2 * Hkv) * D, device=DEV).to(torch.bfloat16)
+    cu = [0, lens[0], sum(lens)]
+    cu_d = torch.tensor(cu, dtype=torch.int32, device=DEV)
+    torch.empty(T * Hq * D * 4, dtype=torch.bfloat16, device=DEV).fill_(7.0)  # dirty the pool
+    out = ops.prefill_attention(qkv, cu_d, Hq, Hkv, D, D ** -0.5, True, cu_host=cu)
+    ops.set_prefill_persist(None)
+    ref = ops.prefill_attention_ref(qkv[:cu[-1]], cu, Hq, Hkv, D, D ** -0.5, True)
+    assert out.shape == (T, Hq * D)
+    assert torch.count_nonzero(out[cu[-1]:]).item() == 0
+    _close(out[:cu[-1]], ref, 2e-2, 2e-2, "prefill padded")
+
+
 @pytest.mark.parametrize("D,Hq,Hkv", [(128, 32, 8), (256, 8, 1), (64, 8, 2)])
 def test_prefill_persistent_many_items(hipk, D, Hq, Hkv):
     """Persistent workgroups at a chat-batch scale (many more (tile, head
