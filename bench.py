@@ -17,7 +17,11 @@ top-p 0.95) through the fused HIP sampler.
 ``value`` = generated tokens / s over all ranks (max wall time over ranks);
 ``p50_latency_ms`` = median request latency (arrival -> last token).
 
-Launch: ``python bench.py`` (1 GPU) or torchrun with --gpus N.
+Launch: ``python bench.py`` (1 GPU); ``python bench.py --gpus N`` starts N rank
+processes itself (one per GPU, RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* in their
+environment, RCCL) before the parent touches the GPU, prints rank 0's JSON line
+and exits non-zero if any rank fails; under torchrun (WORLD_SIZE set) the ranks
+are torchrun's and WORLD_SIZE must equal --gpus.
 """
 from __future__ import annotations
 
@@ -154,6 +158,57 @@ def open_loop(args, eng, make_prompts, params, rank, world, tp, device, cfg) -> 
         dist.destroy_process_group()
 
 
+def _free_port() -> int:
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def self_launch(n: int) -> int:
+    """Run this script as ``n`` rank processes (no torchrun in the parent, no GPU call
+    in the parent: children are started with subprocess, never exec).  Rank 0's
+    stdout (the JSON line) is forwarded; every rank's stderr goes to ours.  When a
+    rank fails the others are stopped and its exit status is returned."""
+    import subprocess
+
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                   HSA_ENABLE_IPC_MODE_LEGACY="0")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]],
+                                      env=env, stdout=subprocess.PIPE if r == 0 else
+                                      subprocess.DEVNULL))
+    rc = 0
+    try:
+        while True:
+            alive = [p for p in procs if p.poll() is None]
+            bad = [p for p in procs if p.poll() not in (None, 0)]
+            if bad:
+                rc = bad[0].returncode
+                break
+            if not alive:
+                break
+            time.sleep(0.2)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        for p in procs:
+            try:
+                p.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+    out = procs[0].stdout.read().decode() if procs[0].stdout else ""
+    sys.stdout.write(out)
+    sys.stdout.flush()
+    return rc if rc else (0 if any(ln.startswith("{") for ln in out.splitlines()) else 1)
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -188,6 +243,12 @@ def main() -> None:
                     help="prompt-token budget of a mixed prefill+decode step")
     ap.add_argument("--no-mixed", action="store_true", help="strict prefill-first scheduling")
     args = ap.parse_args()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(self_launch(args.gpus))
+    if int(os.environ.get("WORLD_SIZE", "1")) != args.gpus:
+        print(f"[bench] error: --gpus {args.gpus} but WORLD_SIZE {os.environ.get('WORLD_SIZE')}",
+              file=sys.stderr, flush=True)
+        sys.exit(2)
     if args.trace:
         from drtc_amd.utils import tracing
         tracing.enable(True)
@@ -200,8 +261,6 @@ def main() -> None:
         device = torch.device("cuda", local)
     else:
         device = torch.device("cpu")
-    if world != args.gpus:
-        log(rank, f"warning: --gpus {args.gpus} but WORLD_SIZE {world}")
 
     cfg = get_config(args.model)
     t0 = time.perf_counter()

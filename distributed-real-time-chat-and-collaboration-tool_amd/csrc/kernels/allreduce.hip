@@ -153,7 +153,8 @@ __global__ __launch_bounds__(512) void custom_allreduce_kernel(
   const int64_t c0 = (int64_t)b * chunk;  // fixed per block, whatever the message size
   const int64_t c1 = c0 + chunk < n8 ? c0 + chunk : n8;
 
-  bf16x8* my_stage = reinterpret_cast<bf16x8*>(mine + buf_off);
+  const int64_t s0 = (int64_t)b * chunk - c0;  // staging index = element index + s0
+  bf16x8* my_stage = reinterpret_cast<bf16x8*>(mine + buf_off) + s0;
   const bf16x8* src = reinterpret_cast<const bf16x8*>(in);
   for (int64_t i = c0 + tid; i < c1; i += blockDim.x) my_stage[i] = src[i];
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -195,14 +196,16 @@ __global__ __launch_bounds__(512) void custom_allreduce_kernel(
 // One-shot all-reduce fused with the residual add and RMSNorm of a TP decode
 // sublayer: h = residual + sum_q partial_q (fixed rank order, rounded to bf16 once
 // as the all-reduce alone would), residual <- h, normed = rmsnorm(h) * w (Gemma:
-// * (1 + w)).  Block b owns whole rows [b R, (b+1) R), R = chunk / H, which lie
-// inside its fixed staging chunk, so the epoch/parity protocol is the one of the
-// plain kernels (they may be interleaved on one communicator).  Every rank
+// * (1 + w)).  Block b owns whole rows [b R, (b+1) R), R = floor(chunk / (H / 8)), and
+// stages them at the START of its own fixed chunk [b chunk, (b+1) chunk) of the staging
+// buffer (not at row * H / 8, which crosses into block b-1's chunk whenever chunk is not a
+// multiple of H / 8, e.g. H = 5120), so the epoch/parity protocol is the one of the plain
+// kernels (they may be interleaved on one communicator).  Every rank
 // reduces the same bytes in the same order: bit-identical outputs on all ranks.
 __global__ __launch_bounds__(512) void custom_ar_rmsnorm_kernel(
     bf16_t* __restrict__ normed, bf16_t* __restrict__ residual, const bf16_t* __restrict__ in,
     const bf16_t* __restrict__ w, ArPeers P, int rank, int world, int rows, int H, float eps,
-    int gemma, int64_t stage_elems, int rows_per_block) {
+    int gemma, int64_t stage_elems, int rows_per_block, int64_t chunk) {
   __shared__ uint64_t s_epoch;
   __shared__ float s_red[16];
   const int b = blockIdx.x, tid = threadIdx.x;
@@ -222,7 +225,8 @@ __global__ __launch_bounds__(512) void custom_ar_rmsnorm_kernel(
   const int r0 = b * rows_per_block;
   const int r1 = min(rows, r0 + rows_per_block);
   const int64_t c0 = (int64_t)r0 * hv, c1 = (int64_t)r1 * hv;
-  bf16x8* my_stage = reinterpret_cast<bf16x8*>(mine + buf_off);
+  const int64_t s0 = (int64_t)b * chunk - c0;  // staging index = element index + s0
+  bf16x8* my_stage = reinterpret_cast<bf16x8*>(mine + buf_off) + s0;
   const bf16x8* src = reinterpret_cast<const bf16x8*>(in);
   for (int64_t i = c0 + tid; i < c1; i += blockDim.x) my_stage[i] = src[i];
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -238,7 +242,7 @@ __global__ __launch_bounds__(512) void custom_ar_rmsnorm_kernel(
       const int64_t i = (int64_t)row * hv + j;
       float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
       for (int q = 0; q < world; ++q) {
-        const bf16x8 v = reinterpret_cast<const bf16x8*>(P.base[q] + buf_off)[i];
+        const bf16x8 v = reinterpret_cast<const bf16x8*>(P.base[q] + buf_off)[i + s0];
 #pragma unroll
         for (int e = 0; e < 8; ++e) acc[e] += bf2f(v[e]);
       }
@@ -288,7 +292,7 @@ int launch_custom_ar_rmsnorm(void* normed, void* residual, const void* in, const
   if (nb > kArMaxBlocks) return -1;
   hipLaunchKernelGGL(custom_ar_rmsnorm_kernel, dim3(nb), dim3(512), 0, st, (bf16_t*)normed,
                      (bf16_t*)residual, (const bf16_t*)in, (const bf16_t*)w, peers, rank, world,
-                     rows, H, eps, gemma, stage_elems, rpb);
+                     rows, H, eps, gemma, stage_elems, rpb, chunk);
   return (int)hipGetLastError();
 }
 

@@ -686,6 +686,8 @@ int cfg_epi() {
 
 int64_t gemm_workspace_bytes(int64_t M, int64_t N, int splitk) {
   const int64_t tiles = ((M + kTM - 1) / kTM) * ((N + kTN - 1) / kTN);
+  // (the 8-wave slab: 32 f32x4 per thread x 512 threads; gemm_w4's is 64 x 256, the same
+  // 256 KiB per tile and slice)
   return splitk > 1 ? tiles * splitk * 32ll * kThreads * 16 : 0;
 }
 
@@ -694,6 +696,9 @@ int launch_gemm(void* c, const void* a, const void* b, const void* r, int M, int
                 int group_m, void* slab, int64_t slab_bytes, int* counters, int n_counters,
                 hipStream_t st) {
   // shape contract (checked here so a bad call never reaches the device)
+  if (variant == 7)
+    return launch_gemm_w4(c, a, b, r, M, N, K, lda, ldb, ldc, ldr, epi, up_off, splitk, group_m,
+                          slab, slab_bytes, counters, n_counters, st);
   const bool glu = epi == EPI_SILU || epi == EPI_GELU;
   if (M <= 0 || N <= 0 || K <= 0 || K % kBK || splitk < 1 || (K / kBK) % splitk) return -1;
   if (glu ? (N % (kTN / 2)) : (N % kTN)) return -1;

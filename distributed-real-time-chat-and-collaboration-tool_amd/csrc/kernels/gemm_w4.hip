@@ -1,0 +1,450 @@
+// Hand-scheduled 4-wave CDNA4 (gfx950) bf16 GEMM for the projection layers:
+//
+//   C[M, N] = epi( A[M, K] . B[N, K]^T )      (A activations, B weights, both K-contiguous)
+//
+// epilogues as gemm.hip: store / + residual (may alias C) / SiLU- or GELU-gated [gate; up].
+// This is the GEMM of the engine's prefill and full-batch decode passes (replacing the model
+// hop of ref llm_server/llm_server.py:231 / :287 with on-node compute).
+//
+// Why a second GEMM: the 8-wave kernels of gemm.hip (2 waves per SIMD, 128 x 64 per wave)
+// reach 0.76-0.81x of hipBLASLt on the Llama shapes (profiles/r2a_hand_gemm.md): the PMC
+// pass shows them parked at barriers (SQ_WAIT_ANY 9x the library's) and issuing 1.5x the LDS
+// reads per MFMA.  This kernel uses the layout that reads the least LDS per FLOP - one wave
+// per SIMD, 128 x 128 outputs per wave (64 MFMA 16x16x32 tiles = 256 accumulator registers,
+// the AGPR half of the unified file) - and hides every latency INSIDE the wave with an
+// explicit instruction schedule instead of a partner wave:
+//
+//   * LDS: 2 stages x [A 256 rows | B 256 rows] x 128 B (one 64-deep K tile) = 128 KiB, filled
+//     by LDS-DMA (buffer_load_dwordx4 ... lds, 1 KiB = 8 rows per wave-instruction), the
+//     16-B chunk of row r stored at chunk ^ ((r >> 1) & 7): conflict-free ds_read_b128 for
+//     the MFMA lane groups (the XOR is applied to the per-lane DMA SOURCE address and to the
+//     read address - the two sides of one involution).
+//   * Registers: the fragments of a whole K tile (both 32-deep halves, A and B: 128 VGPRs),
+//     so a stage is released as soon as its reads are in registers - the DMA of tile t + 2
+//     goes into the stage of tile t while tile t's MFMAs still run (two tiles in flight).
+//   * Per K tile (128 MFMAs) a fixed order, pinned with sched_barrier:
+//       MFMA   0- 21  half 0 | ds_read of B half 1 (tile t)
+//       [lgkmcnt(0), barrier 1: B region of stage t free]
+//       MFMA  22- 57  half 0 | ds_read of A half 1 (tile t) + 8 DMA of B (tile t+2), one per 4 MFMA
+//       [lgkmcnt(0), barrier 2: A region free]
+//       MFMA  58-103  half 0/1 | 8 DMA of A (tile t+2)
+//       [vmcnt(16): own DMA of tile t+1 landed; barrier 3: everyone's]
+//       MFMA 104-127  half 1 | 16 ds_read of half 0 of tile t+1
+//     Three barriers per K tile, each in the middle of an MFMA stream.
+//   * B rows permuted on their way into LDS (fragment j, fragment row l <- tile row 8 l + j),
+//     so a lane's accumulators over the 8 B fragments are 8 consecutive output columns: the
+//     epilogue stores 16 B per lane (4 rows x 256 contiguous bytes per instruction), and a
+//     gated tile pairs gate fragment j with up fragment j + 4 of the same columns in a lane.
+//   * XCD-aware, row-grouped tile order; split-K with an fp32 slab and an in-launch combine
+//     by the last arriving slice (agent-scope release / acquire ticket) for short-M shapes.
+#include "common.h"
+#include "launchers.h"
+
+#include <utility>
+
+namespace drtc {
+namespace {
+
+typedef __attribute__((address_space(3))) void* w4_lds_ptr;
+
+constexpr int kW4Threads = 256;
+constexpr int kW4Stage = 65536;  // bytes: [A 256 rows | B 256 rows] x 128 B
+constexpr int kW4BOff = 32768;   // B region within a stage
+constexpr int kW4Lds = 2 * kW4Stage;
+
+enum { W4_STORE = 0, W4_RESIDUAL = 1, W4_SILU = 2, W4_GELU = 3 };
+
+struct W4Params {
+  bf16_t* c;
+  const bf16_t* a;
+  const bf16_t* b;
+  const bf16_t* r;
+  float* slab;
+  int* counters;
+  int M, N, K;  // N = columns of C
+  int lda, ldb, ldc, ldr;
+  int tiles_m, tiles_n, splitk, kt_split;
+  int up_off;
+  int group_m;
+};
+
+template <int EPI>
+DRTC_DEVICE constexpr bool w4_glu() { return EPI == W4_SILU || EPI == W4_GELU; }
+
+// One LDS-DMA wave-instruction: 64 lanes x 16 B from rsrc + voff + soff into LDS bytes
+// [dst, dst + 1024).  Inline asm (hipcc would pin vmcnt / lgkmcnt waits around a builtin
+// form it cannot order against the ds_reads); M0 is written and restored in the statement.
+DRTC_DEVICE void w4_dma(unsigned dst, unsigned voff, __amdgpu_buffer_rsrc_t rsrc, unsigned soff) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
+      "buffer_load_dwordx4 %2, %3, %4 offen lds\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "s"(dst), "v"(voff), "s"(rsrc), "s"(soff)
+      : "memory");
+}
+
+template <int N>
+DRTC_DEVICE void w4_vmcnt() {
+  constexpr int imm = (N & 0xF) | (0x7 << 4) | (0xF << 8) | ((N >> 4) << 14);
+  __builtin_amdgcn_s_waitcnt(imm);
+}
+DRTC_DEVICE void w4_lgkm0() { __builtin_amdgcn_s_waitcnt(0xC07F); }
+DRTC_DEVICE void w4_barrier() {
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+DRTC_DEVICE bf16x8 w4_rd(const char* lds, int off) {
+  return *reinterpret_cast<const bf16x8*>(lds + off);
+}
+
+// Per-wave DMA plan: A rows of instruction i are 32 i + 8 wv + (lane >> 3) of the tile
+// (clamped to the last valid row: one VGPR offset per instruction), B rows 32 i / 16 i
+// (gated) apart (one VGPR offset + scalar steps).
+struct W4Dma {
+  __amdgpu_buffer_rsrc_t ra, rb;
+  unsigned va[8];
+  unsigned vb;
+  unsigned sb[8];     // byte offset of B instruction s (beyond the per-lane row)
+  unsigned lds_a, lds_b;  // LDS byte address of this wave's first block in stage 0
+};
+
+// Per-tile state handed to every step of the unrolled schedule.
+struct W4Tile {
+  const char* lds;
+  int cur, nxt;        // byte offsets of this tile's stage and the next tile's
+  int ra0, ra1, rb0, rb1;
+  unsigned kb;         // K byte offset of tile t + 2 (its DMA goes into stage `cur`)
+};
+
+// Step Q (0..127) of a K tile: MFMA Q, then the memory work scheduled behind it.  Every
+// condition is a compile-time constant (the tile is a fold over Q), so the emitted stream is
+// straight-line, and sched_barrier(0) pins it in this order.
+template <bool DMA, bool NEXT, int Q>
+DRTC_DEVICE void w4_step(f32x4 (&acc)[8][8], bf16x8 (&fa0)[8], bf16x8 (&fb0)[8],
+                         bf16x8 (&fa1)[8], bf16x8 (&fb1)[8], const W4Tile& T, const W4Dma& d) {
+  constexpr int i = (Q >> 3) & 7, j = Q & 7;
+  if constexpr (Q < 64)
+    acc[i][j] = mfma16(fa0[i], fb0[j], acc[i][j]);
+  else
+    acc[i][j] = mfma16(fa1[i], fb1[j], acc[i][j]);
+  // ---- B half 1 of this tile (consumed from MFMA 64 on)
+  if constexpr (Q < 16 && (Q & 1) == 0) fb1[Q >> 1] = w4_rd(T.lds, T.cur + T.rb1 + 2048 * (Q >> 1));
+  if constexpr (Q == 21) {
+    w4_lgkm0();
+    w4_barrier();  // every wave's B reads of this stage are done
+  }
+  // ---- A half 1 of this tile, interleaved with the B DMA of tile t + 2
+  if constexpr (Q >= 22 && Q < 38 && ((Q - 22) & 3) < 2) {
+    constexpr int a = ((Q - 22) >> 2) * 2 + ((Q - 22) & 1);
+    fa1[a] = w4_rd(T.lds, T.cur + T.ra1 + 2048 * a);
+  }
+  if constexpr (DMA && Q >= 24 && Q <= 52 && ((Q - 24) & 3) == 0) {
+    constexpr int s = (Q - 24) >> 2;
+    w4_dma(d.lds_b + T.cur + 4096 * s, d.vb, d.rb, T.kb + d.sb[s]);
+  }
+  if constexpr (Q == 57) {
+    w4_lgkm0();
+    w4_barrier();  // every wave's A reads of this stage are done
+  }
+  if constexpr (DMA && Q >= 60 && Q <= 88 && ((Q - 60) & 3) == 0) {
+    constexpr int s = (Q - 60) >> 2;
+    w4_dma(d.lds_a + T.cur + 4096 * s, d.va[s], d.ra, T.kb);
+  }
+  if constexpr (NEXT && Q == 103) {
+    if constexpr (DMA)
+      w4_vmcnt<16>();
+    else
+      w4_vmcnt<0>();
+    w4_barrier();  // tile t + 1 landed for every wave
+  }
+  // ---- half 0 of tile t + 1: fa0[0], fb0[0..7], fa0[1..7]
+  if constexpr (NEXT && Q >= 104 && Q < 120) {
+    constexpr int r = Q - 104;
+    if constexpr (r == 0)
+      fa0[0] = w4_rd(T.lds, T.nxt + T.ra0);
+    else if constexpr (r <= 8)
+      fb0[r - 1] = w4_rd(T.lds, T.nxt + T.rb0 + 2048 * (r - 1));
+    else
+      fa0[r - 8] = w4_rd(T.lds, T.nxt + T.ra0 + 2048 * (r - 8));
+  }
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+template <bool DMA, bool NEXT, int... Qs>
+DRTC_DEVICE void w4_steps(std::integer_sequence<int, Qs...>, f32x4 (&acc)[8][8],
+                          bf16x8 (&fa0)[8], bf16x8 (&fb0)[8], bf16x8 (&fa1)[8],
+                          bf16x8 (&fb1)[8], const W4Tile& T, const W4Dma& d) {
+  (w4_step<DMA, NEXT, Qs>(acc, fa0, fb0, fa1, fb1, T, d), ...);
+}
+
+template <bool DMA, bool NEXT>
+DRTC_DEVICE void w4_tile(f32x4 (&acc)[8][8], bf16x8 (&fa0)[8], bf16x8 (&fb0)[8],
+                         bf16x8 (&fa1)[8], bf16x8 (&fb1)[8], const char* lds, int cur, int ra0,
+                         int ra1, int rb0, int rb1, const W4Dma& d, int t2) {
+  const W4Tile T{lds, cur, cur ^ kW4Stage, ra0, ra1, rb0, rb1, (unsigned)t2 * 128u};
+  w4_steps<DMA, NEXT>(std::make_integer_sequence<int, 128>{}, acc, fa0, fb0, fa1, fb1, T, d);
+}
+
+// acc[i][j][r] = C[row 128 wm + 16 i + 4 g + r][column of B fragment j, row l16]: lane l16
+// holds columns 8 l16 + j (j = 0..7) of its 4 rows -> one 16-B store per (i, r); a store
+// instruction writes 4 rows x 256 contiguous bytes.
+template <int EPI>
+DRTC_DEVICE void w4_epilogue(const W4Params& p, f32x4 (&acc)[8][8], int tm, int tn, int wm,
+                             int wn, int l16, int g) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = 256 * tm + 128 * wm + 16 * i + 4 * g + r;
+      if (m >= p.M) continue;
+      bf16_t* crow = p.c + (int64_t)m * p.ldc;
+      if constexpr (w4_glu<EPI>()) {
+        const int n = 128 * tn + 64 * wn + 4 * l16;
+        bf16x4 o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          o[j] = f2bf(act_value<EPI == W4_SILU ? 0 : 1>(acc[i][j][r]) * acc[i][j + 4][r]);
+        *reinterpret_cast<bf16x4*>(crow + n) = o;
+      } else {
+        const int n = 256 * tn + 128 * wn + 8 * l16;
+        bf16x8 o;
+        if constexpr (EPI == W4_RESIDUAL) {
+          const bf16x8 rv = *reinterpret_cast<const bf16x8*>(p.r + (int64_t)m * p.ldr + n);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] = f2bf(acc[i][j][r] + bf2f(rv[j]));
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] = f2bf(acc[i][j][r]);
+        }
+        *reinterpret_cast<bf16x8*>(crow + n) = o;
+      }
+    }
+  }
+}
+
+// Split-K: publish this slice's fp32 partial tile, draw a ticket; the last arriver adds every
+// other slice's partials (cdna_hip_programming.md §5 'Projection GEMM at M = 256' item 2).
+DRTC_DEVICE bool w4_splitk(const W4Params& p, f32x4 (&acc)[8][8], int tile, int slice,
+                           char* lds) {
+  const int tid = threadIdx.x;
+  const int64_t per_slice = 64ll * kW4Threads;  // f32x4 elements (256 KiB)
+  f32x4* mine = reinterpret_cast<f32x4*>(p.slab) + ((int64_t)tile * p.splitk + slice) * per_slice;
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) mine[(i * 8 + j) * kW4Threads + tid] = acc[i][j];
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  int* flag = reinterpret_cast<int*>(lds);
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int t = __hip_atomic_fetch_add(p.counters + tile, 1, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+    const int last = (t == p.splitk - 1);
+    if (last) {
+      __hip_atomic_store(p.counters + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    *flag = last;
+  }
+  __syncthreads();
+  if (!*flag) return false;
+  const f32x4* base = reinterpret_cast<const f32x4*>(p.slab) + (int64_t)tile * p.splitk * per_slice;
+  for (int s = 0; s < p.splitk; ++s) {
+    if (s == slice) continue;
+    const f32x4* src = base + s * per_slice;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[i][j] += src[(i * 8 + j) * kW4Threads + tid];
+  }
+  return true;
+}
+
+template <int EPI>
+__global__ __launch_bounds__(kW4Threads, 1) void gemm_w4_kernel(W4Params p) {
+  extern __shared__ __attribute__((aligned(16))) char w4_lds[];
+  // ---- tile assignment: XCD remap (bijective), split-K slice fastest, grouped rows
+  const int nwg = gridDim.x, orig = blockIdx.x;
+  const int xcd = orig & 7, qq = nwg >> 3, rmd = nwg & 7;
+  const int wgid = (xcd < rmd ? xcd * (qq + 1) : rmd * (qq + 1) + (xcd - rmd) * qq) + (orig >> 3);
+  const int slice = wgid % p.splitk;
+  const int tt = wgid / p.splitk;
+  const int gsize = p.group_m * p.tiles_n;
+  const int first_m = (tt / gsize) * p.group_m;
+  const int gm = min(p.tiles_m - first_m, p.group_m);
+  const int tm = first_m + (tt % gsize) % gm;
+  const int tn = (tt % gsize) / gm;
+  const int tile = tm * p.tiles_n + tn;
+
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wv >> 1, wn = wv & 1, l16 = lane & 15, g = lane >> 4;
+  const int k_base = slice * p.kt_split * 64;
+  const int nk = p.kt_split;
+
+  // ---- DMA plan
+  W4Dma d;
+  const unsigned lds0 = (unsigned)(uintptr_t)(w4_lds_ptr)w4_lds;
+  {
+    const int r8 = lane >> 3;
+    const int chunk = (lane & 7) ^ ((4 * wv + (lane >> 4)) & 7);  // logical chunk of this lane
+    const int rows_a = min(256, p.M - 256 * tm);
+    const bf16_t* abase = p.a + (int64_t)(256 * tm) * p.lda + k_base;
+    d.ra = __builtin_amdgcn_make_buffer_rsrc((void*)abase, (short)0, 0x7FFFFFFF, 0x00020000);
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      const int row = min(32 * s + 8 * wv + r8, rows_a - 1);
+      d.va[s] = (unsigned)(row * p.lda * 2 + chunk * 16);
+    }
+    // B rows are permuted on the way into LDS: LDS row 128 h + 16 j + l (wave column half h,
+    // fragment j, fragment row l) holds tile weight row 128 h + 8 l + j, so lane l16 of the
+    // MFMA output holds the 8 CONSECUTIVE columns 8 l16 .. 8 l16 + 7 over j = 0..7 (16-B
+    // epilogue stores).  Gated tiles: 64 output columns per half, fragments j < 4 the gate
+    // rows and j + 4 the up rows of columns 4 l + j.  DMA instruction s of wave wv fills LDS
+    // rows 32 s + 8 wv + r8, i.e. h = s >> 2, j = 2 (s & 3) + (wv >> 1), l = 8 (wv & 1) + r8.
+    const bf16_t* bbase;
+    int brow;
+    if constexpr (w4_glu<EPI>()) {
+      bbase = p.b + (int64_t)(128 * tn) * p.ldb + k_base;
+      brow = 32 * (wv & 1) + 4 * r8 + (wv >> 1);
+#pragma unroll
+      for (int s = 0; s < 8; ++s)
+        d.sb[s] = (unsigned)((64 * (s >> 2) + 2 * (s & 1) + ((s & 3) >= 2 ? p.up_off : 0)) *
+                             p.ldb * 2);
+    } else {
+      bbase = p.b + (int64_t)(256 * tn) * p.ldb + k_base;
+      brow = 64 * (wv & 1) + 8 * r8 + (wv >> 1);
+#pragma unroll
+      for (int s = 0; s < 8; ++s) d.sb[s] = (unsigned)((128 * (s >> 2) + 2 * (s & 3)) * p.ldb * 2);
+    }
+    d.rb = __builtin_amdgcn_make_buffer_rsrc((void*)bbase, (short)0, 0x7FFFFFFF, 0x00020000);
+    d.vb = (unsigned)(brow * p.ldb * 2 + chunk * 16);
+    d.lds_a = __builtin_amdgcn_readfirstlane(lds0 + 8 * wv * 128);
+    d.lds_b = __builtin_amdgcn_readfirstlane(lds0 + kW4BOff + 8 * wv * 128);
+  }
+  // fragment read offsets (bytes within a stage): row 128 w + l16 (+ 16 per fragment), the
+  // 16-B chunk 4 h + g stored at chunk ^ ((row >> 1) & 7)
+  const int fx = (l16 >> 1) & 7;
+  const int ra0 = (128 * wm + l16) * 128 + ((0 + g) ^ fx) * 16;
+  const int ra1 = (128 * wm + l16) * 128 + ((4 + g) ^ fx) * 16;
+  const int rb0 = kW4BOff + (128 * wn + l16) * 128 + ((0 + g) ^ fx) * 16;
+  const int rb1 = kW4BOff + (128 * wn + l16) * 128 + ((4 + g) ^ fx) * 16;
+  const char* lds = w4_lds;
+
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  // ---- prologue: tiles 0 and 1 into stages 0 and 1
+#pragma unroll
+  for (int s = 0; s < 8; ++s) w4_dma(d.lds_b + 4096 * s, d.vb, d.rb, d.sb[s]);
+#pragma unroll
+  for (int s = 0; s < 8; ++s) w4_dma(d.lds_a + 4096 * s, d.va[s], d.ra, 0u);
+  if (nk > 1) {
+#pragma unroll
+    for (int s = 0; s < 8; ++s)
+      w4_dma(d.lds_b + kW4Stage + 4096 * s, d.vb, d.rb, 128u + d.sb[s]);
+#pragma unroll
+    for (int s = 0; s < 8; ++s) w4_dma(d.lds_a + kW4Stage + 4096 * s, d.va[s], d.ra, 128u);
+    w4_vmcnt<16>();
+  } else {
+    w4_vmcnt<0>();
+  }
+  w4_barrier();
+  bf16x8 fa0[8], fb0[8], fa1[8], fb1[8];
+  fa0[0] = w4_rd(lds, ra0);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) fb0[j] = w4_rd(lds, rb0 + 2048 * j);
+#pragma unroll
+  for (int i = 1; i < 8; ++i) fa0[i] = w4_rd(lds, ra0 + 2048 * i);
+
+  // One loop body for every tile (a single straight-line schedule keeps the 256 accumulators
+  // in place in the AGPRs): the last two tiles re-stage the final tile (kb clamped: valid
+  // bytes, never read) and the last one reads stale fragments it never uses.
+  for (int t = 0; t < nk; ++t)
+    w4_tile<true, true>(acc, fa0, fb0, fa1, fb1, lds, (t & 1) * kW4Stage, ra0, ra1, rb0, rb1, d,
+                        min(t + 2, nk - 1));
+  w4_vmcnt<0>();  // no LDS-DMA may still be landing when the workgroup leaves
+
+  if (p.splitk > 1) {
+    __syncthreads();
+    if (!w4_splitk(p, acc, tile, slice, w4_lds)) return;
+  }
+  w4_epilogue<EPI>(p, acc, tm, tn, wm, wn, l16, g);
+}
+
+template <int EPI>
+int w4_launch(const W4Params& p, hipStream_t st) {
+  const int nwg = p.tiles_m * p.tiles_n * p.splitk;
+  hipLaunchKernelGGL((gemm_w4_kernel<EPI>), dim3(nwg), dim3(kW4Threads), kW4Lds, st, p);
+  return (int)hipGetLastError();
+}
+
+}  // namespace
+
+int launch_gemm_w4(void* c, const void* a, const void* b, const void* r, int M, int N, int K,
+                   int lda, int ldb, int ldc, int ldr, int epi, int up_off, int splitk,
+                   int group_m, void* slab, int64_t slab_bytes, int* counters, int n_counters,
+                   hipStream_t st) {
+  // shape contract (checked here so a bad call never reaches the device)
+  const bool glu = epi == W4_SILU || epi == W4_GELU;
+  if (M <= 0 || N <= 0 || K <= 0 || K % 64 || splitk < 1 || (K / 64) % splitk) return -1;
+  if (glu ? (N % 128 || up_off != N) : (N % 256)) return -1;
+  if (lda % 8 || ldb % 8 || (glu ? ldc % 4 : ldc % 8)) return -1;
+  if (epi == W4_RESIDUAL && (ldr % 8 || r == nullptr || (uintptr_t)r % 16)) return -1;
+  if ((uintptr_t)a % 16 || (uintptr_t)b % 16 || (uintptr_t)c % (glu ? 8 : 16)) return -1;
+  // 32-bit buffer offsets: every staged row must sit within 2 GiB of its operand base
+  if ((int64_t)min(M, 256) * lda * 2 >= (1ll << 31)) return -1;
+  if ((int64_t)(glu ? up_off + 128 : 256) * ldb * 2 >= (1ll << 31)) return -1;
+  if (group_m < 1) group_m = 8;
+  W4Params p{};
+  p.c = (bf16_t*)c;
+  p.a = (const bf16_t*)a;
+  p.b = (const bf16_t*)b;
+  p.r = (const bf16_t*)r;
+  p.M = M; p.N = N; p.K = K;
+  p.lda = lda; p.ldb = ldb; p.ldc = ldc; p.ldr = ldr;
+  p.tiles_m = (M + 255) / 256;
+  p.tiles_n = glu ? N / 128 : N / 256;
+  p.splitk = splitk;
+  p.kt_split = K / 64 / splitk;
+  p.up_off = up_off;
+  p.group_m = group_m;
+  if (splitk > 1) {
+    const int64_t tiles = (int64_t)p.tiles_m * p.tiles_n;
+    if (slab == nullptr || counters == nullptr || n_counters < tiles ||
+        slab_bytes < tiles * splitk * 64ll * kW4Threads * 16)
+      return -2;
+    p.slab = (float*)slab;
+    p.counters = counters;
+  }
+  switch (epi) {
+    case W4_STORE: return w4_launch<W4_STORE>(p, st);
+    case W4_RESIDUAL: return w4_launch<W4_RESIDUAL>(p, st);
+    case W4_SILU: return w4_launch<W4_SILU>(p, st);
+    case W4_GELU: return w4_launch<W4_GELU>(p, st);
+    default: return -1;
+  }
+}
+
+int configure_gemm_w4() {
+  int e = 0;
+  e |= (int)hipFuncSetAttribute((const void*)gemm_w4_kernel<W4_STORE>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, kW4Lds);
+  e |= (int)hipFuncSetAttribute((const void*)gemm_w4_kernel<W4_RESIDUAL>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, kW4Lds);
+  e |= (int)hipFuncSetAttribute((const void*)gemm_w4_kernel<W4_SILU>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, kW4Lds);
+  e |= (int)hipFuncSetAttribute((const void*)gemm_w4_kernel<W4_GELU>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, kW4Lds);
+  return e;
+}
+
+}  // namespace drtc

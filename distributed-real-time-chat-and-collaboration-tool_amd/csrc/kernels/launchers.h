@@ -102,6 +102,13 @@ int launch_gemm(void* c, const void* a, const void* b, const void* r, int M, int
                 int group_m, void* slab, int64_t slab_bytes, int* counters, int n_counters,
                 hipStream_t st);
 int64_t gemm_workspace_bytes(int64_t M, int64_t N, int splitk);
+// 4-wave hand-scheduled GEMM (gemm_w4.hip): same contract as launch_gemm (gated: up_off == N);
+// launch_gemm variant 7 routes here.  Split-K slabs: 256 KiB per tile and slice.
+int launch_gemm_w4(void* c, const void* a, const void* b, const void* r, int M, int N, int K,
+                   int lda, int ldb, int ldc, int ldr, int epi, int up_off, int splitk,
+                   int group_m, void* slab, int64_t slab_bytes, int* counters, int n_counters,
+                   hipStream_t st);
+int configure_gemm_w4();
 
 // Raise the dynamic-LDS ceiling of the kernels that need > 64 KiB (head_dim
 // 256).  Called once at import, before any graph capture.

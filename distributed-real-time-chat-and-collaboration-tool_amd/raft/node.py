@@ -255,8 +255,19 @@ class RaftRuntime:
                 t0 = time.perf_counter()
                 files = self.state.encode(self.dir, list(self.state.FILES) if all_files else None)
                 held = time.perf_counter() - t0
-            for path, data in files:
-                pickle_compat.write_bytes(data, path)
+            names = {os.path.join(self.dir, f): w for w, f in self.state.FILES.items()}
+            for k, (path, data) in enumerate(files):
+                try:
+                    pickle_compat.write_bytes(data, path)
+                except BaseException:
+                    # disk full / I/O error: encode() marked these files clean, so mark
+                    # this one and every one not yet written dirty again (the next persist
+                    # retries them instead of leaving them stale until an unrelated change)
+                    with self.state_lock:
+                        for p2, _ in files[k:]:
+                            if p2 in names:
+                                self.state.dirty.add(names[p2])
+                    raise
         return held
 
     # ------------------------------------------------------------ apply

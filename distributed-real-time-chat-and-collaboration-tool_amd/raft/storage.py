@@ -18,7 +18,12 @@ is made durable with ONE fdatasync before the append returns (group commit:
 an AppendEntries batch or a leader proposal is acknowledged only after it),
 and a change of ``current_term`` / ``voted_for`` is fsynced (file + directory)
 before a vote is answered.  ``commit_index`` / ``last_applied`` are
-recomputable and written without a sync.
+recomputable and written without a sync.  NativeStorage keeps the hard state
+(term, vote) in a file of its own, ``raft_hardstate_port_{port}.pkl``, rewritten
+(and fsynced) only when it changes: the reference-format state pickle, which is
+also rewritten on every commit_index change without a sync, can then come back
+empty or stale after a power loss without undoing a vote (the term and vote are
+taken from the hard-state file when it is at least as new).
 
 Crash consistency of the reference-format PAIR: the state pickle is written
 on every state change but its ``commit_index`` / ``last_applied`` are
@@ -58,7 +63,10 @@ class _StateFile:
     def load(self) -> dict:
         st = {"current_term": 0, "voted_for": None, "commit_index": -1, "last_applied": -1}
         if os.path.exists(self.path):
-            st.update(pickle_compat.safe_load(self.path))
+            try:
+                st.update(pickle_compat.safe_load(self.path))
+            except Exception:  # torn / empty after a crash: the hard state lives elsewhere
+                pass
         return st
 
     def save(self, state: dict) -> None:
@@ -153,6 +161,7 @@ class NativeStorage:
         self.log_path = os.path.join(directory, f"raft_log_port_{port}.pkl")
         self.export_path = os.path.join(directory, f"raft_log_port_{port}.exported")
         self.state = _StateFile(os.path.join(directory, f"raft_state_port_{port}.pkl"), fsync)
+        self.hard_path = os.path.join(directory, f"raft_hardstate_port_{port}.pkl")
         self.snap = _SnapshotFile(os.path.join(directory, f"raft_snapshot_port_{port}.pkl"), fsync)
         pkg = __name__.rsplit(".", 2)[0]
         self._native = importlib.import_module(pkg + "._native")
@@ -211,8 +220,20 @@ class NativeStorage:
                 out.append((int(mid[2:]), os.path.join(self.dir, f)))
         return sorted(out)
 
+    def _load_hard(self):
+        if not os.path.exists(self.hard_path):
+            return None
+        try:
+            d = pickle_compat.safe_load(self.hard_path)
+            return int(d["current_term"]), d["voted_for"]
+        except Exception:  # never fsync-acknowledged if torn: the previous vote stands
+            return None
+
     def load(self):
         st = self.state.load()
+        hard = self._load_hard()
+        if hard is not None and hard[0] >= int(st.get("current_term") or 0):
+            st["current_term"], st["voted_for"] = hard
         snap = self.snap.load()
         st["snap_index"], st["snap_term"] = (snap[0], snap[1]) if snap else (-1, 0)
         skip = st["snap_index"] + 1 - self.base  # entries the snapshot already covers
@@ -284,10 +305,11 @@ class NativeStorage:
                "commit_index": min(int(st["commit_index"]), clamp),
                "last_applied": min(int(st["last_applied"]), clamp)}
         hard = (st["current_term"], st["voted_for"])
-        durable = self.fsync and hard != self._durable  # term / vote: sync before replying
-        pickle_compat.dump(ref, self.state.path, durable)
-        if durable:
+        if hard != self._durable:  # term / vote changed: durable before the vote is answered
+            pickle_compat.dump({"current_term": hard[0], "voted_for": hard[1]}, self.hard_path,
+                               self.fsync)
             self._durable = hard
+        pickle_compat.dump(ref, self.state.path, False)
 
     # -- export of the reference-format log, in three steps so the runtime can
     # pickle a large log outside its consensus lock

@@ -302,11 +302,14 @@ class ChatNode:
         if not p:
             return raft_pb.StatusResponse(success=False, message="Invalid token")
         name = p["username"]
-        if self.rt.is_leader():
-            # replicated: the token stays invalid on every node and after failover
-            self._propose("REVOKE_TOKEN", {"username": name,
-                                           "token_hash": self._token_hash(request.token),
-                                           "exp": int(p.get("exp", 0)), "ts": int(time.time())})
+        # replicated through the leader, like every other write (the client redirects on
+        # "Not the leader"): the token then stays invalid on every node and after failover.
+        # A follower never revokes node-locally and reports success.
+        if not self.rt.is_leader():
+            return raft_pb.StatusResponse(success=False, message="Not the leader")
+        err = self._propose("REVOKE_TOKEN", {"username": name,
+                                             "token_hash": self._token_hash(request.token),
+                                             "exp": int(p.get("exp", 0)), "ts": int(time.time())})
         with self.rt.state_lock:
             self.sessions.pop(request.token, None)
             now = int(time.time())
@@ -319,6 +322,8 @@ class ChatNode:
                 u["status"] = "offline"
                 self.st.online_users.discard(name)
                 self.st.dirty.add("users")
+        if err:  # revoked on this node; the replicated revocation did not commit
+            return raft_pb.StatusResponse(success=False, message=f"Logout not replicated: {err}")
         return raft_pb.StatusResponse(success=True, message="Logged out")
 
     # ------------------------------------------------------------ channels
@@ -451,7 +456,7 @@ class ChatNode:
             err = self._propose("JOIN_CHANNEL", {"channel_id": cid, "user_id": p["user_id"]})
             if err:
                 return raft_pb.StatusResponse(success=False, message=err)
-        msg = {"id": self._write_id(request), "sender_id": p["user_id"],
+        msg = {"id": self._write_id(request, p["user_id"]), "sender_id": p["user_id"],
                "sender_name": p["username"], "channel_id": cid, "content": request.content,
                "timestamp": int(time.time() * 1000)}
         err = self._propose("SEND_MESSAGE", msg)
@@ -459,14 +464,20 @@ class ChatNode:
             return raft_pb.StatusResponse(success=False, message=err)
         return raft_pb.StatusResponse(success=True, message="Message sent")
 
-    @staticmethod
-    def _write_id(request) -> str:
-        """Record id of a write: the client's request_id when it sent one (a
-        retry then maps onto the same record and the apply de-duplicates
-        it), else a fresh uuid4 as in the reference."""
+    # namespace of the record ids derived from (sender, request_id)
+    _WRITE_NS = uuid.UUID("6f1c2d0e-9a57-4c1b-8e43-2b7d0c5a9e11")
+
+    @classmethod
+    def _write_id(cls, request, sender_id: str) -> str:
+        """Record id of a write.  With a client request_id it is
+        uuid5(sender_id, request_id): a retry of the same write by the same
+        user maps onto the same record (the apply de-duplicates it), while two
+        users that happen to pick the same request_id (counters, or an id
+        copied from GetMessages) get different records.  Without one: a fresh
+        uuid4 as in the reference (server/raft_node.py:1837)."""
         rid = getattr(request, "request_id", "")
         if rid and len(rid) <= 64:
-            return rid
+            return str(uuid.uuid5(cls._WRITE_NS, f"{sender_id}:{rid}"))
         return str(uuid.uuid4())
 
     @staticmethod
@@ -500,7 +511,7 @@ class ChatNode:
             if rec is None:
                 return raft_pb.StatusResponse(success=False, message="User not found")
             rid = rec["id"]
-        dm = {"id": self._write_id(request), "sender_id": p["user_id"], "sender_name": p["username"],
+        dm = {"id": self._write_id(request, p["user_id"]), "sender_id": p["user_id"], "sender_name": p["username"],
               "recipient_id": rid, "recipient_name": request.recipient_username,
               "content": request.content, "timestamp": int(time.time() * 1000), "is_read": False}
         err = self._propose("SEND_DM", dm)
@@ -562,7 +573,7 @@ class ChatNode:
             return raft_pb.FileUploadResponse(success=False, message="Invalid token")
         if not self.rt.is_leader():
             return raft_pb.FileUploadResponse(success=False, message="Not the leader")
-        fid = self._write_id(request)
+        fid = self._write_id(request, p["user_id"])
         mime = request.mime_type or mimetypes.guess_type(request.file_name)[0] or "application/octet-stream"
         data = {"file_id": fid, "name": request.file_name, "data": request.file_data.hex(),
                 "size": len(request.file_data), "mime_type": mime, "uploader_id": p["user_id"],

@@ -1,0 +1,81 @@
+#!/usr/bin/env python3
+"""Focused A/B probe of one GEMM shape: hipBLASLt (ops.linear / addmm_ beta=1) against the
+hand-written kernels of ops.gemm.mfma_gemm, interleaved in one process (rule 24), for
+rocprofv3 PMC passes and quick timing.
+
+  python scripts/w4_probe.py --shape 16384,6144,4096 --epi store --arms lib,v7 --iters 10
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import drtc_amd  # noqa: E402,F401
+from drtc_amd import ops  # noqa: E402
+from drtc_amd.ops import gemm as G  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--shape", default="16384,6144,4096", help="M,N,K (N = rows of W)")
+    ap.add_argument("--epi", default="store")
+    ap.add_argument("--arms", default="lib,v7")
+    ap.add_argument("--splitk", type=int, default=1)
+    ap.add_argument("--group-m", type=int, default=8)
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--rounds", type=int, default=5)
+    a = ap.parse_args()
+    M, N, K = (int(v) for v in a.shape.split(","))
+    dev = torch.device("cuda")
+    torch.manual_seed(0)
+    x = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
+    w = torch.randn(N, K, device=dev, dtype=torch.bfloat16) * 0.02
+    glu = a.epi in ("silu", "gelu_tanh")
+    nout = N // 2 if glu else N
+    res = torch.randn(M, nout, device=dev, dtype=torch.bfloat16) if a.epi == "residual" else None
+    out = torch.empty(M, nout, device=dev, dtype=torch.bfloat16)
+    G.gemm_workspace(dev)
+    fns = {}
+    for arm in a.arms.split(","):
+        if arm == "lib":
+            if a.epi == "residual":
+                fns[arm] = lambda: res.addmm_(x, w.t())
+            elif glu:
+                fns[arm] = lambda: ops.act_glu(ops.linear(x, w), a.epi)
+            else:
+                fns[arm] = lambda: ops.linear(x, w)
+        else:
+            v = int(arm[1:])
+            if a.epi == "residual":
+                fns[arm] = (lambda v=v: G.mfma_gemm(x, w, "residual", residual=res, out=res,
+                                                    variant=v, splitk=a.splitk, group_m=a.group_m))
+            else:
+                fns[arm] = (lambda v=v: G.mfma_gemm(x, w, a.epi, out=out, variant=v,
+                                                    splitk=a.splitk, group_m=a.group_m))
+    for f in fns.values():
+        f()
+    torch.cuda.synchronize()
+    times = {k: [] for k in fns}
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for _ in range(a.rounds):
+        for k, f in fns.items():
+            s.record()
+            for _ in range(a.iters):
+                f()
+            e.record()
+            e.synchronize()
+            times[k].append(s.elapsed_time(e) * 1e3 / a.iters)
+    fl = 2.0 * M * N * K
+    for k, ts in times.items():
+        med = statistics.median(ts)
+        print(json.dumps({"shape": [M, N, K], "epi": a.epi, "arm": k, "us_med": round(med, 1),
+                          "us_min": round(min(ts), 1), "TFLOPs": round(fl / med / 1e6, 1)}),
+              flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,7 +1,9 @@
 """Worker for test_custom_allreduce_gpu.py: one rank of a custom all-reduce
-group.  Every rank runs on cuda:0 (the test box has one GPU) - the IPC
-handle exchange, flag protocol and reduction are the same code path as
-across the GPUs of an xGMI hive."""
+group on device rank % device_count().  On a one-GPU box every rank shares
+cuda:0 (the IPC handle exchange, flag protocol and reduction are the same code
+path as across the GPUs of an xGMI hive); on a box with >= world GPUs each rank
+owns its own device, the peer mapping crosses xGMI (hipDeviceCanAccessPeer is
+asserted) and the custom sums are also checked against RCCL's all-reduce."""
 import os
 import sys
 
@@ -27,8 +29,15 @@ def expected(world, it, n):
 def main():
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    torch.cuda.set_device(0)
-    car = CustomAllReduce(dist.group.WORLD, torch.device("cuda", 0), max_bytes=4 << 20)
+    ndev = torch.cuda.device_count()
+    dev = rank % ndev
+    torch.cuda.set_device(dev)
+    distinct = ndev >= world
+    if distinct:  # one device per rank: every peer must be reachable over xGMI
+        for q in range(world):
+            if q != dev:
+                assert torch.cuda.can_device_access_peer(dev, q), f"no P2P {dev}->{q}"
+    car = CustomAllReduce(dist.group.WORLD, torch.device("cuda", dev), max_bytes=4 << 20)
     it = 0
     for n in (8, 4096, 8 * 1001, 8 * 12345, 1 << 20, 2 << 20):
         for mode in (None, False, True):  # by size / one-shot / two-shot, interleaved
@@ -63,8 +72,12 @@ def main():
             print(f"rank {rank}: graph mismatch it={it}", flush=True)
             sys.exit(4)
         it += 1
-    # fused all-reduce + residual add + RMSNorm (decode sublayer epilogue)
-    for rows, H, gemma in ((1, 4096, False), (7, 8192, True), (64, 2048, False)):
+    # fused all-reduce + residual add + RMSNorm (decode sublayer epilogue); H = 5120 does not
+    # divide a block's staging chunk, and plain calls interleave with the fused ones
+    for rows, H, gemma in ((1, 4096, False), (7, 8192, True), (64, 2048, False),
+                           (37, 5120, False), (5, 3072, True), (64, 5120, False)):
+        xp = data(rank, it + 500, 8 * 12345).cuda()
+        yp = car.all_reduce(xp)
         part = data(rank, it, rows * H).view(rows, H).cuda()
         res0 = data(99, it, rows * H).view(rows, H)
         w = (data(98, it, H) * 0.1 + 1.0).to(torch.bfloat16)
@@ -79,8 +92,11 @@ def main():
             print(f"rank {rank}: fused residual mismatch rows={rows}", flush=True)
             sys.exit(6)
         if (y.cpu().float() - ref).abs().max().item() > 0.02 * ref.abs().max().item():
-            print(f"rank {rank}: fused norm mismatch rows={rows}", flush=True)
+            print(f"rank {rank}: fused norm mismatch rows={rows} H={H}", flush=True)
             sys.exit(7)
+        if not torch.equal(yp.cpu(), expected(world, it + 500, 8 * 12345)):
+            print(f"rank {rank}: plain all-reduce beside the fused one H={H}", flush=True)
+            sys.exit(11)
         ys = [torch.empty_like(y.cpu()) for _ in range(world)]
         dist.all_gather(ys, y.cpu())
         if not all(torch.equal(ys[0], t) for t in ys):
@@ -115,6 +131,22 @@ def main():
             if not torch.equal(y.cpu(), expected(world, it, 4096)):
                 print(f"rank {rank}: mismatch after epoch {start}", flush=True)
                 sys.exit(10)
+            it += 1
+    if distinct:  # RCCL over the same devices: same sums to bf16 rounding of its own order
+        grp = dist.new_group(backend="nccl")
+        for n in (4096, 1 << 20):
+            x = data(rank, it, n).cuda()
+            y = car.all_reduce(x.clone())
+            dist.all_reduce(x, group=grp)
+            torch.cuda.synchronize()
+            want = expected(world, it, n)
+            if not torch.equal(y.cpu(), want):
+                print(f"rank {rank}: custom mismatch on distinct devices n={n}", flush=True)
+                sys.exit(12)
+            tol = 0.02 * want.float().abs().max().item()
+            if (x.cpu().float() - want.float()).abs().max().item() > tol:
+                print(f"rank {rank}: RCCL and the reference disagree n={n}", flush=True)
+                sys.exit(13)
             it += 1
     if car.error():
         print(f"rank {rank}: flag wait timed out", flush=True)

@@ -1,6 +1,7 @@
-"""Worker for test_expert_parallel_gpu.py: one rank of an EP group sharing the
-box's GPU (gloo; device tensors are staged through host memory by
-parallel/comm.py).  Local experts run on the fused HIP grouped-MFMA kernel."""
+"""Worker for test_expert_parallel_gpu.py: one rank of an EP group on device
+rank % device_count() (on a one-GPU box every rank shares it; gloo: device
+tensors are staged through host memory by parallel/comm.py).  Local experts run
+on the fused HIP grouped-MFMA kernel."""
 import os
 import sys
 
@@ -15,7 +16,7 @@ from drtc_amd.parallel.expert_parallel import ep_moe_forward  # noqa: E402
 def main():
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    torch.cuda.set_device(0)
+    torch.cuda.set_device(rank % torch.cuda.device_count())
     g = torch.Generator().manual_seed(11)
     E, H, I, k, T = 8, 256, 256, 2, 48
     router = (torch.randn(E, H, generator=g) * 0.2).to(torch.bfloat16).cuda()

@@ -82,3 +82,21 @@ def test_service_bench_open_loop_scripted():
     r = _json_line(p.stdout)
     assert r["load"].startswith("open-loop") and r["requests"] == 40 and r["errors"] == 0
     assert r["p99_latency_ms"] >= r["p50_latency_ms"] > 0
+
+
+def test_bench_self_launch_two_ranks():
+    """`python bench.py --gpus 2` with no torchrun: the script starts its two rank
+    processes itself (gloo here, RCCL on GPUs) and reports the whole-job value."""
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", *ARGS],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-2000:]
+    _check(_json_line(p.stdout), 2)
+
+
+def test_bench_world_size_mismatch_is_an_error():
+    env = dict(os.environ, RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", *ARGS],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode != 0 and not [ln for ln in p.stdout.splitlines() if ln.startswith("{")]

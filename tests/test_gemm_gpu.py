@@ -29,7 +29,7 @@ def _check(out, ref, tol=1.5e-2):
     assert err <= tol * max(scale, 1e-3), (err, scale)
 
 
-@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5])
+@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 7])
 @pytest.mark.parametrize("epi", ["store", "residual", "silu", "gelu_tanh"])
 @pytest.mark.parametrize("M,N,K,splitk", [(256, 256, 256, 1), (300, 512, 512, 2), (1, 768, 1024, 4),
                                           (1024, 1024, 2048, 2), (515, 256, 384, 3)])
@@ -44,7 +44,7 @@ def test_mfma_gemm_matches_fp32(hipk, variant, epi, M, N, K, splitk):
     _check(out, ref)
 
 
-@pytest.mark.parametrize("variant", [1, 5])
+@pytest.mark.parametrize("variant", [1, 5, 7])
 def test_mfma_gemm_residual_in_place_and_strided(hipk, variant):
     """o / down projection adding into the residual stream in place; x is a
     column slice of a wider buffer (row stride > K)."""
@@ -59,18 +59,19 @@ def test_mfma_gemm_residual_in_place_and_strided(hipk, variant):
     _check(h, ref)
 
 
-def test_mfma_gemm_graph_replay_splitk(hipk):
+@pytest.mark.parametrize("variant", [5, 7])
+def test_mfma_gemm_graph_replay_splitk(hipk, variant):
     """Split-K inside a hipGraph: counters are re-armed by each tile's last
     arriver, so replays with new inputs stay exact."""
     g = torch.Generator(device="cuda").manual_seed(3)
     x = torch.randn(512, 1024, device="cuda", dtype=torch.bfloat16, generator=g)
     w = torch.randn(768, 1024, device="cuda", dtype=torch.bfloat16, generator=g) * 0.05
     out = torch.empty(512, 768, device="cuda", dtype=torch.bfloat16)
-    G.mfma_gemm(x, w, out=out, variant=5, splitk=4)  # eager warm-up (workspace exists)
+    G.mfma_gemm(x, w, out=out, variant=variant, splitk=4)  # eager warm-up (workspace exists)
     torch.cuda.synchronize()
     gr = torch.cuda.CUDAGraph()
     with torch.cuda.graph(gr):
-        G.mfma_gemm(x, w, out=out, variant=5, splitk=4)
+        G.mfma_gemm(x, w, out=out, variant=variant, splitk=4)
     for i in range(3):
         x.copy_(torch.randn(512, 1024, device="cuda", dtype=torch.bfloat16, generator=g))
         gr.replay()

@@ -26,6 +26,7 @@ from drtc_amd.protos import RAFT_SERVICE, make_stub, raft_pb
 from drtc_amd.raft.core import Entry
 from drtc_amd.raft.state_machine import ChatState
 from drtc_amd.raft.storage import NativeStorage
+from drtc_amd.server.raft_service import ChatNode
 from drtc_amd.utils import pickle_compat
 from drtc_amd.utils.cluster import LocalCluster, free_port
 
@@ -172,9 +173,41 @@ def test_request_id_makes_writes_idempotent(cluster):
         assert s.SendDirectMessage(raft_pb.DirectMessageRequest(token=tok, recipient_username="bob",
                                                                 content="dm", request_id="req-43")).success
     msgs = s.GetMessages(raft_pb.GetMessagesRequest(token=tok, channel_id="general")).messages
-    assert [m.content for m in msgs].count("once") == 1 and msgs[-1].message_id == "req-42"
+    assert [m.content for m in msgs].count("once") == 1
+    assert msgs[-1].message_id == ChatNode._write_id(
+        raft_pb.SendMessageRequest(request_id="req-42"), "alice")
     dms = s.GetDirectMessages(raft_pb.GetDirectMessagesRequest(token=tok, other_username="bob")).messages
     assert len(dms) == 1
+
+
+def test_same_request_id_from_two_users_stores_both(cluster):
+    """request_id de-duplicates one user's retries only: another user's write
+    that carries the same request_id (a counter, or an id read back from
+    GetMessages) is a different record, and an upload returns its own file_id."""
+    L = cluster.leader()
+    s = cluster.stub(L)
+    ta, tb = cluster.login(L, "alice"), cluster.login(L, "bob")
+    for tok, text in ((ta, "from alice"), (tb, "from bob")):
+        assert s.SendMessage(raft_pb.SendMessageRequest(token=tok, channel_id="general", content=text,
+                                                        request_id="7")).success
+    msgs = s.GetMessages(raft_pb.GetMessagesRequest(token=ta, channel_id="general")).messages
+    got = [m.content for m in msgs]
+    assert got.count("from alice") == 1 and got.count("from bob") == 1
+    assert len({m.message_id for m in msgs}) == len(msgs)
+    # alice re-uses an id she can see (bob's message id) as her request_id: still her own record
+    bob_id = next(m.message_id for m in msgs if m.content == "from bob")
+    assert s.SendMessage(raft_pb.SendMessageRequest(token=ta, channel_id="general", content="copycat",
+                                                    request_id=bob_id[:64])).success
+    got = [m.content for m in s.GetMessages(raft_pb.GetMessagesRequest(token=ta, channel_id="general")).messages]
+    assert "copycat" in got and got.count("from bob") == 1
+    fa = s.UploadFile(raft_pb.FileUploadRequest(token=ta, file_name="a.txt", file_data=b"A",
+                                                channel_id="general", request_id="f1"))
+    fb = s.UploadFile(raft_pb.FileUploadRequest(token=tb, file_name="b.txt", file_data=b"B",
+                                                channel_id="general", request_id="f1"))
+    assert fa.success and fb.success and fa.file_id != fb.file_id
+    da = s.DownloadFile(raft_pb.FileDownloadRequest(token=ta, file_id=fa.file_id))
+    db = s.DownloadFile(raft_pb.FileDownloadRequest(token=tb, file_id=fb.file_id))
+    assert da.file_data == b"A" and db.file_data == b"B"
 
 
 def test_native_storage_reference_pair_never_ahead_of_log(tmp_path):
@@ -302,7 +335,7 @@ def test_sigkill_leader_mid_write_then_restart_from_disk(tmp_path):
                 except grpc.RpcError:
                     ok = False
                     break
-                ids = [m.message_id for m in ms]
+                ids = [m.content for m in ms]  # content = the write's request_id
                 if not want <= set(ids) or len(ids) != len(set(ids)):
                     ok = False
             time.sleep(0.2)
@@ -335,3 +368,59 @@ def test_persist_writes_app_state_outside_the_state_lock(cluster, monkeypatch):
     st = ChatState()
     st.load(rt.dir)
     assert [m["content"] for m in st.channel_messages[cid]] == [f"m{k}" for k in range(5)]
+
+
+def test_failed_persist_keeps_files_dirty(cluster, monkeypatch):
+    """encode() marks the files clean before they are written (outside the lock):
+    a write that fails (disk full, I/O error) must put its file - and every file
+    not written yet - back on the dirty list so the next persist retries it."""
+    L, cid = _workload(cluster)
+    rt = cluster.nodes[L].rt
+    rt.persist(all_files=True)
+    with rt.state_lock:
+        rt.state.dirty.update({"users", "messages"})
+    real = pickle_compat.write_bytes
+
+    def broken(data, path, fsync=False):
+        raise OSError(28, "No space left on device")
+
+    monkeypatch.setattr(pickle_compat, "write_bytes", broken)
+    with pytest.raises(OSError):
+        rt.persist()
+    with rt.state_lock:
+        assert {"users", "messages"} <= rt.state.dirty
+    monkeypatch.setattr(pickle_compat, "write_bytes", real)
+    rt.persist()
+    with rt.state_lock:
+        assert not ({"users", "messages"} & rt.state.dirty)
+
+
+def test_native_storage_vote_survives_torn_reference_state_file(tmp_path):
+    """term / vote live in their own fsynced hard-state file: the reference-format
+    state pickle (rewritten unsynced on every commit_index change) coming back
+    empty or stale after a power loss must not undo a vote."""
+    d = str(tmp_path)
+    st = NativeStorage(d, 5001, fsync=True)
+    st.load()
+    st.save_state({"current_term": 3, "voted_for": 2, "commit_index": -1, "last_applied": -1})
+    st.append([Entry(3, "NOOP", b"{}")])
+    for c in range(5):  # commit progress: no hard-state change, no sync
+        st.save_state({"commit_index": 0, "last_applied": 0})
+    st.close()
+    state_p = os.path.join(d, "raft_state_port_5001.pkl")
+    with open(state_p, "wb"):
+        pass  # torn: empty file
+    st2 = NativeStorage(d, 5001, fsync=True)
+    s, log = st2.load()
+    assert s["current_term"] == 3 and s["voted_for"] == 2 and len(log) == 1
+    st2.close()
+    # stale: an older term in the reference pickle, the newer vote in the hard state
+    pickle_compat.dump({"current_term": 1, "voted_for": None, "commit_index": -1,
+                        "last_applied": -1}, state_p)
+    st3 = NativeStorage(d, 5001, fsync=True)
+    s, _ = st3.load()
+    assert s["current_term"] == 3 and s["voted_for"] == 2
+    st3.save_state({"current_term": 4, "voted_for": None})
+    st3.close()
+    s, _ = NativeStorage(d, 5001, fsync=True).load()
+    assert s["current_term"] == 4 and s["voted_for"] is None
