@@ -90,6 +90,19 @@ PYBIND11_MODULE(_hipk, m) {
                                  M, N, K, lda, ldb, ldc, ldr, epi, up_off, nr, group_m, S(st));
   });
   m.def("moe_workspace_bytes", &drtc::moe_workspace_bytes);
+  m.def("ep_plan", [](u64 topi, int npairs, int e_local, int world, int cap, u64 dst_row,
+                      u64 send_pair, u64 send_e, u64 overflow, u64 st) {
+    return drtc::launch_ep_plan(P<const int>(topi), npairs, e_local, world, cap, P<int>(dst_row),
+                                P<int>(send_pair), P<int>(send_e), P<int>(overflow), S(st));
+  });
+  m.def("ep_gather", [](u64 send_x, u64 x, u64 send_pair, int rows, int k, int H, int ldx, u64 st) {
+    return drtc::launch_ep_gather(P<void>(send_x), P<const void>(x), P<const int>(send_pair), rows,
+                                  k, H, ldx, S(st));
+  });
+  m.def("ep_combine", [](u64 out, u64 back, u64 dst_row, u64 w, int T, int k, int H, u64 st) {
+    return drtc::launch_ep_combine(P<void>(out), P<const void>(back), P<const int>(dst_row),
+                                   P<const float>(w), T, k, H, S(st));
+  });
   m.def("custom_ar_buffer_bytes", &drtc::custom_ar_buffer_bytes);
   m.def("custom_allreduce", [](u64 out, u64 in, int64_t n, const std::vector<u64>& bases, int rank,
                                int64_t stage_elems, int two_shot, u64 st) {

@@ -74,6 +74,7 @@ DRTC_DEVICE constexpr bool w4_glu() { return EPI == W4_SILU || EPI == W4_GELU; }
 // One LDS-DMA wave-instruction: 64 lanes x 16 B from rsrc + voff + soff into LDS bytes
 // [dst, dst + 1024).  Inline asm (hipcc would pin vmcnt / lgkmcnt waits around a builtin
 // form it cannot order against the ds_reads); M0 is written and restored in the statement.
+// One LDS-DMA wave-instruction outside the main loop (prologue): M0 saved and restored.
 DRTC_DEVICE void w4_dma(unsigned dst, unsigned voff, __amdgpu_buffer_rsrc_t rsrc, unsigned soff) {
   unsigned keep;
   asm volatile(
@@ -108,6 +109,8 @@ struct W4Dma {
   unsigned vb;
   unsigned sb[8];     // byte offset of B instruction s (beyond the per-lane row)
   unsigned lds_a, lds_b;  // LDS byte address of this wave's first block in stage 0
+  const char* abase;      // operand bases (lean form: descriptors rebuilt per tile)
+  const char* bbase;
 };
 
 // Per-tile state handed to every step of the unrolled schedule.
@@ -116,12 +119,24 @@ struct W4Tile {
   int cur, nxt;        // byte offsets of this tile's stage and the next tile's
   int ra0, ra1, rb0, rb1;
   unsigned kb;         // K byte offset of tile t + 2 (its DMA goes into stage `cur`)
+  __amdgpu_buffer_rsrc_t rak, rbk;  // lean form: descriptors based at K byte kb
 };
 
 // Step Q (0..127) of a K tile: MFMA Q, then the memory work scheduled behind it.  Every
 // condition is a compile-time constant (the tile is a fold over Q), so the emitted stream is
 // straight-line, and sched_barrier(0) pins it in this order.
-template <bool DMA, bool NEXT, int Q>
+//
+// Main-loop DMA issue: M0 (the LDS destination) is set once per operand group, one MFMA ahead
+// of the group's first DMA, and advanced by 4 KiB right after each DMA; K advances through
+// the buffer base (descriptor rebuilt once per tile) so the scalar offsets are loop-invariant:
+// one SALU per DMA (nothing else in this kernel uses M0).
+//
+// Schedule variants (launch_gemm variant 7 + V), A/B'd in one binary:
+//   V & 1  two barriers per K tile: both half-1 fragment sets are read first (MFMA 0-31),
+//          one lgkmcnt(0) + barrier frees the whole stage, then all 16 DMAs (MFMA 38-98)
+//   V & 2  the RAW barrier of the next tile at MFMA 111 (its reads over MFMA 112-127)
+//   V & 4  K start staggered over tiles (rotation by ((tm + tn) & 3) * nk / 4)
+template <int V, bool DMA, bool NEXT, int Q>
 DRTC_DEVICE void w4_step(f32x4 (&acc)[8][8], bf16x8 (&fa0)[8], bf16x8 (&fb0)[8],
                          bf16x8 (&fa1)[8], bf16x8 (&fb1)[8], const W4Tile& T, const W4Dma& d) {
   constexpr int i = (Q >> 3) & 7, j = Q & 7;
@@ -129,39 +144,60 @@ DRTC_DEVICE void w4_step(f32x4 (&acc)[8][8], bf16x8 (&fa0)[8], bf16x8 (&fb0)[8],
     acc[i][j] = mfma16(fa0[i], fb0[j], acc[i][j]);
   else
     acc[i][j] = mfma16(fa1[i], fb1[j], acc[i][j]);
-  // ---- B half 1 of this tile (consumed from MFMA 64 on)
+  constexpr bool two = (V & 1) != 0;
+  // ---- half 1 of this tile: B fragments (one read per 2 MFMA), then A
   if constexpr (Q < 16 && (Q & 1) == 0) fb1[Q >> 1] = w4_rd(T.lds, T.cur + T.rb1 + 2048 * (Q >> 1));
-  if constexpr (Q == 21) {
-    w4_lgkm0();
-    w4_barrier();  // every wave's B reads of this stage are done
+  if constexpr (two) {
+    if constexpr (Q >= 16 && Q < 32 && (Q & 1) == 0)
+      fa1[(Q - 16) >> 1] = w4_rd(T.lds, T.cur + T.ra1 + 2048 * ((Q - 16) >> 1));
+    if constexpr (Q == 35) {
+      w4_lgkm0();
+      w4_barrier();  // every wave's reads of this stage are done: the stage is free
+    }
+  } else {
+    if constexpr (Q == 21) {
+      w4_lgkm0();
+      w4_barrier();  // every wave's B reads of this stage are done
+    }
+    if constexpr (Q >= 22 && Q < 38 && ((Q - 22) & 3) < 2) {
+      constexpr int a = ((Q - 22) >> 2) * 2 + ((Q - 22) & 1);
+      fa1[a] = w4_rd(T.lds, T.cur + T.ra1 + 2048 * a);
+    }
+    if constexpr (Q == 57) {
+      w4_lgkm0();
+      w4_barrier();  // every wave's A reads of this stage are done
+    }
   }
-  // ---- A half 1 of this tile, interleaved with the B DMA of tile t + 2
-  if constexpr (Q >= 22 && Q < 38 && ((Q - 22) & 3) < 2) {
-    constexpr int a = ((Q - 22) >> 2) * 2 + ((Q - 22) & 1);
-    fa1[a] = w4_rd(T.lds, T.cur + T.ra1 + 2048 * a);
+  // ---- DMA of tile t + 2 into this stage: B group, then A group, one per 4 MFMA
+  constexpr int qb = two ? 38 : 24, qa = two ? 70 : 60;
+  if constexpr (DMA && Q == qb - 1)
+    asm volatile("s_mov_b32 m0, %0" : : "s"(d.lds_b + T.cur) : "memory");
+  if constexpr (DMA && Q >= qb && Q <= qb + 28 && ((Q - qb) & 3) == 0) {
+    constexpr int s = (Q - qb) >> 2;
+    asm volatile("buffer_load_dwordx4 %0, %1, %2 offen lds"
+                 : : "v"(d.vb), "s"(T.rbk), "s"(d.sb[s]) : "memory");
+    if constexpr (s < 7) asm volatile("s_add_u32 m0, m0, 0x1000" ::: "memory");
   }
-  if constexpr (DMA && Q >= 24 && Q <= 52 && ((Q - 24) & 3) == 0) {
-    constexpr int s = (Q - 24) >> 2;
-    w4_dma(d.lds_b + T.cur + 4096 * s, d.vb, d.rb, T.kb + d.sb[s]);
+  if constexpr (DMA && Q == qa - 1)
+    asm volatile("s_mov_b32 m0, %0" : : "s"(d.lds_a + T.cur) : "memory");
+  if constexpr (DMA && Q >= qa && Q <= qa + 28 && ((Q - qa) & 3) == 0) {
+    constexpr int s = (Q - qa) >> 2;
+    asm volatile("buffer_load_dwordx4 %0, %1, 0 offen lds"
+                 : : "v"(d.va[s]), "s"(T.rak) : "memory");
+    if constexpr (s < 7) asm volatile("s_add_u32 m0, m0, 0x1000" ::: "memory");
   }
-  if constexpr (Q == 57) {
-    w4_lgkm0();
-    w4_barrier();  // every wave's A reads of this stage are done
-  }
-  if constexpr (DMA && Q >= 60 && Q <= 88 && ((Q - 60) & 3) == 0) {
-    constexpr int s = (Q - 60) >> 2;
-    w4_dma(d.lds_a + T.cur + 4096 * s, d.va[s], d.ra, T.kb);
-  }
-  if constexpr (NEXT && Q == 103) {
+  // ---- tile t + 1: its DMA (issued during tile t - 1) landed for every wave, then its
+  // half-0 fragments: fa0[0], fb0[0..7], fa0[1..7]
+  constexpr int qn = (V & 2) ? 111 : 103;
+  if constexpr (NEXT && Q == qn) {
     if constexpr (DMA)
       w4_vmcnt<16>();
     else
       w4_vmcnt<0>();
-    w4_barrier();  // tile t + 1 landed for every wave
+    w4_barrier();
   }
-  // ---- half 0 of tile t + 1: fa0[0], fb0[0..7], fa0[1..7]
-  if constexpr (NEXT && Q >= 104 && Q < 120) {
-    constexpr int r = Q - 104;
+  if constexpr (NEXT && Q > qn && Q <= qn + 16) {
+    constexpr int r = Q - qn - 1;
     if constexpr (r == 0)
       fa0[0] = w4_rd(T.lds, T.nxt + T.ra0);
     else if constexpr (r <= 8)
@@ -172,25 +208,40 @@ DRTC_DEVICE void w4_step(f32x4 (&acc)[8][8], bf16x8 (&fa0)[8], bf16x8 (&fb0)[8],
   __builtin_amdgcn_sched_barrier(0);
 }
 
-template <bool DMA, bool NEXT, int... Qs>
+template <int V, bool DMA, bool NEXT, int... Qs>
 DRTC_DEVICE void w4_steps(std::integer_sequence<int, Qs...>, f32x4 (&acc)[8][8],
                           bf16x8 (&fa0)[8], bf16x8 (&fb0)[8], bf16x8 (&fa1)[8],
                           bf16x8 (&fb1)[8], const W4Tile& T, const W4Dma& d) {
-  (w4_step<DMA, NEXT, Qs>(acc, fa0, fb0, fa1, fb1, T, d), ...);
+  (w4_step<V, DMA, NEXT, Qs>(acc, fa0, fb0, fa1, fb1, T, d), ...);
 }
 
-template <bool DMA, bool NEXT>
+template <int V, bool DMA, bool NEXT>
 DRTC_DEVICE void w4_tile(f32x4 (&acc)[8][8], bf16x8 (&fa0)[8], bf16x8 (&fb0)[8],
                          bf16x8 (&fa1)[8], bf16x8 (&fb1)[8], const char* lds, int cur, int ra0,
                          int ra1, int rb0, int rb1, const W4Dma& d, int t2) {
-  const W4Tile T{lds, cur, cur ^ kW4Stage, ra0, ra1, rb0, rb1, (unsigned)t2 * 128u};
-  w4_steps<DMA, NEXT>(std::make_integer_sequence<int, 128>{}, acc, fa0, fb0, fa1, fb1, T, d);
+  W4Tile T{lds, cur, cur ^ kW4Stage, ra0, ra1, rb0, rb1, (unsigned)t2 * 128u};
+  T.rak = __builtin_amdgcn_make_buffer_rsrc((void*)(d.abase + T.kb), (short)0, 0x7FFFFFFF,
+                                            0x00020000);
+  T.rbk = __builtin_amdgcn_make_buffer_rsrc((void*)(d.bbase + T.kb), (short)0, 0x7FFFFFFF,
+                                            0x00020000);
+  w4_steps<V, DMA, NEXT>(std::make_integer_sequence<int, 128>{}, acc, fa0, fb0, fa1, fb1, T, d);
 }
 
 // acc[i][j][r] = C[row 128 wm + 16 i + 4 g + r][column of B fragment j, row l16]: lane l16
 // holds columns 8 l16 + j (j = 0..7) of its 4 rows -> one 16-B store per (i, r); a store
 // instruction writes 4 rows x 256 contiguous bytes.
-template <int EPI>
+// Epilogue stores are non-temporal (measured +2-3 % on the 16k-row shapes: the output does
+// not displace the operands' lines in the L2 on its way out).
+template <int V>
+DRTC_DEVICE void w4_st16(bf16_t* p, bf16x8 v) {
+  __builtin_nontemporal_store(v, reinterpret_cast<bf16x8*>(p));
+}
+template <int V>
+DRTC_DEVICE void w4_st8(bf16_t* p, bf16x4 v) {
+  __builtin_nontemporal_store(v, reinterpret_cast<bf16x4*>(p));
+}
+
+template <int EPI, int V>
 DRTC_DEVICE void w4_epilogue(const W4Params& p, f32x4 (&acc)[8][8], int tm, int tn, int wm,
                              int wn, int l16, int g) {
 #pragma unroll
@@ -206,21 +257,40 @@ DRTC_DEVICE void w4_epilogue(const W4Params& p, f32x4 (&acc)[8][8], int tm, int 
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           o[j] = f2bf(act_value<EPI == W4_SILU ? 0 : 1>(acc[i][j][r]) * acc[i][j + 4][r]);
-        *reinterpret_cast<bf16x4*>(crow + n) = o;
-      } else {
+        w4_st8<V>(crow + n, o);
+      } else if constexpr (EPI != W4_RESIDUAL) {
         const int n = 256 * tn + 128 * wn + 8 * l16;
         bf16x8 o;
-        if constexpr (EPI == W4_RESIDUAL) {
-          const bf16x8 rv = *reinterpret_cast<const bf16x8*>(p.r + (int64_t)m * p.ldr + n);
 #pragma unroll
-          for (int j = 0; j < 8; ++j) o[j] = f2bf(acc[i][j][r] + bf2f(rv[j]));
-        } else {
-#pragma unroll
-          for (int j = 0; j < 8; ++j) o[j] = f2bf(acc[i][j][r]);
-        }
-        *reinterpret_cast<bf16x8*>(crow + n) = o;
+        for (int j = 0; j < 8; ++j) o[j] = f2bf(acc[i][j][r]);
+        w4_st16<V>(crow + n, o);
       }
     }
+  }
+  if constexpr (EPI == W4_RESIDUAL) {
+    // every residual row is loaded before the first store: R may alias C (in-place add into
+    // the residual stream), so a load placed after a store could not be hoisted above it and
+    // each (load, add, store) would pay a full memory round trip
+    const int n = 256 * tn + 128 * wn + 8 * l16;
+    bf16x8 rv[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = min(256 * tm + 128 * wm + 16 * i + 4 * g + r, p.M - 1);
+        rv[i][r] = *reinterpret_cast<const bf16x8*>(p.r + (int64_t)m * p.ldr + n);
+      }
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = 256 * tm + 128 * wm + 16 * i + 4 * g + r;
+        if (m >= p.M) continue;
+        bf16x8 o;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = f2bf(acc[i][j][r] + bf2f(rv[i][r][j]));
+        w4_st16<V>(p.c + (int64_t)m * p.ldc + n, o);
+      }
   }
 }
 
@@ -265,7 +335,7 @@ DRTC_DEVICE bool w4_splitk(const W4Params& p, f32x4 (&acc)[8][8], int tile, int 
   return true;
 }
 
-template <int EPI>
+template <int EPI, int V>
 __global__ __launch_bounds__(kW4Threads, 1) void gemm_w4_kernel(W4Params p) {
   extern __shared__ __attribute__((aligned(16))) char w4_lds[];
   // ---- tile assignment: XCD remap (bijective), split-K slice fastest, grouped rows
@@ -323,6 +393,8 @@ __global__ __launch_bounds__(kW4Threads, 1) void gemm_w4_kernel(W4Params p) {
       for (int s = 0; s < 8; ++s) d.sb[s] = (unsigned)((128 * (s >> 2) + 2 * (s & 3)) * p.ldb * 2);
     }
     d.rb = __builtin_amdgcn_make_buffer_rsrc((void*)bbase, (short)0, 0x7FFFFFFF, 0x00020000);
+    d.abase = reinterpret_cast<const char*>(abase);
+    d.bbase = reinterpret_cast<const char*>(bbase);
     d.vb = (unsigned)(brow * p.ldb * 2 + chunk * 16);
     d.lds_a = __builtin_amdgcn_readfirstlane(lds0 + 8 * wv * 128);
     d.lds_b = __builtin_amdgcn_readfirstlane(lds0 + kW4BOff + 8 * wv * 128);
@@ -342,17 +414,21 @@ __global__ __launch_bounds__(kW4Threads, 1) void gemm_w4_kernel(W4Params p) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
+  // K tiles run in the rotated order kst, kst + 1, ... (mod nk) when staggered (V & 4)
+  int kst = 0;
+  if constexpr ((V & 4) != 0) kst = (nk & 3) == 0 ? ((tm + tn) & 3) * (nk >> 2) : 0;
+  const unsigned k0b = (unsigned)kst * 128u, k1b = (unsigned)(kst + 1 < nk ? kst + 1 : 0) * 128u;
   // ---- prologue: tiles 0 and 1 into stages 0 and 1
 #pragma unroll
-  for (int s = 0; s < 8; ++s) w4_dma(d.lds_b + 4096 * s, d.vb, d.rb, d.sb[s]);
+  for (int s = 0; s < 8; ++s) w4_dma(d.lds_b + 4096 * s, d.vb, d.rb, k0b + d.sb[s]);
 #pragma unroll
-  for (int s = 0; s < 8; ++s) w4_dma(d.lds_a + 4096 * s, d.va[s], d.ra, 0u);
+  for (int s = 0; s < 8; ++s) w4_dma(d.lds_a + 4096 * s, d.va[s], d.ra, k0b);
   if (nk > 1) {
 #pragma unroll
     for (int s = 0; s < 8; ++s)
-      w4_dma(d.lds_b + kW4Stage + 4096 * s, d.vb, d.rb, 128u + d.sb[s]);
+      w4_dma(d.lds_b + kW4Stage + 4096 * s, d.vb, d.rb, k1b + d.sb[s]);
 #pragma unroll
-    for (int s = 0; s < 8; ++s) w4_dma(d.lds_a + kW4Stage + 4096 * s, d.va[s], d.ra, 128u);
+    for (int s = 0; s < 8; ++s) w4_dma(d.lds_a + kW4Stage + 4096 * s, d.va[s], d.ra, k1b);
     w4_vmcnt<16>();
   } else {
     w4_vmcnt<0>();
@@ -368,23 +444,53 @@ __global__ __launch_bounds__(kW4Threads, 1) void gemm_w4_kernel(W4Params p) {
   // One loop body for every tile (a single straight-line schedule keeps the 256 accumulators
   // in place in the AGPRs): the last two tiles re-stage the final tile (kb clamped: valid
   // bytes, never read) and the last one reads stale fragments it never uses.
-  for (int t = 0; t < nk; ++t)
-    w4_tile<true, true>(acc, fa0, fb0, fa1, fb1, lds, (t & 1) * kW4Stage, ra0, ra1, rb0, rb1, d,
-                        min(t + 2, nk - 1));
+  for (int t = 0; t < nk; ++t) {
+    int t2 = min(t + 2, nk - 1) + kst;
+    t2 -= t2 >= nk ? nk : 0;
+    w4_tile<V, true, true>(acc, fa0, fb0, fa1, fb1, lds, (t & 1) * kW4Stage, ra0, ra1, rb0, rb1, d,
+                           t2);
+  }
   w4_vmcnt<0>();  // no LDS-DMA may still be landing when the workgroup leaves
 
   if (p.splitk > 1) {
     __syncthreads();
     if (!w4_splitk(p, acc, tile, slice, w4_lds)) return;
   }
-  w4_epilogue<EPI>(p, acc, tm, tn, wm, wn, l16, g);
+  w4_epilogue<EPI, V>(p, acc, tm, tn, wm, wn, l16, g);
+}
+
+template <int EPI, int V>
+int w4_launch_v(const W4Params& p, hipStream_t st) {
+  const int nwg = p.tiles_m * p.tiles_n * p.splitk;
+  hipLaunchKernelGGL((gemm_w4_kernel<EPI, V>), dim3(nwg), dim3(kW4Threads), kW4Lds, st, p);
+  return (int)hipGetLastError();
 }
 
 template <int EPI>
-int w4_launch(const W4Params& p, hipStream_t st) {
-  const int nwg = p.tiles_m * p.tiles_n * p.splitk;
-  hipLaunchKernelGGL((gemm_w4_kernel<EPI>), dim3(nwg), dim3(kW4Threads), kW4Lds, st, p);
-  return (int)hipGetLastError();
+int w4_launch(const W4Params& p, int v, hipStream_t st) {
+  switch (v) {
+    case 0: return w4_launch_v<EPI, 0>(p, st);
+    case 1: return w4_launch_v<EPI, 1>(p, st);
+    case 2: return w4_launch_v<EPI, 2>(p, st);
+    case 3: return w4_launch_v<EPI, 3>(p, st);
+    case 4: return w4_launch_v<EPI, 4>(p, st);
+    case 5: return w4_launch_v<EPI, 5>(p, st);
+    case 6: return w4_launch_v<EPI, 6>(p, st);
+    case 7: return w4_launch_v<EPI, 7>(p, st);
+    default: return -1;
+  }
+}
+
+template <int EPI, int V>
+int w4_cfg_one() {
+  return (int)hipFuncSetAttribute((const void*)gemm_w4_kernel<EPI, V>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, kW4Lds);
+}
+template <int EPI>
+int w4_cfg() {
+  return w4_cfg_one<EPI, 0>() | w4_cfg_one<EPI, 1>() | w4_cfg_one<EPI, 2>() |
+         w4_cfg_one<EPI, 3>() | w4_cfg_one<EPI, 4>() | w4_cfg_one<EPI, 5>() |
+         w4_cfg_one<EPI, 6>() | w4_cfg_one<EPI, 7>();
 }
 
 }  // namespace
@@ -392,7 +498,7 @@ int w4_launch(const W4Params& p, hipStream_t st) {
 int launch_gemm_w4(void* c, const void* a, const void* b, const void* r, int M, int N, int K,
                    int lda, int ldb, int ldc, int ldr, int epi, int up_off, int splitk,
                    int group_m, void* slab, int64_t slab_bytes, int* counters, int n_counters,
-                   hipStream_t st) {
+                   int v, hipStream_t st) {
   // shape contract (checked here so a bad call never reaches the device)
   const bool glu = epi == W4_SILU || epi == W4_GELU;
   if (M <= 0 || N <= 0 || K <= 0 || K % 64 || splitk < 1 || (K / 64) % splitk) return -1;
@@ -426,25 +532,16 @@ int launch_gemm_w4(void* c, const void* a, const void* b, const void* r, int M, 
     p.counters = counters;
   }
   switch (epi) {
-    case W4_STORE: return w4_launch<W4_STORE>(p, st);
-    case W4_RESIDUAL: return w4_launch<W4_RESIDUAL>(p, st);
-    case W4_SILU: return w4_launch<W4_SILU>(p, st);
-    case W4_GELU: return w4_launch<W4_GELU>(p, st);
+    case W4_STORE: return w4_launch<W4_STORE>(p, v, st);
+    case W4_RESIDUAL: return w4_launch<W4_RESIDUAL>(p, v, st);
+    case W4_SILU: return w4_launch<W4_SILU>(p, v, st);
+    case W4_GELU: return w4_launch<W4_GELU>(p, v, st);
     default: return -1;
   }
 }
 
 int configure_gemm_w4() {
-  int e = 0;
-  e |= (int)hipFuncSetAttribute((const void*)gemm_w4_kernel<W4_STORE>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, kW4Lds);
-  e |= (int)hipFuncSetAttribute((const void*)gemm_w4_kernel<W4_RESIDUAL>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, kW4Lds);
-  e |= (int)hipFuncSetAttribute((const void*)gemm_w4_kernel<W4_SILU>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, kW4Lds);
-  e |= (int)hipFuncSetAttribute((const void*)gemm_w4_kernel<W4_GELU>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, kW4Lds);
-  return e;
+  return w4_cfg<W4_STORE>() | w4_cfg<W4_RESIDUAL>() | w4_cfg<W4_SILU>() | w4_cfg<W4_GELU>();
 }
 
 }  // namespace drtc

@@ -49,6 +49,13 @@ int launch_moe(void* out, const void* x, const void* router_logits, const void* 
                const void* w_dn, int T, int H, int I, int E, int k, int e_off, int e_local,
                int act, void* workspace, int64_t ws_bytes, int variant, hipStream_t st);
 int64_t moe_workspace_bytes(int T, int H, int I, int e_local, int k);
+// Expert-parallel dispatch / combine with a static per-destination capacity (moe_ep.hip).
+int launch_ep_plan(const int* topi, int P, int e_local, int world, int cap, int* dst_row,
+                   int* send_pair, int* send_e, int* overflow, hipStream_t st);
+int launch_ep_gather(void* send_x, const void* x, const int* send_pair, int rows, int k, int H,
+                     int ldx, hipStream_t st);
+int launch_ep_combine(void* out, const void* back, const int* dst_row, const float* w, int T,
+                      int k, int H, hipStream_t st);
 
 // One-shot P2P all-reduce over IPC-mapped staging buffers (allreduce.hip).
 struct ArPeers {
@@ -103,11 +110,12 @@ int launch_gemm(void* c, const void* a, const void* b, const void* r, int M, int
                 hipStream_t st);
 int64_t gemm_workspace_bytes(int64_t M, int64_t N, int splitk);
 // 4-wave hand-scheduled GEMM (gemm_w4.hip): same contract as launch_gemm (gated: up_off == N);
-// launch_gemm variant 7 routes here.  Split-K slabs: 256 KiB per tile and slice.
+// launch_gemm variants 7..14 route here (schedule variant v = variant - 7).  Split-K slabs:
+// 256 KiB per tile and slice.
 int launch_gemm_w4(void* c, const void* a, const void* b, const void* r, int M, int N, int K,
                    int lda, int ldb, int ldc, int ldr, int epi, int up_off, int splitk,
                    int group_m, void* slab, int64_t slab_bytes, int* counters, int n_counters,
-                   hipStream_t st);
+                   int v, hipStream_t st);
 int configure_gemm_w4();
 
 // Raise the dynamic-LDS ceiling of the kernels that need > 64 KiB (head_dim

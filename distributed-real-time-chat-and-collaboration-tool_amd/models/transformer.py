@@ -233,11 +233,19 @@ class TransformerLM:
     def _mlp(self, L: dict, x: ops.PendingNorm, decode: bool = False) -> torch.Tensor:
         if self.cfg.is_moe:
             return self._moe(L, x.materialize(), decode), False
-        gu = ops.norm_linear(x, L["gate_up"])
-        res = self._fusable_residual(gu, x)
-        if res is not None:
-            return ops.linear_residual(ops.act_glu(gu, self.cfg.act), L["down"], res), True
-        y = ops.glu_linear(gu, L["down"], self.cfg.act)
+        if ops.w4_glu_ok(x.x, L["gate_up"], self.cfg.act):
+            # prefill-sized: gate_up GEMM with the GLU in its epilogue (gemm_w4.hip)
+            h = ops.norm_glu(x, L["gate_up"], self.cfg.act)
+            res = self._fusable_residual(h, x)
+            if res is not None:
+                return ops.linear_residual(h, L["down"], res), True
+            y = ops.linear(h, L["down"])
+        else:
+            gu = ops.norm_linear(x, L["gate_up"])
+            res = self._fusable_residual(gu, x)
+            if res is not None:
+                return ops.linear_residual(ops.act_glu(gu, self.cfg.act), L["down"], res), True
+            y = ops.glu_linear(gu, L["down"], self.cfg.act)
         if decode and self.pc.tp_size > 1:
             return y, False, True  # reduced by the next norm (fused all-reduce + add + norm)
         return self.pc.all_reduce_tp(y), False
@@ -464,8 +472,11 @@ class TransformerLM:
                 m_rows = pc.reduce_scatter_rows(part)
             else:
                 xg = pc.all_gather_rows(x.materialize())
-                gu = ops.linear(xg, L["gate_up"])
-                m_rows = pc.reduce_scatter_rows(ops.linear(ops.act_glu(gu, cfg.act), L["down"]))
+                if ops.w4_glu_ok(xg, L["gate_up"], cfg.act):
+                    h = ops.mfma_gemm(xg, L["gate_up"], cfg.act, variant=7)
+                else:
+                    h = ops.act_glu(ops.linear(xg, L["gate_up"]), cfg.act)
+                m_rows = pc.reduce_scatter_rows(ops.linear(h, L["down"]))
             x = ops.PendingNorm(m_rows, x.stream(), self.layers[i + 1]["ln_in"], cfg.rms_eps,
                                 cfg.gemma_norm)
         raise AssertionError("unreachable")

@@ -205,6 +205,8 @@ def linear(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
         key = (M, N, K, x.stride(0))
         ent = _activate().get(key)
         if ent is None and M > DECODE_MAX_M:
+            if w4_ok(x, w):
+                return mfma_gemm(x, w, "store", variant=W4_VARIANT, group_m=w4_group_m(M, N, K))
             if _prefill_algo(M, N, K, x.stride(0), 0) >= 0:
                 y = torch.empty((M, N), dtype=x.dtype, device=x.device)
                 check(hipk().lt_gemm(y.data_ptr(), x.data_ptr(), w.data_ptr(), M, N, K,
@@ -253,6 +255,9 @@ def linear_residual(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor) ->
     assert residual.shape == (x.shape[0], w.shape[0]) and w.dtype == x.dtype
     M, K = x.shape
     N = w.shape[0]
+    if w4_ok(x, w, residual):
+        return mfma_gemm(x, w, "residual", residual=residual, out=residual, variant=W4_VARIANT,
+                         group_m=w4_group_m(M, N, K))
     if (_enabled and x.stride(1) == 1 and w.is_contiguous() and residual.stride(0) == N
             and x.dtype == torch.bfloat16):
         _activate()
@@ -425,9 +430,77 @@ def save_entries(entries: dict[str, dict], path: str | None = None) -> str:
     return path
 
 
-__all__ = ["linear", "norm_linear", "glu_linear", "skinny_linear", "skinny_ok", "skinny_variant",
+# ------------------------------------------------------------ 4-wave GEMM dispatch
+W4_VARIANT = 7  # gemm_w4.hip through launch_gemm
+_w4_glu = os.environ.get("DRTC_W4_GLU", "1") != "0"
+_w4_plain = os.environ.get("DRTC_W4_GEMM", "1") != "0"
+# Prefill-sized passes (M >= W4_MIN_M rows) run the 4-wave hand GEMM (profiles/r3a_w4_gemm.md,
+# Llama-3-8B at M = 16384, interleaved with the library in one process):
+#   gate_up + SiLU-GLU epilogue  1.03-1.05x hipBLASLt + act_glu   -> hand (no act_glu pass)
+#   qkv (store), o (+residual)   0.98-0.99x                        -> hand
+#   down (K = 14336, +residual)  0.94-0.96x                        -> library (K > W4_MAX_K)
+# Decode buckets (M <= 1024) keep the tuned library / skinny / medium-M kernels.
+W4_GLU_MIN_M = int(os.environ.get("DRTC_W4_GLU_MIN_M", "4096"))
+W4_MIN_M = int(os.environ.get("DRTC_W4_MIN_M", "4096"))
+W4_MAX_K = int(os.environ.get("DRTC_W4_MAX_K", "8192"))
+
+
+def w4_group_m(M: int, N: int, K: int, glu: bool = False) -> int:
+    """Row-tile group of the XCD-aware tile order (scripts/gpu_w4_groups.sh): a group's A
+    panels must stay cache-resident while it sweeps the columns - 2 for the long-K down
+    projection (7 MB per 256-row panel), 8 for the gated gate_up, 4 otherwise."""
+    if K >= 12288:
+        return 2
+    return 8 if glu else 4
+
+
+def w4_ok(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor | None = None) -> bool:
+    """Whether a prefill-sized projection y = x @ w.T (+ residual) takes gemm_w4."""
+    if not (_w4_plain and on_gpu(x) and _enabled and x.dim() == 2 and x.dtype == torch.bfloat16
+            and w.dtype == torch.bfloat16 and w.is_contiguous() and x.stride(1) == 1):
+        return False
+    M, K = x.shape
+    N = w.shape[0]
+    if not (M >= W4_MIN_M and K <= W4_MAX_K and K % 64 == 0 and N % 256 == 0
+            and w.shape[1] == K and x.stride(0) % 8 == 0 and x.data_ptr() % 16 == 0
+            and w.data_ptr() % 16 == 0):
+        return False
+    if residual is not None:
+        return (residual.dim() == 2 and residual.shape == (M, N) and residual.stride(1) == 1
+                and residual.stride(0) % 8 == 0 and residual.data_ptr() % 16 == 0
+                and residual.dtype == torch.bfloat16)
+    return True
+
+
+def w4_glu_ok(x: torch.Tensor, w: torch.Tensor, act: str) -> bool:
+    """Whether ``norm_glu`` takes the fused-GLU hand GEMM for x [M, K] @ [gate; up]^T."""
+    if not (_w4_glu and on_gpu(x) and _enabled and x.dim() == 2 and act in ("silu", "gelu_tanh")
+            and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and w.is_contiguous()
+            and x.stride(1) == 1):
+        return False
+    M, K = x.shape
+    N2 = w.shape[0]
+    return (M >= W4_GLU_MIN_M and K % 64 == 0 and w.shape[1] == K and N2 % 256 == 0
+            and x.stride(0) % 8 == 0 and x.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0)
+
+
+def norm_glu(p, w: torch.Tensor, act: str = "silu") -> torch.Tensor:
+    """h = act(norm(x) @ gate^T) * (norm(x) @ up^T) for an ``ops.PendingNorm`` p and the
+    fused [gate; up] weight: on the 4-wave hand GEMM with the GLU in its epilogue when
+    ``w4_glu_ok`` (one launch, no [M, 2I] intermediate), else norm_linear + act_glu."""
+    from .activation import act_glu
+
+    if w4_glu_ok(p.x, w, act):
+        x = p.materialize()
+        M, K = x.shape
+        return mfma_gemm(x, w, act, variant=W4_VARIANT,
+                         group_m=w4_group_m(M, w.shape[0] // 2, K, glu=True))
+    return act_glu(norm_linear(p, w), act)
+
+
+__all__ = ["linear", "norm_linear", "glu_linear", "norm_glu", "w4_glu_ok", "skinny_linear", "skinny_ok", "skinny_variant",
            "skinny_supports", "mfma_gemm", "midm_gemm", "midm_supported", "dec_gemm", "dec_supported",
-           "tune", "save_entries",
+           "tune", "save_entries", "w4_ok", "w4_group_m",
            "load_table", "reset", "set_enabled", "table_path"]
 
 

@@ -56,6 +56,26 @@ def main():
             else:
                 fns[arm] = (lambda v=v: G.mfma_gemm(x, w, a.epi, out=out, variant=v,
                                                     splitk=a.splitk, group_m=a.group_m))
+    # correctness of every hand arm against an fp32 reference (one call each)
+    ref = x.float() @ w.float().t()
+    if a.epi == "residual":
+        ref = ref + res.float()
+    elif glu:
+        ref = (torch.nn.functional.silu(ref[:, :nout]) if a.epi == "silu" else
+               torch.nn.functional.gelu(ref[:, :nout], approximate="tanh")) * ref[:, nout:]
+    errs = {}
+    for k, f in fns.items():
+        if k == "lib":
+            continue
+        if a.epi == "residual":
+            r0 = res.clone()
+            f()
+            got, res.data = res.clone(), r0
+        else:
+            got = f()
+        torch.cuda.synchronize()
+        errs[k] = round((got.float() - ref).abs().max().item() / ref.abs().max().item(), 5)
+    del ref
     for f in fns.values():
         f()
     torch.cuda.synchronize()
@@ -73,7 +93,8 @@ def main():
     for k, ts in times.items():
         med = statistics.median(ts)
         print(json.dumps({"shape": [M, N, K], "epi": a.epi, "arm": k, "us_med": round(med, 1),
-                          "us_min": round(min(ts), 1), "TFLOPs": round(fl / med / 1e6, 1)}),
+                          "us_min": round(min(ts), 1), "TFLOPs": round(fl / med / 1e6, 1),
+                          "err": errs.get(k)}),
               flush=True)
 
 
