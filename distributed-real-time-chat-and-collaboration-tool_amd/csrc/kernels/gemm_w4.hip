@@ -14,11 +14,12 @@
 // the AGPR half of the unified file) - and hides every latency INSIDE the wave with an
 // explicit instruction schedule instead of a partner wave:
 //
-//   * LDS: 2 stages x [A 256 rows | B 256 rows] x 128 B (one 64-deep K tile) = 128 KiB, filled
-//     by LDS-DMA (buffer_load_dwordx4 ... lds, 1 KiB = 8 rows per wave-instruction), the
-//     16-B chunk of row r stored at chunk ^ ((r >> 1) & 7): conflict-free ds_read_b128 for
+//   * LDS: 2 stages x [A 256 rows | B 256 rows] x 128 B (one 64-deep K tile) = 129 KiB, filled
+//     by LDS-DMA (buffer_load_dwordx4 ... lds, 1 KiB = 8 rows per wave-instruction).  A: the
+//     16-B chunk of row r stored at chunk ^ ((r >> 1) & 7) - conflict-free ds_read_b128 for
 //     the MFMA lane groups (the XOR is applied to the per-lane DMA SOURCE address and to the
-//     read address - the two sides of one involution).
+//     read address - the two sides of one involution).  B: 1040-B blocks of 8 rows (16 B of
+//     padding), read 8 rows apart (fragment j, lane row l -> B row 8 l + j).
 //   * Registers: the fragments of a whole K tile (both 32-deep halves, A and B: 128 VGPRs),
 //     so a stage is released as soon as its reads are in registers - the DMA of tile t + 2
 //     goes into the stage of tile t while tile t's MFMAs still run (two tiles in flight).
@@ -31,10 +32,12 @@
 //       [vmcnt(16): own DMA of tile t+1 landed; barrier 3: everyone's]
 //       MFMA 104-127  half 1 | 16 ds_read of half 0 of tile t+1
 //     Three barriers per K tile, each in the middle of an MFMA stream.
-//   * B rows permuted on their way into LDS (fragment j, fragment row l <- tile row 8 l + j),
-//     so a lane's accumulators over the 8 B fragments are 8 consecutive output columns: the
-//     epilogue stores 16 B per lane (4 rows x 256 contiguous bytes per instruction), and a
-//     gated tile pairs gate fragment j with up fragment j + 4 of the same columns in a lane.
+//   * B fragment j, lane row l reads B row 8 l + j, so a lane's accumulators over the 8 B
+//     fragments are 8 consecutive output columns: the epilogue stores 16 B per lane (4 rows x
+//     256 contiguous bytes per instruction), and a gated tile pairs gate fragment j with up
+//     fragment j + 4 of the same columns in a lane.  Every DMA instruction still reads 8
+//     consecutive weight rows (a first form that permuted the rows in the DMA read 8 rows
+//     64 KiB apart per instruction and ran 1.5-2.5x slower wherever B streams from HBM).
 //   * XCD-aware, row-grouped tile order; split-K with an fp32 slab and an in-launch combine
 //     by the last arriving slice (agent-scope release / acquire ticket) for short-M shapes.
 #include "common.h"
@@ -48,8 +51,12 @@ namespace {
 typedef __attribute__((address_space(3))) void* w4_lds_ptr;
 
 constexpr int kW4Threads = 256;
-constexpr int kW4Stage = 65536;  // bytes: [A 256 rows | B 256 rows] x 128 B
-constexpr int kW4BOff = 32768;   // B region within a stage
+// Stage: A 256 rows x 128 B (XOR-swizzled chunks) | B 32 blocks of 8 rows x 128 B, each block
+// followed by 16 B of padding (1040-B blocks: B rows are read 8 apart, the padding spreads
+// them over the banks while every DMA instruction still loads 8 CONSECUTIVE weight rows).
+constexpr int kW4BOff = 32768;                 // B region within a stage
+constexpr int kW4BBlk = 1040;                  // bytes per 8-row B block
+constexpr int kW4Stage = kW4BOff + 32 * kW4BBlk;  // 66048
 constexpr int kW4Lds = 2 * kW4Stage;
 
 enum { W4_STORE = 0, W4_RESIDUAL = 1, W4_SILU = 2, W4_GELU = 3 };
@@ -134,8 +141,9 @@ struct W4Tile {
 // Schedule variants (launch_gemm variant 7 + V), A/B'd in one binary:
 //   V & 1  two barriers per K tile: both half-1 fragment sets are read first (MFMA 0-31),
 //          one lgkmcnt(0) + barrier frees the whole stage, then all 16 DMAs (MFMA 38-98)
-//   V & 2  the RAW barrier of the next tile at MFMA 111 (its reads over MFMA 112-127)
-//   V & 4  K start staggered over tiles (rotation by ((tm + tn) & 3) * nk / 4)
+//   V & 2  plain (temporal) epilogue stores instead of non-temporal ones
+//   V & 4  reduce-scatter split-K (w4_splitk_rs: every slice finishes part of the tile,
+//          all workgroups resident) instead of the last-arriver combine
 template <int V, bool DMA, bool NEXT, int Q>
 DRTC_DEVICE void w4_step(f32x4 (&acc)[8][8], bf16x8 (&fa0)[8], bf16x8 (&fb0)[8],
                          bf16x8 (&fa1)[8], bf16x8 (&fb1)[8], const W4Tile& T, const W4Dma& d) {
@@ -146,7 +154,7 @@ DRTC_DEVICE void w4_step(f32x4 (&acc)[8][8], bf16x8 (&fa0)[8], bf16x8 (&fb0)[8],
     acc[i][j] = mfma16(fa1[i], fb1[j], acc[i][j]);
   constexpr bool two = (V & 1) != 0;
   // ---- half 1 of this tile: B fragments (one read per 2 MFMA), then A
-  if constexpr (Q < 16 && (Q & 1) == 0) fb1[Q >> 1] = w4_rd(T.lds, T.cur + T.rb1 + 2048 * (Q >> 1));
+  if constexpr (Q < 16 && (Q & 1) == 0) fb1[Q >> 1] = w4_rd(T.lds, T.cur + T.rb1 + 128 * (Q >> 1));
   if constexpr (two) {
     if constexpr (Q >= 16 && Q < 32 && (Q & 1) == 0)
       fa1[(Q - 16) >> 1] = w4_rd(T.lds, T.cur + T.ra1 + 2048 * ((Q - 16) >> 1));
@@ -170,17 +178,26 @@ DRTC_DEVICE void w4_step(f32x4 (&acc)[8][8], bf16x8 (&fa0)[8], bf16x8 (&fb0)[8],
   }
   // ---- DMA of tile t + 2 into this stage: B group, then A group, one per 4 MFMA
   constexpr int qb = two ? 38 : 24, qa = two ? 70 : 60;
-  if constexpr (DMA && Q == qb - 1)
+  constexpr bool classic = false;
+  if constexpr (classic && DMA && Q >= qb && Q <= qb + 28 && ((Q - qb) & 3) == 0) {
+    constexpr int s = (Q - qb) >> 2;
+    w4_dma(d.lds_b + T.cur + 4 * kW4BBlk * s, d.vb, d.rb, T.kb + d.sb[s]);
+  }
+  if constexpr (classic && DMA && Q >= qa && Q <= qa + 28 && ((Q - qa) & 3) == 0) {
+    constexpr int s = (Q - qa) >> 2;
+    w4_dma(d.lds_a + T.cur + 4096 * s, d.va[s], d.ra, T.kb);
+  }
+  if constexpr (!classic && DMA && Q == qb - 1)
     asm volatile("s_mov_b32 m0, %0" : : "s"(d.lds_b + T.cur) : "memory");
-  if constexpr (DMA && Q >= qb && Q <= qb + 28 && ((Q - qb) & 3) == 0) {
+  if constexpr (!classic && DMA && Q >= qb && Q <= qb + 28 && ((Q - qb) & 3) == 0) {
     constexpr int s = (Q - qb) >> 2;
     asm volatile("buffer_load_dwordx4 %0, %1, %2 offen lds"
                  : : "v"(d.vb), "s"(T.rbk), "s"(d.sb[s]) : "memory");
-    if constexpr (s < 7) asm volatile("s_add_u32 m0, m0, 0x1000" ::: "memory");
+    if constexpr (s < 7) asm volatile("s_add_u32 m0, m0, 0x1040" ::: "memory");  // 4 blocks
   }
-  if constexpr (DMA && Q == qa - 1)
+  if constexpr (!classic && DMA && Q == qa - 1)
     asm volatile("s_mov_b32 m0, %0" : : "s"(d.lds_a + T.cur) : "memory");
-  if constexpr (DMA && Q >= qa && Q <= qa + 28 && ((Q - qa) & 3) == 0) {
+  if constexpr (!classic && DMA && Q >= qa && Q <= qa + 28 && ((Q - qa) & 3) == 0) {
     constexpr int s = (Q - qa) >> 2;
     asm volatile("buffer_load_dwordx4 %0, %1, 0 offen lds"
                  : : "v"(d.va[s]), "s"(T.rak) : "memory");
@@ -188,7 +205,7 @@ DRTC_DEVICE void w4_step(f32x4 (&acc)[8][8], bf16x8 (&fa0)[8], bf16x8 (&fb0)[8],
   }
   // ---- tile t + 1: its DMA (issued during tile t - 1) landed for every wave, then its
   // half-0 fragments: fa0[0], fb0[0..7], fa0[1..7]
-  constexpr int qn = (V & 2) ? 111 : 103;
+  constexpr int qn = 103;
   if constexpr (NEXT && Q == qn) {
     if constexpr (DMA)
       w4_vmcnt<16>();
@@ -201,7 +218,7 @@ DRTC_DEVICE void w4_step(f32x4 (&acc)[8][8], bf16x8 (&fa0)[8], bf16x8 (&fb0)[8],
     if constexpr (r == 0)
       fa0[0] = w4_rd(T.lds, T.nxt + T.ra0);
     else if constexpr (r <= 8)
-      fb0[r - 1] = w4_rd(T.lds, T.nxt + T.rb0 + 2048 * (r - 1));
+      fb0[r - 1] = w4_rd(T.lds, T.nxt + T.rb0 + 128 * (r - 1));
     else
       fa0[r - 8] = w4_rd(T.lds, T.nxt + T.ra0 + 2048 * (r - 8));
   }
@@ -219,7 +236,7 @@ template <int V, bool DMA, bool NEXT>
 DRTC_DEVICE void w4_tile(f32x4 (&acc)[8][8], bf16x8 (&fa0)[8], bf16x8 (&fb0)[8],
                          bf16x8 (&fa1)[8], bf16x8 (&fb1)[8], const char* lds, int cur, int ra0,
                          int ra1, int rb0, int rb1, const W4Dma& d, int t2) {
-  W4Tile T{lds, cur, cur ^ kW4Stage, ra0, ra1, rb0, rb1, (unsigned)t2 * 128u};
+  W4Tile T{lds, cur, kW4Stage - cur, ra0, ra1, rb0, rb1, (unsigned)t2 * 128u};
   T.rak = __builtin_amdgcn_make_buffer_rsrc((void*)(d.abase + T.kb), (short)0, 0x7FFFFFFF,
                                             0x00020000);
   T.rbk = __builtin_amdgcn_make_buffer_rsrc((void*)(d.bbase + T.kb), (short)0, 0x7FFFFFFF,
@@ -234,11 +251,17 @@ DRTC_DEVICE void w4_tile(f32x4 (&acc)[8][8], bf16x8 (&fa0)[8], bf16x8 (&fb0)[8],
 // not displace the operands' lines in the L2 on its way out).
 template <int V>
 DRTC_DEVICE void w4_st16(bf16_t* p, bf16x8 v) {
-  __builtin_nontemporal_store(v, reinterpret_cast<bf16x8*>(p));
+  if constexpr (V & 2)
+    *reinterpret_cast<bf16x8*>(p) = v;
+  else
+    __builtin_nontemporal_store(v, reinterpret_cast<bf16x8*>(p));
 }
 template <int V>
 DRTC_DEVICE void w4_st8(bf16_t* p, bf16x4 v) {
-  __builtin_nontemporal_store(v, reinterpret_cast<bf16x4*>(p));
+  if constexpr (V & 2)
+    *reinterpret_cast<bf16x4*>(p) = v;
+  else
+    __builtin_nontemporal_store(v, reinterpret_cast<bf16x4*>(p));
 }
 
 template <int EPI, int V>
@@ -295,44 +318,176 @@ DRTC_DEVICE void w4_epilogue(const W4Params& p, f32x4 (&acc)[8][8], int tm, int 
 }
 
 // Split-K: publish this slice's fp32 partial tile, draw a ticket; the last arriver adds every
-// other slice's partials (cdna_hip_programming.md §5 'Projection GEMM at M = 256' item 2).
+// other slice's partials.  The slabs are written through (sc1 stores: no L2 write-back fence,
+// cdna_hip_programming.md §5 'Projection GEMM at M = 256' item 2 and the MI355X hand-off
+// table's counter row): every storing wave waits for its stores, a workgroup barrier, then
+// ONE lane's agent-scope atomic add; the workgroup whose add returns splitk - 1 reads the
+// other slabs with sc1 loads only (its other waves after the LDS flag + barrier).
 DRTC_DEVICE bool w4_splitk(const W4Params& p, f32x4 (&acc)[8][8], int tile, int slice,
                            char* lds) {
+  constexpr int kSc1 = 16;  // cache-policy bits of the buffer op: sc1
   const int tid = threadIdx.x;
-  const int64_t per_slice = 64ll * kW4Threads;  // f32x4 elements (256 KiB)
-  f32x4* mine = reinterpret_cast<f32x4*>(p.slab) + ((int64_t)tile * p.splitk + slice) * per_slice;
+  const int per_slice = 64 * kW4Threads * 16;  // bytes (256 KiB)
+  const __amdgpu_buffer_rsrc_t slab = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(reinterpret_cast<char*>(p.slab) + (int64_t)tile * p.splitk * per_slice), (short)0,
+      p.splitk * per_slice, 0x00020000);
+  const int mine = slice * per_slice + tid * 16;
 #pragma unroll
   for (int i = 0; i < 8; ++i)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) mine[(i * 8 + j) * kW4Threads + tid] = acc[i][j];
+    for (int j = 0; j < 8; ++j)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), slab,
+                                             mine + (i * 8 + j) * kW4Threads * 16, 0, kSc1);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   int* flag = reinterpret_cast<int*>(lds);
   if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const int t = __hip_atomic_fetch_add(p.counters + tile, 1, __ATOMIC_RELAXED,
                                          __HIP_MEMORY_SCOPE_AGENT);
     const int last = (t == p.splitk - 1);
-    if (last) {
-      __hip_atomic_store(p.counters + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    if (last) __hip_atomic_store(p.counters + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     *flag = last;
   }
   __syncthreads();
   if (!*flag) return false;
-  const f32x4* base = reinterpret_cast<const f32x4*>(p.slab) + (int64_t)tile * p.splitk * per_slice;
   for (int s = 0; s < p.splitk; ++s) {
     if (s == slice) continue;
-    const f32x4* src = base + s * per_slice;
+    const int src = s * per_slice + tid * 16;
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) acc[i][j] += src[(i * 8 + j) * kW4Threads + tid];
+      for (int j = 0; j < 8; ++j)
+        acc[i][j] += __builtin_bit_cast(
+            f32x4, __builtin_amdgcn_raw_buffer_load_b128(slab, src + (i * 8 + j) * kW4Threads * 16,
+                                                         0, kSc1));
   }
   return true;
+}
+
+// Output rows 256 tm + 128 wm + 16 i + 4 g + r (r = 0..3) of one row fragment i of a wave
+// block (wm, wn), from its 8 accumulators over the B fragments j (used by the reduce-scatter
+// split-K, where a block is finished by other waves than the one that computed it).
+template <int EPI, int V>
+DRTC_DEVICE void w4_epi_frag(const W4Params& p, const f32x4 (&v)[8], int tm, int tn, int wm,
+                             int wn, int i, int l16, int g) {
+  const int m0 = 256 * tm + 128 * wm + 16 * i + 4 * g;
+  if constexpr (w4_glu<EPI>()) {
+    const int n = 128 * tn + 64 * wn + 4 * l16;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      if (m0 + r >= p.M) continue;
+      bf16x4 o;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        o[j] = f2bf(act_value<EPI == W4_SILU ? 0 : 1>(v[j][r]) * v[j + 4][r]);
+      w4_st8<V>(p.c + (int64_t)(m0 + r) * p.ldc + n, o);
+    }
+  } else {
+    const int n = 256 * tn + 128 * wn + 8 * l16;
+    bf16x8 rv[4];
+    if constexpr (EPI == W4_RESIDUAL) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        rv[r] = *reinterpret_cast<const bf16x8*>(p.r + (int64_t)min(m0 + r, p.M - 1) * p.ldr + n);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      if (m0 + r >= p.M) continue;
+      bf16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float x = v[j][r];
+        if constexpr (EPI == W4_RESIDUAL) x += bf2f(rv[r][j]);
+        o[j] = f2bf(x);
+      }
+      w4_st16<V>(p.c + (int64_t)(m0 + r) * p.ldc + n, o);
+    }
+  }
+}
+
+// Reduce-scatter split-K (launch_gemm variant 11, splitk 2 or 4, every workgroup resident:
+// tiles x splitk <= CUs).  The tile's four 128 x 128 wave blocks are owned by the slices
+// (block b by slice b % splitk).  Every wave that does not own its block writes its fp32
+// partial (64 KiB) write-through (sc1) to slab[tile][b][slice]; the owner waves stage theirs
+// in LDS.  One lane per workgroup then adds to the tile's arrival counter (after every
+// storing wave's vmcnt(0) and a workgroup barrier) and polls it (sc1) until all slices
+// arrived - bounded, with the error word set on a timeout.  Each workgroup then finishes its
+// owned blocks with all four waves (8 row fragments per block spread over the waves), reading
+// the other slices' partials with sc1 loads only.  The last workgroup to leave re-arms the
+// counters.  Per workgroup 192 KiB written and 192 KiB read, in parallel on every CU, instead
+// of one last arriver reading (splitk - 1) x 256 KiB alone.
+template <int EPI, int V>
+DRTC_DEVICE void w4_splitk_rs(const W4Params& p, f32x4 (&acc)[8][8], int tile, int slice,
+                              int tm, int tn, int wv, int lane, int l16, int g, char* lds) {
+  constexpr int kSc1 = 16;
+  constexpr int kBlk = 64 * 64 * 16;  // one wave's partial block: 64 KiB
+  const int sk = p.splitk;
+  const __amdgpu_buffer_rsrc_t slab = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(reinterpret_cast<char*>(p.slab) + (int64_t)tile * 4 * sk * kBlk), (short)0,
+      4 * sk * kBlk, 0x00020000);
+  f32x4* L = reinterpret_cast<f32x4*>(lds);
+  if (wv % sk == slice) {  // owner: stage in LDS, slot wv / sk
+    f32x4* mine = L + (wv / sk) * 64 * 64 + lane;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) mine[(i * 8 + j) * 64] = acc[i][j];
+  } else {
+    const int base = (wv * sk + slice) * kBlk + lane * 16;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), slab,
+                                               base + (i * 8 + j) * 1024, 0, kSc1);
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+  int* arrive = p.counters + 2 * tile;
+  int* depart = arrive + 1;
+  if (threadIdx.x == 0) {
+    __hip_atomic_fetch_add(arrive, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int spins = 0;
+    while (__hip_atomic_load(arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < sk) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > (1 << 24)) {  // a slice never arrived: give up (never hang the GPU)
+        __hip_atomic_store(p.counters + p.tiles_m * p.tiles_n * 2, 1, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+  // owned blocks b = bi * sk + slice (bi < 4 / sk); row fragments f = bi * 8 + i, split evenly
+  // over the four waves
+  const int per = 8 * (4 / sk) / 4;
+  for (int f = wv * per; f < (wv + 1) * per; ++f) {
+    const int bi = f >> 3, i = f & 7, b = bi * sk + slice;
+    f32x4 v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = L[(bi * 64 + i * 8 + j) * 64 + lane];
+    for (int s2 = 0; s2 < sk; ++s2) {
+      if (s2 == slice) continue;
+      const int src = (b * sk + s2) * kBlk + (i * 8) * 1024 + lane * 16;
+      f32x4 w[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        w[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(slab, src + j * 1024,
+                                                                               0, kSc1));
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] += w[j];
+    }
+    w4_epi_frag<EPI, V>(p, v, tm, tn, b >> 1, b & 1, i, l16, g);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int t = __hip_atomic_fetch_add(depart, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (t == sk - 1) {  // every slice of the tile has read the slabs: re-arm
+      __hip_atomic_store(arrive, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(depart, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
 }
 
 template <int EPI, int V>
@@ -371,41 +526,42 @@ __global__ __launch_bounds__(kW4Threads, 1) void gemm_w4_kernel(W4Params p) {
       const int row = min(32 * s + 8 * wv + r8, rows_a - 1);
       d.va[s] = (unsigned)(row * p.lda * 2 + chunk * 16);
     }
-    // B rows are permuted on the way into LDS: LDS row 128 h + 16 j + l (wave column half h,
-    // fragment j, fragment row l) holds tile weight row 128 h + 8 l + j, so lane l16 of the
-    // MFMA output holds the 8 CONSECUTIVE columns 8 l16 .. 8 l16 + 7 over j = 0..7 (16-B
-    // epilogue stores).  Gated tiles: 64 output columns per half, fragments j < 4 the gate
-    // rows and j + 4 the up rows of columns 4 l + j.  DMA instruction s of wave wv fills LDS
-    // rows 32 s + 8 wv + r8, i.e. h = s >> 2, j = 2 (s & 3) + (wv >> 1), l = 8 (wv & 1) + r8.
+    // B: fragment j of wave column half h reads LDS rows 128 h + 8 l + j (l = lane & 15),
+    // so lane l16 of the MFMA output holds the 8 CONSECUTIVE columns 8 l16 .. 8 l16 + 7 over
+    // j = 0..7 (16-B epilogue stores).  Plain tiles keep tile row = LDS row.  Gated tiles:
+    // 64 output columns per half, LDS row 128 h + 8 l + j holds the gate row (j < 4) or the
+    // up row (j >= 4) of column 64 h + 4 l + (j & 3): each DMA instruction (8 LDS rows) loads
+    // 4 consecutive gate rows and the 4 matching up rows.  DMA instruction s of wave wv fills
+    // LDS rows 32 s + 8 wv + r8: h = s >> 2, l = 4 (s & 3) + wv, j = r8.
     const bf16_t* bbase;
     int brow;
     if constexpr (w4_glu<EPI>()) {
       bbase = p.b + (int64_t)(128 * tn) * p.ldb + k_base;
-      brow = 32 * (wv & 1) + 4 * r8 + (wv >> 1);
+      brow = 4 * wv + (r8 & 3) + (r8 >= 4 ? p.up_off : 0);
 #pragma unroll
       for (int s = 0; s < 8; ++s)
-        d.sb[s] = (unsigned)((64 * (s >> 2) + 2 * (s & 1) + ((s & 3) >= 2 ? p.up_off : 0)) *
-                             p.ldb * 2);
+        d.sb[s] = (unsigned)((64 * (s >> 2) + 16 * (s & 3)) * p.ldb * 2);
     } else {
       bbase = p.b + (int64_t)(256 * tn) * p.ldb + k_base;
-      brow = 64 * (wv & 1) + 8 * r8 + (wv >> 1);
+      brow = 8 * wv + r8;
 #pragma unroll
-      for (int s = 0; s < 8; ++s) d.sb[s] = (unsigned)((128 * (s >> 2) + 2 * (s & 3)) * p.ldb * 2);
+      for (int s = 0; s < 8; ++s) d.sb[s] = (unsigned)(32 * s * p.ldb * 2);
     }
     d.rb = __builtin_amdgcn_make_buffer_rsrc((void*)bbase, (short)0, 0x7FFFFFFF, 0x00020000);
     d.abase = reinterpret_cast<const char*>(abase);
     d.bbase = reinterpret_cast<const char*>(bbase);
-    d.vb = (unsigned)(brow * p.ldb * 2 + chunk * 16);
+    d.vb = (unsigned)(brow * p.ldb * 2 + (lane & 7) * 16);  // B: chunks in natural order
     d.lds_a = __builtin_amdgcn_readfirstlane(lds0 + 8 * wv * 128);
-    d.lds_b = __builtin_amdgcn_readfirstlane(lds0 + kW4BOff + 8 * wv * 128);
+    d.lds_b = __builtin_amdgcn_readfirstlane(lds0 + kW4BOff + wv * kW4BBlk);
   }
   // fragment read offsets (bytes within a stage): row 128 w + l16 (+ 16 per fragment), the
   // 16-B chunk 4 h + g stored at chunk ^ ((row >> 1) & 7)
   const int fx = (l16 >> 1) & 7;
   const int ra0 = (128 * wm + l16) * 128 + ((0 + g) ^ fx) * 16;
   const int ra1 = (128 * wm + l16) * 128 + ((4 + g) ^ fx) * 16;
-  const int rb0 = kW4BOff + (128 * wn + l16) * 128 + ((0 + g) ^ fx) * 16;
-  const int rb1 = kW4BOff + (128 * wn + l16) * 128 + ((4 + g) ^ fx) * 16;
+  // B: block 16 wn + l16 of the padded image, row j in it (+128 j), chunk 4 h + g
+  const int rb0 = kW4BOff + (16 * wn + l16) * kW4BBlk + g * 16;
+  const int rb1 = rb0 + 64;
   const char* lds = w4_lds;
 
   f32x4 acc[8][8];
@@ -414,19 +570,17 @@ __global__ __launch_bounds__(kW4Threads, 1) void gemm_w4_kernel(W4Params p) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  // K tiles run in the rotated order kst, kst + 1, ... (mod nk) when staggered (V & 4)
-  int kst = 0;
-  if constexpr ((V & 4) != 0) kst = (nk & 3) == 0 ? ((tm + tn) & 3) * (nk >> 2) : 0;
+  const int kst = 0;  // K tiles may run in a rotated order kst, kst + 1, ... (mod nk)
   const unsigned k0b = (unsigned)kst * 128u, k1b = (unsigned)(kst + 1 < nk ? kst + 1 : 0) * 128u;
   // ---- prologue: tiles 0 and 1 into stages 0 and 1
 #pragma unroll
-  for (int s = 0; s < 8; ++s) w4_dma(d.lds_b + 4096 * s, d.vb, d.rb, k0b + d.sb[s]);
+  for (int s = 0; s < 8; ++s) w4_dma(d.lds_b + 4 * kW4BBlk * s, d.vb, d.rb, k0b + d.sb[s]);
 #pragma unroll
   for (int s = 0; s < 8; ++s) w4_dma(d.lds_a + 4096 * s, d.va[s], d.ra, k0b);
   if (nk > 1) {
 #pragma unroll
     for (int s = 0; s < 8; ++s)
-      w4_dma(d.lds_b + kW4Stage + 4096 * s, d.vb, d.rb, k1b + d.sb[s]);
+      w4_dma(d.lds_b + kW4Stage + 4 * kW4BBlk * s, d.vb, d.rb, k1b + d.sb[s]);
 #pragma unroll
     for (int s = 0; s < 8; ++s) w4_dma(d.lds_a + kW4Stage + 4096 * s, d.va[s], d.ra, k1b);
     w4_vmcnt<16>();
@@ -437,7 +591,7 @@ __global__ __launch_bounds__(kW4Threads, 1) void gemm_w4_kernel(W4Params p) {
   bf16x8 fa0[8], fb0[8], fa1[8], fb1[8];
   fa0[0] = w4_rd(lds, ra0);
 #pragma unroll
-  for (int j = 0; j < 8; ++j) fb0[j] = w4_rd(lds, rb0 + 2048 * j);
+  for (int j = 0; j < 8; ++j) fb0[j] = w4_rd(lds, rb0 + 128 * j);
 #pragma unroll
   for (int i = 1; i < 8; ++i) fa0[i] = w4_rd(lds, ra0 + 2048 * i);
 
@@ -452,7 +606,13 @@ __global__ __launch_bounds__(kW4Threads, 1) void gemm_w4_kernel(W4Params p) {
   }
   w4_vmcnt<0>();  // no LDS-DMA may still be landing when the workgroup leaves
 
-  if (p.splitk > 1) {
+  if constexpr ((V & 4) != 0) {
+    if (p.splitk > 1) {
+      __syncthreads();
+      w4_splitk_rs<EPI, V>(p, acc, tile, slice, tm, tn, wv, lane, l16, g, w4_lds);
+      return;
+    }
+  } else if (p.splitk > 1) {
     __syncthreads();
     if (!w4_splitk(p, acc, tile, slice, w4_lds)) return;
   }
@@ -495,6 +655,17 @@ int w4_cfg() {
 
 }  // namespace
 
+int w4_num_cus() {
+  static int n = [] {
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return 0;
+    return cus;
+  }();
+  return n;
+}
+
 int launch_gemm_w4(void* c, const void* a, const void* b, const void* r, int M, int N, int K,
                    int lda, int ldb, int ldc, int ldr, int epi, int up_off, int splitk,
                    int group_m, void* slab, int64_t slab_bytes, int* counters, int n_counters,
@@ -525,9 +696,11 @@ int launch_gemm_w4(void* c, const void* a, const void* b, const void* r, int M, 
   p.group_m = group_m;
   if (splitk > 1) {
     const int64_t tiles = (int64_t)p.tiles_m * p.tiles_n;
-    if (slab == nullptr || counters == nullptr || n_counters < tiles ||
+    if (slab == nullptr || counters == nullptr || n_counters < 2 * tiles + 1 ||
         slab_bytes < tiles * splitk * 64ll * kW4Threads * 16)
       return -2;
+    // reduce-scatter form: 2 or 4 slices, and every workgroup resident at once (one per CU)
+    if ((v & 4) && ((splitk != 2 && splitk != 4) || tiles * splitk > w4_num_cus())) return -1;
     p.slab = (float*)slab;
     p.counters = counters;
   }

@@ -204,6 +204,9 @@ def linear(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
         N = w.shape[0]
         key = (M, N, K, x.stride(0))
         ent = _activate().get(key)
+        if ent is None and (sk := w4_rs_splitk(M, N, K)) and x.stride(0) % 8 == 0 \
+                and x.data_ptr() % 16 == 0:
+            return mfma_gemm(x, w, "store", variant=11, splitk=sk, group_m=4)
         if ent is None and M > DECODE_MAX_M:
             if w4_ok(x, w):
                 return mfma_gemm(x, w, "store", variant=W4_VARIANT, group_m=w4_group_m(M, N, K))
@@ -220,6 +223,8 @@ def linear(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
             return skinny_linear(x, w, ent[1])
         elif ent[2] and M <= MIDM_MAX_M:
             return midm_gemm(x, w, "store", splits=ent[2])
+        elif (sk := w4_rs_splitk(M, N, K)) and x.stride(0) % 8 == 0 and x.data_ptr() % 16 == 0:
+            return mfma_gemm(x, w, "store", variant=11, splitk=sk, group_m=4)
         elif ent[0] >= 0 and _plan(key):
             y = torch.empty((M, N), dtype=x.dtype, device=x.device)
             check(hipk().lt_gemm(y.data_ptr(), x.data_ptr(), w.data_ptr(), M, N, K, x.stride(0),
@@ -440,9 +445,31 @@ _w4_plain = os.environ.get("DRTC_W4_GEMM", "1") != "0"
 #   qkv (store), o (+residual)   0.98-0.99x                        -> hand
 #   down (K = 14336, +residual)  0.94-0.96x                        -> library (K > W4_MAX_K)
 # Decode buckets (M <= 1024) keep the tuned library / skinny / medium-M kernels.
-W4_GLU_MIN_M = int(os.environ.get("DRTC_W4_GLU_MIN_M", "4096"))
+# gate_up + GLU also wins at the larger decode buckets: 1.04x at M = 768, 1.06x at 1024
+# (library + act_glu), 0.97x at 512, 0.72x at 256 (profiles/r3b_w4_decode.md)
+W4_GLU_MIN_M = int(os.environ.get("DRTC_W4_GLU_MIN_M", "640"))
 W4_MIN_M = int(os.environ.get("DRTC_W4_MIN_M", "4096"))
 W4_MAX_K = int(os.environ.get("DRTC_W4_MAX_K", "8192"))
+# Decode buckets with few 256 x 256 tiles and a long K (Llama-3-8B down at M = 1024: 64 tiles,
+# K = 14336) can run gemm_w4 with the reduce-scatter split-K (variant 11): 1.13x the library
+# in isolation (weights cache-resident between calls), but 142 vs ~116 us inside the decode
+# step, where the weights stream from HBM (profiles/r3b_w4_decode.md) - off by default
+# (DRTC_W4_RS_MIN_M=768 turns it on).
+W4_RS_MIN_M = int(os.environ.get("DRTC_W4_RS_MIN_M", "100000"))  # off: see below
+W4_RS_MIN_K = int(os.environ.get("DRTC_W4_RS_MIN_K", "8192"))
+W4_RS_CUS = 256  # every workgroup resident: tiles x splitk <= CUs (MI355X)
+
+
+def w4_rs_splitk(M: int, N: int, K: int) -> int:
+    """Split of the reduce-scatter decode form for y[M, N] = x[M, K] W^T, 0 = not taken."""
+    if not (_w4_plain and W4_RS_MIN_M <= M <= DECODE_MAX_M and K >= W4_RS_MIN_K
+            and N % 256 == 0 and K % 64 == 0):
+        return 0
+    tiles = -(-M // 256) * (N // 256)
+    for sk in (4, 2):
+        if tiles * sk <= W4_RS_CUS and (K // 64) % sk == 0:
+            return sk
+    return 0
 
 
 def w4_group_m(M: int, N: int, K: int, glu: bool = False) -> int:
@@ -500,7 +527,7 @@ def norm_glu(p, w: torch.Tensor, act: str = "silu") -> torch.Tensor:
 
 __all__ = ["linear", "norm_linear", "glu_linear", "norm_glu", "w4_glu_ok", "skinny_linear", "skinny_ok", "skinny_variant",
            "skinny_supports", "mfma_gemm", "midm_gemm", "midm_supported", "dec_gemm", "dec_supported",
-           "tune", "save_entries", "w4_ok", "w4_group_m",
+           "tune", "save_entries", "w4_ok", "w4_group_m", "w4_rs_splitk",
            "load_table", "reset", "set_enabled", "table_path"]
 
 

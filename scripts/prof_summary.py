@@ -28,7 +28,7 @@ def short(name: str) -> str:
         for k in ("paged_decode_persist_kernel", "paged_decode_wave_kernel", "paged_decode_kernel",
                   "decode_reduce_kernel", "prefill_attn_persist_kernel", "prefill_attn_kernel",
                   "kv_write_v_kernel", "midm_reduce_kernel", "midm_kernel", "gemm_dec_kernel",
-                  "gemm256", "skinny", "rmsnorm_kernel", "act_glu_kernel", "rope_kv_kernel",
+                  "gemm_w4_kernel", "gemm256", "skinny", "rmsnorm_kernel", "act_glu_kernel", "rope_kv_kernel",
                   "sample_kernel", "moe_", "allreduce"):
             if k in name:
                 return "drtc::" + k

@@ -161,3 +161,22 @@ def test_linear_dispatches_midm_from_table(hipk):
     w = (torch.randn(4096, 14336, device="cuda", generator=g) * 0.02).to(torch.bfloat16)
     got = G.linear(x, w)
     assert _rel(got, x.float() @ w.float().t()) < 1e-2
+
+
+@pytest.mark.parametrize("epi", ["store", "residual", "silu"])
+@pytest.mark.parametrize("M,N,K,splitk", [(1024, 1024, 1024, 4), (300, 512, 2048, 2), (1024, 2048, 4096, 4),
+                                          (700, 768, 1536, 4)])
+def test_w4_reduce_scatter_splitk(hipk, epi, M, N, K, splitk):
+    """gemm_w4's reduce-scatter split-K (variant 11): every slice finishes part of the tile
+    from the others' write-through partials; counters re-arm for the next call (run twice)."""
+    g = torch.Generator(device="cuda").manual_seed(M + N + K + splitk)
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16, generator=g)
+    w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16, generator=g) * 0.05
+    nout = N // 2 if epi == "silu" else N
+    res = torch.randn(M, nout, device="cuda", dtype=torch.bfloat16, generator=g) if epi == "residual" else None
+    ref = _ref(x, w, epi, res)
+    for _ in range(2):
+        r_in = res.clone() if res is not None else None
+        out = G.mfma_gemm(x, w, epi, residual=r_in, out=r_in, variant=11, splitk=splitk)
+        torch.cuda.synchronize()
+        _check(out, ref)
