@@ -9,6 +9,13 @@ the sampled token ids.  Steps can be pipelined: the next step's input tokens
 are gathered from the previous step's samples on the device, so the engine
 enqueues step t+1 before it reads step t's tokens and the host bookkeeping of
 step t overlaps the GPU work of step t+1.
+
+Expert-parallel MoE models dispatch with a capacity factor (parallel/
+expert_parallel.py::ep_moe_a2a_cap).  The step's EP-group count of dropped
+(token, expert) pairs comes back with the sampled tokens; when it is nonzero
+:meth:`DecodeRunner.wait` re-runs that step - and every step launched after it,
+whose inputs depended on it - eagerly at worst-case capacity before returning,
+so the tokens never depend on the capacity.
 """
 from __future__ import annotations
 
@@ -77,6 +84,16 @@ class DecodeRunner:
         self.time_gpu = os.environ.get("DRTC_TIME_DECODE") == "1"
         self.gpu_ms: list[float] = []
         self._timing: dict[int, tuple] = {}  # staging set -> (start, end) events
+        # EP capacity-overflow redo: the input ids each step actually used and
+        # the dropped-pair count, read back with the tokens; launched steps
+        # not yet waited for, in launch order
+        self.ep = getattr(model, "ep_overflow", None) is not None
+        self.ids_used = torch.zeros(B, dtype=torch.int32, device=dev)
+        self.h_in = [torch.zeros(B, dtype=torch.int32, pin_memory=pin) for _ in range(2)]
+        self.h_ovf = [torch.zeros(1, dtype=torch.int32, pin_memory=pin) for _ in range(2)]
+        self._pending: list[dict] = []
+        self._step_no = 0
+        self.redo_steps = 0
 
     # ------------------------------------------------------------------
     def bucket(self, n: int) -> int:
@@ -105,6 +122,8 @@ class DecodeRunner:
         src = self.src[:Bb]
         ids = torch.where(src >= 0, self.out[:Bb].index_select(0, src.clamp(min=0)),
                           self.ids[:Bb])
+        if self.ep:
+            self.ids_used[:Bb].copy_(ids)
         logits = self.model.forward_decode(ids, meta, self.kv, self.attn_out[:Bb])
         ops.sample(logits, self.temp[:Bb], self.topk[:Bb], self.topp[:Bb], seed=self.seed,
                    step=self.step_ctr, out=self.out[:Bb])
@@ -190,16 +209,57 @@ class DecodeRunner:
         if timing:
             ev1.record()
             self._timing[k] = (ev0, ev1)
+        self._readback(n, k)
+        self._pending.append({"n": n, "k": k, "Bb": Bb, "step": self._step_no})
+        del self._pending[:-2]  # two staging sets: at most two steps in flight
+        self._step_no += 1
+        return n, k
+
+    def _readback(self, n: int, k: int) -> None:
+        nb = self.device.type == "cuda"
         self.h_out[k][:n].copy_(self.out[:n], non_blocking=nb)
+        if self.ep:
+            self.h_in[k][:n].copy_(self.ids_used[:n], non_blocking=nb)
+            self.h_ovf[k].copy_(self.model.ep_overflow.count, non_blocking=nb)
         if nb:
             self.events[k].record()
-        return n, k
+
+    def _redo_from(self, i: int) -> None:
+        """Re-run pending step i (its capacity dispatch dropped pairs) and
+        every later pending step, eagerly at worst-case EP capacity.  Step i
+        takes the input ids it used the first time; later steps take theirs
+        from the re-computed samples on the device, as when pipelined."""
+        from ..parallel.expert_parallel import worst_case_capacity
+
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+        B = self.max_batch
+        for j, p in enumerate(self._pending[i:]):
+            n, k = p["n"], p["k"]
+            if j == 0:
+                self.h_i32[k].numpy()[0:n] = self.h_in[k].numpy()[:n]
+                self.h_i64[k].numpy()[B:B + n] = -1
+            self.i32.copy_(self.h_i32[k])
+            self.i64.copy_(self.h_i64[k])
+            self.f32.copy_(self.h_f32[k])
+            self.step_ctr.fill_(p["step"])
+            with worst_case_capacity(), tracing.span("decode.ep_redo", bucket=p["Bb"]):
+                self._forward(p["Bb"])
+            self._readback(n, k)
+            self.redo_steps += 1
+        self.step_ctr.fill_(self._step_no)
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
 
     def wait(self, handle: tuple[int, int]) -> np.ndarray:
         """Sampled token ids of a launched step (blocks until it is done)."""
         n, k = handle
         if self.events[k] is not None:
             self.events[k].synchronize()
+        i = next(j for j, p in enumerate(self._pending) if p["k"] == k)
+        if self.ep and int(self.h_ovf[k][0]) > 0:
+            self._redo_from(i)
+        del self._pending[i]
         ev = self._timing.pop(k, None)
         if ev is not None:
             self.gpu_ms.append(ev[0].elapsed_time(ev[1]))

@@ -90,6 +90,7 @@ class LLMEngine:
                                    use_graphs=use_graphs, seed=seed, buckets=buckets)
         self.seed = seed
         self._prefill_step = 0
+        self._h_ovf: dict[int, torch.Tensor] = {}  # EP dropped-pair counts per prefill launch
         # slot state
         self.bt = np.zeros((max_batch, self.max_blocks), dtype=np.int32)
         self.ctx = np.zeros(max_batch, dtype=np.int32)        # tokens in the KV cache
@@ -379,8 +380,30 @@ class LLMEngine:
         for reqs, lens, h_tok, ev in launched:
             if ev is not None:
                 ev.synchronize()
+            h_tok = self._ep_redo_prefill(reqs, 0, h_tok)
             finished += self._finish_prefill(reqs, lens, h_tok.numpy())
         return finished
+
+    def _ep_redo_prefill(self, batch: list[Request], n_dec: int, h_tok):
+        """Capacity-factor EP dispatch (parallel/expert_parallel.py): when the
+        chunk's forward dropped (token, expert) pairs on any EP rank, run it
+        again at worst-case capacity (same KV slots, same requests; chunks are
+        independent, so the chunks launched after it stay valid)."""
+        ovf = self._h_ovf.pop(id(h_tok), None)
+        if ovf is None or int(ovf[0]) == 0:
+            return h_tok
+        from ..parallel.expert_parallel import worst_case_capacity
+
+        self._prefill_step -= 1  # same sampling stream as the first run
+        with worst_case_capacity():
+            _, _, h_tok, ev = self._launch_prefill(batch, n_dec=n_dec)
+        if ev is not None:
+            ev.synchronize()
+        self._h_ovf.pop(id(h_tok), None)
+        self.stats["prefill_steps"] -= 1
+        self.stats["prefill_tokens"] -= int(sum(r.num_tokens for r in batch))
+        self.stats["ep_redo_steps"] = self.stats.get("ep_redo_steps", 0) + 1
+        return h_tok
 
     def _launch_prefill(self, batch: list[Request], n_dec: int = 0):
         """Enqueue one packed prefill of ``batch``.  ``n_dec > 0`` makes it a
@@ -493,6 +516,11 @@ class LLMEngine:
         toks = ops.sample(logits, temp, topk, topp, seed=self.seed, step=step)
         h_tok = torch.empty(ns_all, dtype=torch.int32, pin_memory=cuda)
         h_tok.copy_(toks, non_blocking=cuda)
+        ovf = getattr(self.model, "ep_overflow", None)
+        if ovf is not None:  # EP dropped-pair count, read with the tokens
+            h_ovf = torch.empty(1, dtype=torch.int32, pin_memory=cuda)
+            h_ovf.copy_(ovf.count, non_blocking=cuda)
+            self._h_ovf[id(h_tok)] = h_ovf
         ev = None
         if cuda:
             ev = torch.cuda.Event()
@@ -529,6 +557,9 @@ class LLMEngine:
         n = len(self.running)
         reqs = list(self.running)
         _, lens, h_tok, ev = self._launch_prefill(batch, n_dec=n)
+        if ev is not None:
+            ev.synchronize()
+        h_tok = self._ep_redo_prefill(batch, n, h_tok)
         self.stats["mixed_steps"] += 1
         self.stats["decode_tokens"] += n
         self.ctx[:n] += 1

@@ -17,8 +17,10 @@ MI355X-first layout decisions
     dispatched to the expert owners and combined back over all-to-all
     (parallel/expert_parallel.py: exact splits in prefill, where the rows are
     already sequence-sharded; decode keeps replicated tokens + the EP
-    all-reduce unless DRTC_EP_DECODE=a2a selects the static-capacity,
-    graph-capturable all-to-all);
+    capacity-factor all-to-all in decode too: device-planned, graph-
+    capturable, overflow counted and redone at worst-case capacity by the
+    engine; DRTC_EP_DECODE=allreduce keeps replicated tokens + the EP
+    all-reduce);
   * decode is static-shaped (persistent metadata buffers) so the whole step
     is hipGraph-capturable by the engine.
 
@@ -40,7 +42,11 @@ from ..parallel.comm import ParallelContext, all_gather_into_tensor
 from .config import ModelConfig
 
 
-_EP_DECODE_A2A = os.environ.get("DRTC_EP_DECODE", "allreduce") == "a2a"
+# EP decode: the capacity-factor all-to-all (default) or the replicated-token
+# fused MoE + EP all-reduce (DRTC_EP_DECODE=allreduce); EP prefill: capacity
+# form (default) or exact splits with one host sync per layer (=exact)
+_EP_DECODE_A2A = os.environ.get("DRTC_EP_DECODE", "a2a") == "a2a"
+_EP_PREFILL = os.environ.get("DRTC_EP_PREFILL", "cap")
 
 
 @dataclass
@@ -121,6 +127,11 @@ class TransformerLM:
             self.moe_ws = _moe_ops.make_workspace(_moe_ops.MOE_CHUNK, cfg.hidden_size,
                                                   self.sh.expert_inter, self.sh.n_local_experts,
                                                   cfg.experts_per_token, self.device)
+        self.ep_overflow = None
+        self._ep_cap_used = False
+        if cfg.is_moe and self.pc.ep_size > 1:
+            from ..parallel.expert_parallel import EpOverflow
+            self.ep_overflow = EpOverflow(self.device)
 
     # ------------------------------------------------------------ weights
     def _init_weights(self, seed: int, full_then_shard: bool) -> None:
@@ -266,9 +277,26 @@ class TransformerLM:
 
         cfg, pc = self.cfg, self.pc
         topi, w = ep.route(x_rows, L["router"], cfg.experts_per_token)
-        fn = ep.ep_moe_a2a_static if static else ep.ep_moe_a2a
-        return fn(x_rows, topi, w, L["gate_up"], L["down"], cfg.act, pc.ep_group,
-                  cfg.num_experts, self.moe_ws)
+        if static or _EP_PREFILL != "exact":
+            self._ep_cap_used = True
+            return ep.ep_moe_a2a_cap(x_rows, topi, w, L["gate_up"], L["down"], cfg.act,
+                                     pc.ep_group, cfg.num_experts, self.moe_ws,
+                                     overflow=self.ep_overflow)
+        return ep.ep_moe_a2a(x_rows, topi, w, L["gate_up"], L["down"], cfg.act, pc.ep_group,
+                             cfg.num_experts, self.moe_ws)
+
+    def _ep_begin(self) -> None:
+        """Start of a forward pass: zero the EP overflow counter."""
+        if self.ep_overflow is not None:
+            self.ep_overflow.reset()
+        self._ep_cap_used = False
+
+    def _ep_end(self, logits: torch.Tensor) -> torch.Tensor:
+        """End of a forward pass: sum the dropped-pair counts over the EP group
+        (every rank took the same dispatch path, so all call the collective)."""
+        if self.ep_overflow is not None and self._ep_cap_used:
+            self.ep_overflow.reduce(self.pc.ep_group)
+        return logits
 
     def _moe(self, L: dict, x: torch.Tensor, decode: bool = False) -> torch.Tensor:
         """Top-k routed experts (Mixtral: softmax over the top-2 logits).
@@ -344,8 +372,9 @@ class TransformerLM:
         """Packed varlen prefill (optionally with decode rows appended, see
         PrefillMeta.decode). Returns logits of the rows in ``meta.last_idx``:
         each sequence's last token, then every decode row."""
+        self._ep_begin()
         if meta.decode is None and self.pc.sp_ok(ids.shape[0]):
-            return self._forward_prefill_sp(ids, meta, kv_caches)
+            return self._ep_end(self._forward_prefill_sp(ids, meta, kv_caches))
         cfg, sh = self.cfg, self.sh
         D = cfg.head_dim
 
@@ -378,7 +407,7 @@ class TransformerLM:
 
         last = len(self.layers) - 1
         x = self._layers(self._embed(ids), attn)
-        return self._logits(x)
+        return self._ep_end(self._logits(x))
 
     def _attn_mixed(self, qkv: torch.Tensor, meta: PrefillMeta, kc, vc) -> torch.Tensor:
         """Attention of a mixed step: causal varlen attention over the prefill
@@ -503,8 +532,9 @@ class TransformerLM:
                 return o, False, True  # reduced by the next norm (fused all-reduce + add + norm)
             return o, False
 
+        self._ep_begin()
         x = self._layers(self._embed(ids), attn, decode=True)
-        return self._logits(x)
+        return self._ep_end(self._logits(x))
 
     # ------------------------------------------------------------ reference
     def forward_reference(self, ids_list: list[list[int]]) -> list[torch.Tensor]:

@@ -36,13 +36,61 @@ def _ep_worker(rank, world, port, q):
     x = x_all[rank * 13:(rank + 1) * 13]
     el = E // world
     ref = moe_reference(x_all, router, gu, dn, k)[rank * 13:(rank + 1) * 13]
+    from drtc_amd.parallel.expert_parallel import EpOverflow, worst_case_capacity
+
     errs = []
-    for static in (False, True):
-        y = ep_moe_forward(x, router, gu[rank * el:(rank + 1) * el], dn[rank * el:(rank + 1) * el],
-                           k, static=static)
+    gl, dl = gu[rank * el:(rank + 1) * el], dn[rank * el:(rank + 1) * el]
+    for form in ("exact", "static", "cap"):
+        ovf = EpOverflow("cpu")
+        y = ep_moe_forward(x, router, gl, dl, k, form=form, overflow=ovf)
         errs.append((y.float() - ref.float()).abs().max().item())
-    q.put((rank, errs))
+        assert int(ovf.count) == 0, form  # cf 2 over 2 ranks = worst case here
+    # a capacity factor too small for the routing: pairs are dropped and counted,
+    # and the redo at worst-case capacity is exact again
+    ovf = EpOverflow("cpu")
+    y_small = ep_moe_forward(x, router, gl, dl, k, form="cap", overflow=ovf, cf=0.3)
+    ovf.reduce(None)
+    with worst_case_capacity():
+        y_redo = ep_moe_forward(x, router, gl, dl, k, form="cap", cf=0.3)
+    errs.append((y_redo.float() - ref.float()).abs().max().item())
+    q.put((rank, errs, int(ovf.count), (y_small.float() - ref.float()).abs().max().item()))
     dist.destroy_process_group()
+
+
+def test_ep_plan_semantics():
+    """ep_plan: slots in (token, pick) order per owner, inverse maps, drops."""
+    from drtc_amd.parallel.expert_parallel import ep_combine, ep_gather, ep_plan
+
+    g = torch.Generator().manual_seed(3)
+    T, k, world, e_local = 37, 2, 4, 2
+    topi = torch.stack([torch.randperm(world * e_local, generator=g)[:k] for _ in range(T)])
+    for cap in (T * k, 24, 8, 3):
+        ovf = torch.zeros(1, dtype=torch.int32)
+        dst, sp, se = ep_plan(topi, e_local, world, cap, ovf)
+        owner = topi.reshape(-1) // e_local
+        dropped = 0
+        for d in range(world):
+            pairs = torch.nonzero(owner == d).flatten()  # ascending = (token, pick) order
+            for s, p in enumerate(pairs.tolist()):
+                if s < cap:
+                    assert dst[p] == d * cap + s and sp[d * cap + s] == p
+                    assert se[d * cap + s] == topi.reshape(-1)[p]
+                else:
+                    assert dst[p] == -1
+                    dropped += 1
+            n_real = min(cap, pairs.numel())
+            assert (sp[d * cap + n_real:(d + 1) * cap] == -1).all()
+            assert (se[d * cap + n_real:(d + 1) * cap] == -1).all()
+        assert int(ovf) == dropped
+        x = torch.randn(T, 16, generator=g).to(torch.bfloat16)
+        sx = ep_gather(x, sp, k)
+        real = sp >= 0
+        assert torch.equal(sx[real], x[sp[real].long() // k])
+        w = torch.rand(T, k, generator=g)
+        out = ep_combine(sx, dst, w, T, k)  # back == send rows: sum_j w_j x_t over kept picks
+        keep = (dst >= 0).view(T, k).float()
+        want = (x.float().unsqueeze(1) * (w * keep).unsqueeze(-1)).sum(1).to(torch.bfloat16)
+        assert torch.equal(out, want)
 
 
 def _tp_worker(rank, world, port, q):
@@ -154,6 +202,38 @@ def _tp_mixed_worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
+def _ep_redo_worker(rank, world, port, q):
+    """EP=2 Mixtral engines with a capacity factor far too small for the
+    routing: every overflowing prefill chunk and (pipelined) decode step is
+    redone at worst-case capacity, so the tokens equal a run that never
+    overflows; both ranks agree."""
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import drtc_amd.parallel.expert_parallel as ep
+    from drtc_amd.engine import LLMEngine, Request, SamplingParams
+    from drtc_amd.models import TINY_MIXTRAL, TransformerLM
+    from drtc_amd.parallel.comm import ParallelContext
+
+    pc = ParallelContext.from_world(tp=True, ep=True)
+    model = TransformerLM(TINY_MIXTRAL, "cpu", pc=pc, seed=4)
+    prompts = [list(range(5 + i, 29 + 3 * i)) for i in range(6)]
+    res = {}
+    for cf in (8.0, 0.2):
+        ep.EP_CF = cf
+        eng = LLMEngine(model, max_batch=8, max_model_len=256, num_blocks=64, use_graphs=False)
+        prm = SamplingParams.greedy(12, ignore_eos=True)
+        reqs = [eng.add_request(Request(list(p), prm)) for p in prompts]
+        while eng.has_work():
+            eng.step()
+        res[cf] = {"out": [r.output_ids for r in reqs],
+                   "prefill_redo": eng.stats.get("ep_redo_steps", 0),
+                   "decode_redo": eng.runner.redo_steps,
+                   "pipelined": eng.stats["decode_steps_pipelined"]}
+    q.put((rank, res))
+    dist.destroy_process_group()
+
+
 def _capped(fn, rank, world, port, q):
     # each rank gets its share of the CPUs: 2 ranks x all cores oversubscribe
     # the machine (and more so under pytest -n), which made the mixed-step test
@@ -177,8 +257,11 @@ def _run(fn, world=2):
 
 
 def test_ep_all_to_all_matches_reference():
-    for rank, errs in _run(_ep_worker):
+    res = _run(_ep_worker)
+    for rank, errs, dropped, err_small in res:
         assert max(errs) == 0.0, (rank, errs)  # same bf16 roundings, fp32 combine
+        assert dropped > 0 and err_small > 0, (rank, dropped)
+    assert res[0][2] == res[1][2]  # the EP-group sum: the same redo decision everywhere
 
 
 def test_tp_and_ep_model_forward_matches_single_process():
@@ -203,3 +286,14 @@ def test_tp_mixed_prefill_decode_steps_match_tp1():
         assert a["tp"] == a["tp_prefill_first"], name
         if a["dense"]:
             assert a["tp"] == a["ref"], name
+
+
+def test_ep_capacity_overflow_redo_is_exact():
+    res = dict(_run(_ep_redo_worker))
+    for rank in (0, 1):
+        big, small = res[rank][8.0], res[rank][0.2]
+        assert big["prefill_redo"] == big["decode_redo"] == 0
+        assert small["prefill_redo"] > 0 and small["decode_redo"] > 0, small
+        assert small["pipelined"] > 0
+        assert small["out"] == big["out"]
+    assert res[0][0.2]["out"] == res[1][0.2]["out"]
