@@ -53,6 +53,9 @@ class Request:
     finish_time: float = 0.0
     num_preemptions: int = 0
     _done: threading.Event = field(default_factory=threading.Event, repr=False)
+    # called once with the request when it finishes (engine thread): lets a server
+    # collect completions from a queue instead of polling every pending request
+    on_done: object = field(default=None, repr=False, compare=False)
 
     def __post_init__(self):
         if not self.request_id:
@@ -82,3 +85,7 @@ class Request:
         self.finish_reason = reason
         self.finish_time = time.perf_counter()
         self._done.set()
+        cb = self.on_done
+        if cb is not None:
+            self.on_done = None  # at most once (an abort may race a normal finish)
+            cb(self)

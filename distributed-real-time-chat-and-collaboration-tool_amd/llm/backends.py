@@ -123,6 +123,11 @@ def _worker_main(rank: int, device: str, model_name: str, engine_kw: dict, inq, 
         return
     pending = {}
     parent = os.getppid()
+    # finished requests arrive here from the engine thread (Request.on_done): the watcher
+    # blocks on it instead of scanning every pending request each millisecond (a Python loop
+    # over ~1k requests, 1000 times a second, that held the GIL against the engine's own
+    # host work), and ships each burst of completions as ONE queue message
+    done_q: queue.SimpleQueue = queue.SimpleQueue()
 
     def watcher():
         last_hb = 0.0
@@ -132,10 +137,20 @@ def _worker_main(rank: int, device: str, model_name: str, engine_kw: dict, inq, 
                 # do not stay behind holding the GPU and its KV cache
                 log.error("engine replica %d: parent process gone, exiting", rank)
                 os._exit(0)
-            for rid, r in list(pending.items()):
-                if r._done.is_set():
-                    pending.pop(rid, None)
-                    outq.put(("done", rid, (r.output_ids, r.finish_reason)))
+            batch = []
+            try:
+                batch.append(done_q.get(timeout=min(0.05, hb_interval)))
+                while True:
+                    batch.append(done_q.get_nowait())
+            except queue.Empty:
+                pass
+            if batch:
+                out = []
+                for r in batch:
+                    if pending.pop(r.request_id, None) is not None:
+                        out.append((r.request_id, (r.output_ids, r.finish_reason)))
+                if out:
+                    outq.put(("done_batch", rank, out))
             if not loop.alive():  # engine fault: exit so the parent evicts/respawns us
                 log.error("engine loop of replica %d died: %r", rank, loop.error)
                 os._exit(3)
@@ -146,7 +161,6 @@ def _worker_main(rank: int, device: str, model_name: str, engine_kw: dict, inq, 
                 st.update(running=len(eng.running), waiting=len(eng.waiting),
                           pending=len(pending), alive=loop.alive())
                 outq.put(("hb", rank, st))
-            time.sleep(0.001)
 
     threading.Thread(target=watcher, daemon=True).start()
     while True:
@@ -159,7 +173,7 @@ def _worker_main(rank: int, device: str, model_name: str, engine_kw: dict, inq, 
                 eng.abort(r)
             continue
         rid, ids, prm = msg
-        r = Request(ids, prm, request_id=rid)
+        r = Request(ids, prm, request_id=rid, on_done=done_q.put)
         pending[rid] = r
         try:
             loop.submit(r)
@@ -245,15 +259,23 @@ class WorkerPool:
             if kind == "fatal":
                 log.error("engine replica %s failed to start: %s", rid, payload)
                 continue
-            if kind != "done":
+            if kind == "done":
+                items = [(rid, payload)]
+            elif kind == "done_batch":  # every completion of one engine step, one message
+                items = payload
+            else:
                 continue
+            ready = []
             with self._lock:
-                ev, slot, w = self.futures.get(rid, (None, None, None))
-                if ev is None or slot:
-                    continue
-                slot.append(payload)
-                self.load[w] -= 1
-            ev.set()
+                for rid, res in items:
+                    ev, slot, w = self.futures.get(rid, (None, None, None))
+                    if ev is None or slot:
+                        continue
+                    slot.append(res)
+                    self.load[w] -= 1
+                    ready.append(ev)
+            for ev in ready:
+                ev.set()
 
     def _monitor(self):
         while not self._closed:

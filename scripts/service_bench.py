@@ -70,7 +70,7 @@ def build_backend(args):
 
 def run_load(target, n_requests: int, threads: int, seed: int):
     """``threads`` client threads issue ``n_requests`` GetSmartReply RPCs in
-    total; returns (latencies s, errors, wall start, wall end)."""
+    total; returns (latencies s, errors, wall start, wall end, finish wall times)."""
     mode, address, token = target
     rng = random.Random(seed)
     if mode == "raft":
@@ -89,6 +89,7 @@ def run_load(target, n_requests: int, threads: int, seed: int):
             assert len(r.suggestions) == 3
         stubs = [make_stub(grpc.insecure_channel(address), LLM_SERVICE) for _ in range(8)]
     lat, errors, lock, it = [], [], threading.Lock(), iter(range(n_requests))
+    fin = []
 
     def worker(k):
         stub = stubs[k % len(stubs)]
@@ -105,11 +106,12 @@ def run_load(target, n_requests: int, threads: int, seed: int):
                 continue
             with lock:
                 lat.append(time.perf_counter() - t)
+                fin.append(time.time())
     ths = [threading.Thread(target=worker, args=(k,)) for k in range(threads)]
     t_start = time.time()
     [t.start() for t in ths]
     [t.join() for t in ths]
-    return lat, errors, t_start, time.time()
+    return lat, errors, t_start, time.time(), fin
 
 
 def run_open_loop(target, n_requests: int, rate: float, seed: int):
@@ -160,7 +162,7 @@ def run_open_loop(target, n_requests: int, rate: float, seed: int):
         f.add_done_callback(lambda fut, ts=t0 + t: on_done(fut, ts))
     for _ in range(n_requests):
         done.acquire()
-    return lat, errors, t_start, time.time()
+    return lat, errors, t_start, time.time(), []
 
 
 def _client_main(target, n_requests, threads, seed, q):
@@ -211,7 +213,7 @@ def main():
             eng.stats.clear()
         METRICS.reset()
         if args.arrival_rate > 0:
-            lat, errors, t_s, t_e = run_open_loop(target, args.requests, args.arrival_rate, 1)
+            lat, errors, t_s, t_e, fin = run_open_loop(target, args.requests, args.arrival_rate, 1)
             dt = t_e - t_s
         elif args.client_procs > 0:  # clients outside this process (no shared GIL)
             ctx = mp.get_context("spawn")
@@ -222,18 +224,24 @@ def main():
                                        args.concurrency // k + (i < args.concurrency % k), i + 1, q))
                      for i in range(k)]
             [p.start() for p in procs]
-            lat, errors, starts, ends = [], [], [], []
+            lat, errors, starts, ends, fin = [], [], [], [], []
             for _ in procs:
-                la, er, t_s, t_e = q.get()
+                la, er, t_s, t_e, fi = q.get()
                 lat += la
                 errors += er
+                fin += fi
                 starts.append(t_s)
                 ends.append(t_e)
             [p.join() for p in procs]
-            dt = max(ends) - min(starts)
+            t_s = min(starts)
+            dt = max(ends) - t_s
         else:
-            lat, errors, t_s, t_e = run_load(target, args.requests, args.concurrency, 1)
+            lat, errors, t_s, t_e, fin = run_load(target, args.requests, args.concurrency, 1)
             dt = t_e - t_s
+        # steady-state service rate: completions in the 20-90 % part of the run (the
+        # whole-run rate also counts the clients' ramp-up and the drain of the last batch)
+        w0, w1 = t_s + 0.2 * dt, t_s + 0.9 * dt
+        steady = sum(1 for f in fin if w0 <= f < w1) / (w1 - w0) if fin else None
         lat.sort()
         gen_tokens = (len(lat) * fp.smart.max_new_tokens) if args.backend != "scripted" else 0
         hist = METRICS.snapshot()["histograms"]
@@ -250,6 +258,9 @@ def main():
             "requests": len(lat), "errors": len(errors), "concurrency": args.concurrency, "seconds": round(dt, 3),
             "requests_per_s": round(len(lat) / dt, 2),
             "gen_tokens_per_s": round(gen_tokens / dt, 1) if gen_tokens else None,
+            "steady_requests_per_s": round(steady, 2) if steady else None,
+            "steady_gen_tokens_per_s": (round(steady * fp.smart.max_new_tokens, 1)
+                                        if steady and args.backend != "scripted" else None),
             "p50_latency_ms": round(1000 * statistics.median(lat), 1),
             "p99_latency_ms": round(1000 * lat[min(len(lat) - 1, int(0.99 * (len(lat) - 1)))], 1),
             "engine_stats": dict(eng.stats) if eng else None,

@@ -28,12 +28,21 @@ def main():
     ap.add_argument("--group-m", type=int, default=8)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--rotate", type=int, default=1,
+                    help="cycle through this many weight copies (> the 256 MB MALL in total: "
+                         "weights stream from HBM as inside a model step)")
     a = ap.parse_args()
     M, N, K = (int(v) for v in a.shape.split(","))
     dev = torch.device("cuda")
     torch.manual_seed(0)
     x = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
-    w = torch.randn(N, K, device=dev, dtype=torch.bfloat16) * 0.02
+    ws = [torch.randn(N, K, device=dev, dtype=torch.bfloat16) * 0.02 for _ in range(a.rotate)]
+    w = ws[0]
+    cur = [0]
+
+    def nxt():  # the weight copy of the next call (same copy when --rotate 1)
+        cur[0] = (cur[0] + 1) % a.rotate
+        return ws[cur[0]]
     glu = a.epi in ("silu", "gelu_tanh")
     nout = N // 2 if glu else N
     res = torch.randn(M, nout, device=dev, dtype=torch.bfloat16) if a.epi == "residual" else None
@@ -43,18 +52,18 @@ def main():
     for arm in a.arms.split(","):
         if arm == "lib":
             if a.epi == "residual":
-                fns[arm] = lambda: res.addmm_(x, w.t())
+                fns[arm] = lambda: res.addmm_(x, nxt().t())
             elif glu:
-                fns[arm] = lambda: ops.act_glu(ops.linear(x, w), a.epi)
+                fns[arm] = lambda: ops.act_glu(ops.linear(x, nxt()), a.epi)
             else:
-                fns[arm] = lambda: ops.linear(x, w)
+                fns[arm] = lambda: ops.linear(x, nxt())
         else:
             v = int(arm[1:])
             if a.epi == "residual":
-                fns[arm] = (lambda v=v: G.mfma_gemm(x, w, "residual", residual=res, out=res,
+                fns[arm] = (lambda v=v: G.mfma_gemm(x, nxt(), "residual", residual=res, out=res,
                                                     variant=v, splitk=a.splitk, group_m=a.group_m))
             else:
-                fns[arm] = (lambda v=v: G.mfma_gemm(x, w, a.epi, out=out, variant=v,
+                fns[arm] = (lambda v=v: G.mfma_gemm(x, nxt(), a.epi, out=out, variant=v,
                                                     splitk=a.splitk, group_m=a.group_m))
     # correctness of every hand arm against an fp32 reference (one call each)
     ref = x.float() @ w.float().t()
@@ -67,6 +76,7 @@ def main():
     for k, f in fns.items():
         if k == "lib":
             continue
+        cur[0] = a.rotate - 1  # the next call uses ws[0] = w
         if a.epi == "residual":
             r0 = res.clone()
             f()
@@ -92,7 +102,8 @@ def main():
     fl = 2.0 * M * N * K
     for k, ts in times.items():
         med = statistics.median(ts)
-        print(json.dumps({"shape": [M, N, K], "epi": a.epi, "arm": k, "us_med": round(med, 1),
+        print(json.dumps({"shape": [M, N, K], "epi": a.epi, "arm": k, "splitk": a.splitk,
+                          "rotate": a.rotate, "us_med": round(med, 1),
                           "us_min": round(min(ts), 1), "TFLOPs": round(fl / med / 1e6, 1),
                           "err": errs.get(k)}),
               flush=True)

@@ -437,6 +437,47 @@ def test_sample_top_k_heavy_ties_fallback(hipk):
     assert torch.isin(out[32:], torch.tensor([5, 900, 31999])).all()
 
 
+def test_sample_topk_register_path_headline_shape(hipk):
+    """Register-resident top-k (rows <= 131072 tokens): the headline sampling mode
+    (top-k 64, top-p 0.95) on Llama-3-sized rows, as a strided view whose length is
+    not a multiple of 8 (the per-thread tail element).  Every draw is inside the
+    top-k set and inside the top-p prefix of the candidates sorted by (value desc,
+    index asc); frequencies on a 3-token row with one leader in the tail match the
+    softmax."""
+    torch.manual_seed(8)
+    B, LD, V, K, P = 256, 128256, 128251, 64, 0.95
+    full = (torch.randn(B, LD, device=DEV) * 2).to(torch.bfloat16)
+    logits = full[:, :V]
+    temp = torch.ones(B, device=DEV)
+    k = torch.full((B,), K, dtype=torch.int32, device=DEV)
+    p = torch.full((B,), P, device=DEV)
+    step = torch.zeros(1, dtype=torch.int64, device=DEV)
+    lf = logits.float()
+    vals, idx = torch.sort(lf, dim=-1, descending=True, stable=True)
+    kth = vals[:, K - 1:K]
+    for i in range(4):
+        step.fill_(i)
+        out = ops.sample(logits, temp, k, p, seed=13, step=step).long()
+        picked = lf.gather(1, out[:, None])
+        assert (picked >= kth).all()
+        # exclusive softmax mass (over the top-k candidates) ahead of the pick
+        cand = vals[:, :K]
+        pr = torch.softmax(cand, -1)
+        pos = (idx[:, :K] == out[:, None]).float().argmax(-1)
+        excl = (torch.cumsum(pr, -1) - pr).gather(1, pos[:, None])[:, 0]
+        assert (excl < P + 1e-3).all(), excl.max()
+    R = 4096
+    row = torch.full((LD,), -30.0)
+    row[11], row[70000], row[V - 2] = 2.0, 1.0, 0.0  # V - 2: a tail token of the view
+    lg = row.to(torch.bfloat16).to(DEV).repeat(R, 1)[:, :V]
+    out = ops.sample(lg, torch.ones(R, device=DEV), torch.full((R,), 3, dtype=torch.int32, device=DEV),
+                     torch.ones(R, device=DEV), seed=4).long().cpu()
+    f = torch.bincount(out, minlength=V)[[11, 70000, V - 2]].float() / R
+    e = torch.softmax(torch.tensor([2.0, 1.0, 0.0]), 0)
+    assert abs(f.sum().item() - 1.0) < 1e-6
+    assert (f - e).abs().max() < 0.03, (f, e)
+
+
 def _moe_inputs(T, H, I, E, seed=0):
     g = torch.Generator(device=DEV).manual_seed(seed)
     x = torch.randn(T, H, device=DEV, generator=g).to(torch.bfloat16)
