@@ -459,14 +459,59 @@ DRTC_DEVICE void load_kv_block_n(KVRegs<D>& r, const bf16_t* kb, const bf16_t* v
 // pays it once per ~6-block chat context).  Tokens past the context in a
 // partial last block are not fetched (load_kv_block_n).  Math per block is
 // variant 2's; per-item outputs / partials likewise.
+// Fused RoPE + KV write (ROPE = true; engine decode steps): q / k / v of the step's token
+// come unrotated straight from the QKV GEMM output (q = its row base, k / v at +Hq*D /
+// +(Hq+Hkv)*D), replacing the rope_kv launch of every layer:
+//   * each item rotates its G query heads in registers when it starts (NeoX halves: dims
+//     32s + 8g + j and D/2 + 32s + 8g + j sit in the same lane, fragments s and s + KS/2);
+//   * the cache holds tokens [0, ctx - 1); the step's token (position ctx - 1, its cache row
+//     not yet written) is masked out of the block loop (its probability forced to 0, its
+//     row not fetched); the item of the LAST partition opens its online softmax with it
+//     from registers instead: k rotated the same way, q.k reduced over the 4 lane groups,
+//     m = that score, p = 1, o = its v row;
+//   * that item also writes the rotated k row and the v row into the paged cache (slot from
+//     `slots`) for the next steps - the same bytes rope_kv_kernel_v2 writes.
+struct DecodeRope {
+  const int* positions;
+  const int64_t* slots;
+  const float* cos_sin;   // [max_pos][D]: cos | sin
+  bf16_t* k_cache;        // the caches the kernel reads (written for the step's token)
+  bf16_t* v_cache;
+};
+
+// rotate the lane's fragments f[0..KS) of one head (position pos), rounding as rope_kv
 template <int D>
+DRTC_DEVICE void rope_frags(bf16x8* f, const float* __restrict__ cos_sin, int pos, int g) {
+  constexpr int KS = D / 32;
+  const float* cs = cos_sin + (int64_t)pos * D + 8 * g;
+#pragma unroll
+  for (int s = 0; s < KS / 2; ++s) {
+    const f32x4 ca = *reinterpret_cast<const f32x4*>(cs + 32 * s);
+    const f32x4 cb = *reinterpret_cast<const f32x4*>(cs + 32 * s + 4);
+    const f32x4 sa = *reinterpret_cast<const f32x4*>(cs + D / 2 + 32 * s);
+    const f32x4 sb = *reinterpret_cast<const f32x4*>(cs + D / 2 + 32 * s + 4);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float c = j < 4 ? ca[j] : cb[j - 4];
+      const float sn = j < 4 ? sa[j] : sb[j - 4];
+      const float a = bf2f(f[s][j]), b = bf2f(f[s + KS / 2][j]);
+      f[s][j] = f2bf(a * c - b * sn);
+      f[s + KS / 2][j] = f2bf(b * c + a * sn);
+    }
+    // one fragment pair's cos / sin (16 VGPRs) live at a time: this runs beside a whole
+    // prefetched K/V block in the persistent kernel, at its register ceiling
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+template <int D, bool ROPE>
 __global__ __launch_bounds__(256, D >= 256 ? 1 : 2) void paged_decode_persist_kernel(
     bf16_t* __restrict__ out, float* __restrict__ part_o,
     float* __restrict__ part_ml, const bf16_t* __restrict__ q, int q_stride,
     const bf16_t* __restrict__ k_cache, const bf16_t* __restrict__ v_cache,
     const int* __restrict__ block_tables, int bt_stride,
     const int* __restrict__ context_lens, int B, int Hq, int Hkv, float scale_log2e,
-    int max_parts, int blocks_per_part) {
+    int max_parts, int blocks_per_part, DecodeRope rope) {
   constexpr int NT = D / 16;
   constexpr int KS = D / 32;
   const int lane = threadIdx.x & 63;
@@ -516,20 +561,73 @@ __global__ __launch_bounds__(256, D >= 256 ? 1 : 2) void paged_decode_persist_ke
     const int* bt = block_tables + (int64_t)A.b * bt_stride;
     return (chunk + lane < A.end) ? bt[chunk + lane] : 0;
   };
+  // tokens read from the cache: all of the context, or (ROPE) all but the step's own token
+  auto cached = [&](const Item& A) { return ROPE ? A.ctx - 1 : A.ctx; };
   auto load_blk = [&](KVRegs<D>& r, const Item& A, int64_t phys, int blk) {
     load_kv_block_n<D>(r, k_cache + (phys * Hkv + A.h) * blk_elems,
-                       v_cache + (phys * Hkv + A.h) * blk_elems, lane, A.ctx - blk * kBS);
+                       v_cache + (phys * Hkv + A.h) * blk_elems, lane, cached(A) - blk * kBS);
+  };
+  auto rope_q = [&](bf16x8* qf, const Item& A) {
+    if constexpr (ROPE)
+      rope_frags<D>(qf, rope.cos_sin, __builtin_amdgcn_readfirstlane(rope.positions[A.b]), g);
   };
 
   Item A = next_item(blockIdx.x * 4 + wave_id_uniform());
   if (A.it >= n_items) return;
   bf16x8 qf[KS], qn[KS];
   load_q(qf, A);
+  rope_q(qf, A);
   int chunk = A.begin;  // block-table slice [chunk, chunk + 64) of item A in bt_reg
   int bt_reg = load_bt(A, chunk);
   KVRegs<D> cur, nxt;
   load_blk(cur, A, __builtin_amdgcn_readlane(bt_reg, 0), A.begin);
   while (true) {
+    f32x4 o[NT];
+#pragma unroll
+    for (int i = 0; i < NT; ++i) o[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    float m = kNegBig, lsum = 0.f;
+    if constexpr (ROPE) {
+      if (A.it / BH == A.nparts - 1) {
+        // the partition holding the step's token: it opens the online softmax (m = its
+        // score, p = 1 counted once in lane group 0, o = its v row), before the next
+        // item's loads are issued (fewest live registers)
+        const bf16_t* kn = q + (int64_t)A.b * q_stride + (int64_t)(Hq + A.h) * D;
+        const bf16_t* vn = kn + (int64_t)Hkv * D;
+        bf16x8 kf[KS];
+#pragma unroll
+        for (int s = 0; s < KS; ++s) kf[s] = load_bf16x8(kn + 32 * s + 8 * g);
+        rope_frags<D>(kf, rope.cos_sin, __builtin_amdgcn_readfirstlane(rope.positions[A.b]), g);
+        float dot = 0.f;
+#pragma unroll
+        for (int s = 0; s < KS; ++s)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) dot += bf2f(qf[s][j]) * bf2f(kf[s][j]);
+        dot += __shfl_xor(dot, 16, 64);
+        dot += __shfl_xor(dot, 32, 64);
+        m = dot * scale_log2e;
+        lsum = g == 0 ? 1.f : 0.f;
+        const int64_t slot = rope.slots[A.b];
+        const bool writer = col == 0 && slot >= 0;  // lanes 0 / 16 / 32 / 48
+        const int64_t cblk = slot / kBS, off = slot - cblk * kBS;
+        if (writer) {
+          bf16_t* kd = rope.k_cache + ((cblk * Hkv + A.h) * kBS + off) * D + 8 * g;
+#pragma unroll
+          for (int s = 0; s < KS; ++s) store_bf16x8(kd + 32 * s, kf[s]);
+        }
+#pragma unroll
+        for (int i = 0; i < NT; ++i) {
+          const bf16x4 v = load_bf16x4(vn + 16 * i + 4 * g);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o[i][r] = bf2f(v[r]);  // p = 1 (exact in bf16) times v
+        }
+        if (slot >= 0) {  // V block [8 groups of 4 tokens][D][4]: one dim per lane per store
+          bf16_t* vd = rope.v_cache + (cblk * Hkv + A.h) * blk_elems + (off >> 2) * (4 * D) +
+                       (off & 3);
+#pragma unroll
+          for (int d = lane; d < D; d += 64) vd[d * 4] = vn[d];
+        }
+      }
+    }
     const Item Bn = next_item(A.it + W);
     const bool have_next = Bn.it < n_items;
     int bt_n = 0;
@@ -537,10 +635,6 @@ __global__ __launch_bounds__(256, D >= 256 ? 1 : 2) void paged_decode_persist_ke
       load_q(qn, Bn);
       bt_n = load_bt(Bn, Bn.begin);
     }
-    f32x4 o[NT];
-#pragma unroll
-    for (int i = 0; i < NT; ++i) o[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    float m = kNegBig, lsum = 0.f;
     for (int blk = A.begin; blk < A.end; ++blk) {
       const bool more = blk + 1 < A.end;
       if (more) {
@@ -559,11 +653,12 @@ __global__ __launch_bounds__(256, D >= 256 ? 1 : 2) void paged_decode_persist_ke
         s1 = mfma16(cur.k1[s], qf[s], s1);
       }
       const int tok0 = blk * kBS + 4 * g;
+      const int nc = cached(A);
       float bmax = kNegBig;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        s0[r] = (tok0 + r < A.ctx) ? s0[r] * scale_log2e : kNegBig;
-        s1[r] = (tok0 + 16 + r < A.ctx) ? s1[r] * scale_log2e : kNegBig;
+        s0[r] = (tok0 + r < nc) ? s0[r] * scale_log2e : kNegBig;
+        s1[r] = (tok0 + 16 + r < nc) ? s1[r] * scale_log2e : kNegBig;
         bmax = fmaxf(bmax, fmaxf(s0[r], s1[r]));
       }
       bmax = fmaxf(bmax, __shfl_xor(bmax, 16, 64));
@@ -575,8 +670,12 @@ __global__ __launch_bounds__(256, D >= 256 ? 1 : 2) void paged_decode_persist_ke
       float psum = 0.f;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float p0 = fast_exp2(s0[r] - m_new);
-        const float p1 = fast_exp2(s1[r] - m_new);
+        float p0 = fast_exp2(s0[r] - m_new);
+        float p1 = fast_exp2(s1[r] - m_new);
+        if constexpr (ROPE) {  // a block may hold no cached token at all (m_new = kNegBig)
+          p0 = (tok0 + r < nc) ? p0 : 0.f;
+          p1 = (tok0 + 16 + r < nc) ? p1 : 0.f;
+        }
         psum += p0 + p1;
         pf[r] = f2bf(p0);
         pf[4 + r] = f2bf(p1);
@@ -625,6 +724,7 @@ __global__ __launch_bounds__(256, D >= 256 ? 1 : 2) void paged_decode_persist_ke
     A = Bn;
 #pragma unroll
     for (int s = 0; s < KS; ++s) qf[s] = qn[s];
+    rope_q(qf, A);
     chunk = A.begin;
     bt_reg = bt_n;
   }
@@ -679,15 +779,16 @@ int launch_paged_decode(void* out, float* part_o, float* part_ml, int* counters,
     const int items = B * Hkv * max_parts;
     const int per_cu = D >= 256 ? 1 : 2;
     const dim3 pgrid(std::max(1, std::min((items + 3) / 4, per_cu * n_cu))), pblock(256);
+    const DecodeRope nr{};
     switch (D) {
       case 64:
-        hipLaunchKernelGGL(paged_decode_persist_kernel<64>, pgrid, pblock, 0, st, (bf16_t*)out, part_o, part_ml, (const bf16_t*)q, q_stride, (const bf16_t*)k_cache, (const bf16_t*)v_cache, block_tables, bt_stride, context_lens, B, Hq, Hkv, sl2, max_parts, blocks_per_part);
+        hipLaunchKernelGGL((paged_decode_persist_kernel<64, false>), pgrid, pblock, 0, st, (bf16_t*)out, part_o, part_ml, (const bf16_t*)q, q_stride, (const bf16_t*)k_cache, (const bf16_t*)v_cache, block_tables, bt_stride, context_lens, B, Hq, Hkv, sl2, max_parts, blocks_per_part, nr);
         break;
       case 128:
-        hipLaunchKernelGGL(paged_decode_persist_kernel<128>, pgrid, pblock, 0, st, (bf16_t*)out, part_o, part_ml, (const bf16_t*)q, q_stride, (const bf16_t*)k_cache, (const bf16_t*)v_cache, block_tables, bt_stride, context_lens, B, Hq, Hkv, sl2, max_parts, blocks_per_part);
+        hipLaunchKernelGGL((paged_decode_persist_kernel<128, false>), pgrid, pblock, 0, st, (bf16_t*)out, part_o, part_ml, (const bf16_t*)q, q_stride, (const bf16_t*)k_cache, (const bf16_t*)v_cache, block_tables, bt_stride, context_lens, B, Hq, Hkv, sl2, max_parts, blocks_per_part, nr);
         break;
       case 256:
-        hipLaunchKernelGGL(paged_decode_persist_kernel<256>, pgrid, pblock, 0, st, (bf16_t*)out, part_o, part_ml, (const bf16_t*)q, q_stride, (const bf16_t*)k_cache, (const bf16_t*)v_cache, block_tables, bt_stride, context_lens, B, Hq, Hkv, sl2, max_parts, blocks_per_part);
+        hipLaunchKernelGGL((paged_decode_persist_kernel<256, false>), pgrid, pblock, 0, st, (bf16_t*)out, part_o, part_ml, (const bf16_t*)q, q_stride, (const bf16_t*)k_cache, (const bf16_t*)v_cache, block_tables, bt_stride, context_lens, B, Hq, Hkv, sl2, max_parts, blocks_per_part, nr);
         break;
       default:
         return -1;
@@ -736,6 +837,48 @@ int launch_paged_decode(void* out, float* part_o, float* part_ml, int* counters,
       return -1;
   }
   if (max_parts > 1 && counters == nullptr)
+    hipLaunchKernelGGL(decode_reduce_kernel, dim3(B * Hq), dim3(256), 0, st,
+                       (bf16_t*)out, (const float*)part_o, (const float*)part_ml,
+                       context_lens, Hq, D, max_parts, blocks_per_part);
+  return (int)hipGetLastError();
+}
+
+// Persistent decode attention with the step's RoPE + KV write fused (DecodeRope above).
+// q = row 0 of the QKV GEMM output [B][q_stride] (q | k | v heads, unrotated); D <= 128
+// (the persistent form at D = 256 spills; the caller runs rope_kv + the plain form there).
+int launch_paged_decode_rope(void* out, float* part_o, float* part_ml, const void* q,
+                             int q_stride, void* k_cache, void* v_cache,
+                             const int* block_tables, int bt_stride, const int* context_lens,
+                             int B, int Hq, int Hkv, int D, float scale, int max_parts,
+                             int blocks_per_part, const int* positions, const int64_t* slots,
+                             const float* cos_sin, hipStream_t st) {
+  if (B == 0) return 0;
+  if (Hkv <= 0 || Hq % Hkv != 0 || Hq / Hkv > 16 || D > 128) return -1;
+  if (!positions || !slots || !cos_sin || q_stride < (Hq + 2 * Hkv) * D) return -1;
+  if (max_parts > 1 && (!part_o || !part_ml)) return -2;
+  static int n_cu = 0;
+  if (n_cu == 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        n_cu <= 0)
+      n_cu = 256;
+  }
+  const float sl2 = scale * kLog2e;
+  const int items = B * Hkv * max_parts;
+  const dim3 pgrid(std::max(1, std::min((items + 3) / 4, 2 * n_cu))), pblock(256);
+  const DecodeRope r{positions, slots, cos_sin, (bf16_t*)k_cache, (bf16_t*)v_cache};
+  switch (D) {
+    case 64:
+      hipLaunchKernelGGL((paged_decode_persist_kernel<64, true>), pgrid, pblock, 0, st, (bf16_t*)out, part_o, part_ml, (const bf16_t*)q, q_stride, (const bf16_t*)k_cache, (const bf16_t*)v_cache, block_tables, bt_stride, context_lens, B, Hq, Hkv, sl2, max_parts, blocks_per_part, r);
+      break;
+    case 128:
+      hipLaunchKernelGGL((paged_decode_persist_kernel<128, true>), pgrid, pblock, 0, st, (bf16_t*)out, part_o, part_ml, (const bf16_t*)q, q_stride, (const bf16_t*)k_cache, (const bf16_t*)v_cache, block_tables, bt_stride, context_lens, B, Hq, Hkv, sl2, max_parts, blocks_per_part, r);
+      break;
+    default:
+      return -1;
+  }
+  if (max_parts > 1)
     hipLaunchKernelGGL(decode_reduce_kernel, dim3(B * Hq), dim3(256), 0, st,
                        (bf16_t*)out, (const float*)part_o, (const float*)part_ml,
                        context_lens, Hq, D, max_parts, blocks_per_part);

@@ -1,4 +1,4 @@
-// Medium-M projection GEMM for decode batches 17..128: y[M, N] = x[M, K] @ W[N, K]^T,
+// Medium-M projection GEMM for decode batches 17..256: y[M, N] = x[M, K] @ W[N, K]^T,
 // bf16 in/out, fp32 accumulation, 16x16x32 bf16 MFMA.
 //
 // Regime: at these M the weights are read once per call and every weight byte is used
@@ -39,8 +39,14 @@ constexpr int mid_depth() { return 4; }  // 8 measured slower (VGPRs, fewer vali
 
 enum { MID_STORE = 0, MID_RESIDUAL = 1, MID_SLAB = 2 };
 
+// Occupancy: 2 workgroups per CU up to 8 column groups (M <= 128); beyond that (the
+// 129-256-row buckets of the 70B decode) the 2 x MG accumulators need the AGPR half of the
+// register file and the x double buffer is up to 74 KiB of LDS, so one workgroup per CU.
+template <int MG>
+constexpr int mid_wgs_per_cu() { return MG > 8 ? 1 : 2; }
+
 template <int MG, int OUT>
-__global__ __launch_bounds__(kMidThreads, 2) void midm_kernel(
+__global__ __launch_bounds__(kMidThreads, mid_wgs_per_cu<MG>()) void midm_kernel(
     bf16_t* __restrict__ y, float* __restrict__ slab, const bf16_t* __restrict__ x,
     const bf16_t* __restrict__ w, const bf16_t* __restrict__ res, int M, int N, int K,
     int ldx, int ldy, int ldr, int n_blocks, int kps) {
@@ -227,7 +233,7 @@ int launch_midm_gemm(void* y, const void* x, const void* w, const void* res, int
                      int K, int ldx, int ldy, int ldr, int epi, int S, void* slab,
                      int64_t slab_bytes, hipStream_t st) {
   // K per split: whole register rings (4 chunks of 64)
-  if (M < 1 || M > 128 || N % kMidRows || S < 1 || K % (4 * kMidKC * S) || ldx % 8 ||
+  if (M < 1 || M > 256 || N % kMidRows || S < 1 || K % (4 * kMidKC * S) || ldx % 8 ||
       ldy % 4 ||
       epi < 0 || epi > 3 || (epi == 1 && (res == nullptr || ldr % 4)) ||
       (epi >= 2 && (N / 2) % 4))
@@ -247,6 +253,10 @@ int launch_midm_gemm(void* y, const void* x, const void* w, const void* res, int
     case 4: launch_mg<4>(yy, sl, xx, ww, rr, M, N, K, ldx, ldy, ldr, S, out, st); break;
     case 6: launch_mg<6>(yy, sl, xx, ww, rr, M, N, K, ldx, ldy, ldr, S, out, st); break;
     case 8: launch_mg<8>(yy, sl, xx, ww, rr, M, N, K, ldx, ldy, ldr, S, out, st); break;
+    case 10: launch_mg<10>(yy, sl, xx, ww, rr, M, N, K, ldx, ldy, ldr, S, out, st); break;
+    case 12: launch_mg<12>(yy, sl, xx, ww, rr, M, N, K, ldx, ldy, ldr, S, out, st); break;
+    case 14: launch_mg<14>(yy, sl, xx, ww, rr, M, N, K, ldx, ldy, ldr, S, out, st); break;
+    case 16: launch_mg<16>(yy, sl, xx, ww, rr, M, N, K, ldx, ldy, ldr, S, out, st); break;
     default: return -1;
   }
   if (use_slab) {

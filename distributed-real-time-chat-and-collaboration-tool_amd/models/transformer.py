@@ -520,13 +520,12 @@ class TransformerLM:
         def attn(i, L, x):
             qkv = ops.norm_linear(x, L["qkv"])
             kc, vc = kv_caches[i]
-            ops.rope_kv_(qkv, meta.positions, meta.slots, self.cos_sin, sh.hq, sh.hkv, D,
-                         kc, vc, ops.KV_BLOCK)
-            q = qkv.as_strided((B, sh.hq, D), (qkv.stride(0), D, 1))
-            a = ops.paged_decode_attention(q, kc, vc, meta.block_tables, meta.context_lens,
-                                           cfg.attn_scale, out=attn_out,
-                                           blocks_per_part=meta.blocks_per_part,
-                                           workspace=meta.workspace)
+            # RoPE + the step's KV write inside the attention launch (persistent kernel)
+            a = ops.paged_decode_attention_rope(qkv, meta.positions, meta.slots, self.cos_sin,
+                                                sh.hq, sh.hkv, D, kc, vc, meta.block_tables,
+                                                meta.context_lens, cfg.attn_scale, out=attn_out,
+                                                blocks_per_part=meta.blocks_per_part,
+                                                workspace=meta.workspace)
             o = ops.linear(a.view(B, sh.hq * D), L["o"])
             if self.pc.tp_size > 1:
                 return o, False, True  # reduced by the next norm (fused all-reduce + add + norm)

@@ -11,7 +11,7 @@ them is fused here.
 from ._ext import on_gpu, reference_mode
 from .activation import act_glu, act_glu_ref
 from .attention import (KV_BLOCK, DecodeWorkspace, decode_partitioning, paged_decode_attention,
-                        set_prefill_persist,
+                        paged_decode_attention_rope, set_prefill_persist,
                         paged_decode_ref, prefill_attention, prefill_attention_ref, prefill_tiles)
 from .gemm import (glu_linear, linear, linear_residual, mfma_gemm, norm_glu, norm_linear,
                    residual_fusable, w4_glu_ok)
@@ -23,7 +23,7 @@ from .sampling import sample, sample_ref
 __all__ = [
     "on_gpu", "reference_mode", "linear", "norm_linear", "glu_linear", "norm_glu", "w4_glu_ok", "mfma_gemm", "linear_residual", "residual_fusable", "PendingNorm", "fused_moe", "fused_moe_ref",
     "act_glu", "act_glu_ref", "KV_BLOCK", "DecodeWorkspace", "decode_partitioning",
-    "paged_decode_attention", "paged_decode_ref", "prefill_attention", "prefill_attention_ref",
+    "paged_decode_attention", "paged_decode_attention_rope", "paged_decode_ref", "prefill_attention", "prefill_attention_ref",
     "prefill_tiles", "rmsnorm", "rmsnorm_ref", "build_rope_cache", "rope_kv_", "rope_kv_ref",
     "kv_write_v", "kv_write_v_ref",
     "sample", "sample_ref",

@@ -243,3 +243,58 @@ def paged_decode_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torc
                               workspace.max_parts, blocks_per_part, variant, stream_ptr(q)),
           "paged_decode")
     return out
+
+
+# RoPE + KV write fused into the persistent decode attention (attention_decode.hip
+# DecodeRope): the step's q / k / v come unrotated from the QKV GEMM output; one launch
+# per layer instead of rope_kv + attention.  DRTC_DECODE_FUSED_ROPE=0 keeps the two launches.
+FUSED_ROPE = os.environ.get("DRTC_DECODE_FUSED_ROPE", "1") != "0"
+
+
+def paged_decode_attention_rope(qkv: torch.Tensor, positions: torch.Tensor, slots: torch.Tensor,
+                                cos_sin: torch.Tensor, Hq: int, Hkv: int, D: int,
+                                k_cache: torch.Tensor, v_cache: torch.Tensor,
+                                block_tables: torch.Tensor, context_lens: torch.Tensor,
+                                scale: float, out: torch.Tensor | None = None,
+                                blocks_per_part: int | None = None,
+                                workspace: DecodeWorkspace | None = None) -> torch.Tensor:
+    """Decode-step attention from the raw QKV rows [B, (Hq + 2 Hkv) D]: rotate q / k of
+    the step's token (position ``positions[b]`` = context_lens[b] - 1), write its k / v
+    into the paged cache at ``slots[b]`` and attend over the whole context - the result
+    of ``rope_kv_`` followed by ``paged_decode_attention``.  On the GPU the persistent
+    kernel (variant 3, D <= 128) does it in one launch; other shapes run the two ops."""
+    from .rope import rope_kv_
+
+    B = qkv.shape[0]
+    q = qkv.as_strided((B, Hq, D), (qkv.stride(0), D, 1))
+    variant = decode_variant(B, Hkv, D, block_tables.shape[1]) if on_gpu(qkv) else 0
+    if not (on_gpu(qkv) and FUSED_ROPE and variant == 3 and D <= 128):
+        rope_kv_(qkv, positions, slots, cos_sin, Hq, Hkv, D, k_cache, v_cache, KV_BLOCK)
+        return paged_decode_attention(q, k_cache, v_cache, block_tables, context_lens, scale,
+                                      out=out, blocks_per_part=blocks_per_part,
+                                      workspace=workspace)
+    assert qkv.dtype == torch.bfloat16 and qkv.stride(1) == 1
+    assert qkv.shape[1] >= (Hq + 2 * Hkv) * D
+    nb, hkv, bs, D2 = k_cache.shape
+    assert hkv == Hkv and bs == KV_BLOCK and D2 == D and k_cache.is_contiguous()
+    assert v_cache.is_contiguous() and v_cache.shape == (nb, Hkv, D, bs)
+    assert positions.dtype == torch.int32 and positions.numel() >= B
+    assert slots.dtype == torch.int64 and slots.numel() >= B
+    assert cos_sin.dtype == torch.float32 and cos_sin.shape[1] == D and cos_sin.is_contiguous()
+    assert block_tables.dtype == torch.int32 and block_tables.stride(1) == 1
+    assert context_lens.dtype == torch.int32 and context_lens.numel() >= B
+    if blocks_per_part is None or workspace is None:
+        blocks_per_part, max_parts = decode_partitioning(B, Hkv, block_tables.shape[1],
+                                                         variant=variant, D=D)
+        workspace = DecodeWorkspace(B, Hq, D, max_parts, qkv.device)
+    if out is None:
+        out = torch.empty((B, Hq, D), dtype=qkv.dtype, device=qkv.device)
+    assert out.is_contiguous() and out.shape == (B, Hq, D)
+    check(hipk().paged_decode_rope(out.data_ptr(), ptr(workspace.part_o), ptr(workspace.part_ml),
+                                   qkv.data_ptr(), qkv.stride(0), k_cache.data_ptr(),
+                                   v_cache.data_ptr(), block_tables.data_ptr(),
+                                   block_tables.stride(0), context_lens.data_ptr(), B, Hq, Hkv, D,
+                                   float(scale), workspace.max_parts, blocks_per_part,
+                                   positions.data_ptr(), slots.data_ptr(), cos_sin.data_ptr(),
+                                   stream_ptr(qkv)), "paged_decode_rope")
+    return out

@@ -533,13 +533,15 @@ __all__ = ["linear", "norm_linear", "glu_linear", "norm_glu", "w4_glu_ok", "skin
 
 # ------------------------------------------------------------------ medium-M decode GEMM
 MIDM_EPI = {"store": 0, "residual": 1, "silu": 2, "gelu_tanh": 3}
-MIDM_MAX_M = 128
+MIDM_MAX_M = 256
 
 
-def midm_splits(M: int, N: int, K: int, target_wgs: int = 512) -> int:
+def midm_splits(M: int, N: int, K: int, target_wgs: int | None = None) -> int:
     """K splits of the medium-M GEMM: the largest S <= 16 with K a multiple of
     256 S (whole 4-chunk register rings per split) and at most ~2 workgroups
-    per CU."""
+    per CU (one above 128 rows, where the kernel runs one workgroup per CU)."""
+    if target_wgs is None:
+        target_wgs = 256 if M > 128 else 512
     nb = N // 128
     ring = 64 * midm_depth(M)
     best = 1
@@ -563,7 +565,7 @@ def midm_supported(M: int, N: int, K: int, epi: str = "store") -> bool:
 def midm_gemm(x: torch.Tensor, w: torch.Tensor, epi: str = "store",
               residual: torch.Tensor | None = None, out: torch.Tensor | None = None,
               splits: int | None = None) -> torch.Tensor:
-    """Medium-M (17..128 rows) decode GEMM, csrc/kernels/gemm_midm.hip:
+    """Medium-M (17..256 rows) decode GEMM, csrc/kernels/gemm_midm.hip:
     y = x @ w^T with a store / residual (y = residual + x w^T, in place when
     out is residual) / SiLU- or GELU-gated [gate | up] epilogue.  W streams
     once from HBM into registers, x is shared through LDS, K is split over

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Measure the medium-M decode GEMM (csrc/kernels/gemm_midm.hip) against the
 engine's current path (ops.linear: tuned hipBLASLt / F.linear) for every decode
-projection of a model at the decode buckets 17..128, and write a tuning entry
+projection of a model at the decode buckets 17..256, and write a tuning entry
 {"midm": S} (K splits) where the hand kernel wins by at least --min-gain.
 
 W is rotated over copies (>= 512 MB in all) so it streams from HBM, as in a
@@ -24,7 +24,7 @@ import torch  # noqa: E402
 
 from tune_gemms import projection_shapes  # noqa: E402
 
-BUCKETS = (24, 32, 48, 64, 96, 128)
+BUCKETS = (24, 32, 48, 64, 96, 128, 160, 192, 224, 256)
 
 
 def time_arm(fn, ws, rounds=5, iters=24):

@@ -95,7 +95,7 @@ def _rel(out, ref):
     return (out.float() - ref).abs().max().item() / max(ref.abs().max().item(), 1e-6)
 
 
-@pytest.mark.parametrize("M", [17, 24, 33, 64, 100, 128])
+@pytest.mark.parametrize("M", [17, 24, 33, 64, 100, 128, 150, 192, 256])
 @pytest.mark.parametrize("N,K,S", [(4096, 4096, 8), (6144, 4096, 4), (2560, 2048, 8),
                                    (4096, 14336, 7), (4096, 14336, 14), (1024, 1024, 1)])
 def test_midm_store_and_residual(hipk, M, N, K, S):
@@ -114,7 +114,7 @@ def test_midm_store_and_residual(hipk, M, N, K, S):
 
 
 @pytest.mark.parametrize("act", ["silu", "gelu_tanh"])
-@pytest.mark.parametrize("M", [24, 64, 128])
+@pytest.mark.parametrize("M", [24, 64, 128, 200, 256])
 def test_midm_glu_epilogue(hipk, act, M):
     I, K = 2048, 2048
     g = torch.Generator(device="cuda").manual_seed(M)

@@ -213,6 +213,55 @@ def test_paged_decode_persistent_many_items(hipk):
         assert torch.equal(out, v3)
 
 
+@pytest.mark.parametrize("D,Hq,Hkv", [(128, 32, 8), (64, 4, 2), (128, 64, 8)])
+@pytest.mark.parametrize("ctx_lens", [[1, 2, 31, 32, 33, 64, 65, 100, 257], [0, 40, 0, 77],
+                                      [1000, 2049, 513]])
+@pytest.mark.parametrize("bpp", [None, 4])
+def test_paged_decode_fused_rope(hipk, monkeypatch, D, Hq, Hkv, ctx_lens, bpp):
+    """RoPE + KV write fused into the persistent decode kernel (DecodeRope) equals
+    rope_kv_ followed by the plain decode attention: same output, same K/V cache rows
+    for the step's token (position ctx - 1, including the first row of a new block and
+    a context of 1), padded slots untouched, one or several partitions."""
+    from drtc_amd.ops import attention as attn_ops
+
+    monkeypatch.setattr(attn_ops, "DECODE_VARIANT", 3)
+    B = len(ctx_lens)
+    _, kc, vc, bt, cl = _paged_setup(B, Hq, Hkv, D, [max(c, 1) for c in ctx_lens], seed=11)
+    cl = torch.tensor(ctx_lens, dtype=torch.int32, device=DEV)
+    g = torch.Generator(device="cpu").manual_seed(12)
+    qkv = torch.randn(B, (Hq + 2 * Hkv) * D, generator=g).to(torch.bfloat16).to(DEV)
+    pos = (cl - 1).clamp(min=0)
+    bt_c = bt.cpu()
+    slots = torch.tensor([int(bt_c[b, p // 32]) * 32 + p % 32 if c > 0 else -1
+                          for b, (c, p) in enumerate(zip(ctx_lens, pos.tolist()))],
+                         dtype=torch.int64, device=DEV)
+    cs = ops.build_rope_cache(4096, D, 5e5, device=DEV)
+    if bpp is None:
+        bpp_, mp = ops.decode_partitioning(B, Hkv, bt.shape[1], variant=3, D=D)
+    else:
+        bpp_, mp = bpp, math.ceil(bt.shape[1] / bpp)
+    scale = D ** -0.5
+    # two-launch form
+    kc1, vc1, qkv1 = kc.clone(), vc.clone(), qkv.clone()
+    ops.rope_kv_(qkv1, pos.to(torch.int32), slots, cs, Hq, Hkv, D, kc1, vc1, ops.KV_BLOCK)
+    q1 = qkv1.as_strided((B, Hq, D), (qkv1.stride(0), D, 1))
+    ref = ops.paged_decode_attention(q1, kc1, vc1, bt, cl, scale, blocks_per_part=bpp_,
+                                     workspace=ops.DecodeWorkspace(B, Hq, D, mp, DEV))
+    # fused
+    kc2, vc2, qkv2 = kc.clone(), vc.clone(), qkv.clone()
+    out = ops.paged_decode_attention_rope(qkv2, pos.to(torch.int32), slots, cs, Hq, Hkv, D, kc2,
+                                          vc2, bt, cl, scale, blocks_per_part=bpp_,
+                                          workspace=ops.DecodeWorkspace(B, Hq, D, mp, DEV))
+    torch.cuda.synchronize()
+    _close(out, ref, 2e-2, 2e-2, "fused rope attention")
+    _close(kc2, kc1, 1e-2, 1e-2, "k cache")
+    assert torch.equal(vc2, vc1)
+    assert torch.equal(qkv2, qkv)  # the QKV rows are read, never rotated in place
+    for b, c in enumerate(ctx_lens):
+        if c == 0:
+            assert out[b].abs().max().item() == 0.0
+
+
 @pytest.mark.parametrize("variant", [1, 2, 3])
 def test_paged_decode_strided_q_and_padding(hipk, variant):
     Hq, Hkv, D = 32, 8, 128
