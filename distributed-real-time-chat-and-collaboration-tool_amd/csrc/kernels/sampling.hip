@@ -13,8 +13,8 @@
 //    back to a 16-bit radix select (two histogram passes) and a ballot-
 //    compacted full gather.
 //    Candidates are bitonic-sorted; all tokens tied with the k-th value stay.
-//    Rows that fit in registers (<= 131072 tokens) take sample_topk_reg: one
-//    load pass, register gather, rank-count sort, one-scan softmax.
+//    Up to 256 candidates (the common case) are ordered by rank counting (one
+//    barrier) and the softmax prefix sum is one block scan (two barriers).
 //  * top_k == 0       : temperature sampling with EXACT top-p over the whole
 //    vocabulary (no candidate cap).  With p_i ~ exp(x_i / T) and
 //    P = top_p * sum(p), token i is in the nucleus iff the mass of tokens
@@ -41,6 +41,7 @@ constexpr int kSampThreads = 1024;
 constexpr int kSampWaves = kSampThreads / 64;
 constexpr int kCand = 1024;
 constexpr int kMaxRounds = 40;
+constexpr int kRankMax = 256;  // candidates ordered by rank counting up to this many
 
 DRTC_DEVICE unsigned ord16(unsigned short b) {
   return (b & 0x8000u) ? (unsigned)(~b & 0xFFFFu) : (unsigned)(b | 0x8000u);
@@ -326,154 +327,9 @@ DRTC_DEVICE void sample_topk(SampShared& s, int* out_tokens, const unsigned shor
     const unsigned thr = radix_kth(s, lr, V, vec, k);
     n = min(gather_ge(s, lr, V, vec, thr), kCand);
   }
-  int np2 = 1;
-  while (np2 < n) np2 <<= 1;
-  // ---- bitonic sort, descending (ties -> lower index first)
-  for (int size = 2; size <= np2; size <<= 1) {
-    for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      const int j = tid ^ stride;
-      if (tid < np2 && j > tid) {
-        const bool desc = ((tid & size) == 0);
-        const float a = s.val[tid], b = s.val[j];
-        const int ia = s.idx[tid], ib = s.idx[j];
-        const bool a_first = (a > b) || (a == b && ia < ib);
-        if (desc != a_first) {
-          s.val[tid] = b; s.val[j] = a;
-          s.idx[tid] = ib; s.idx[j] = ia;
-        }
-      }
-      __syncthreads();
-    }
-  }
-  // keep exactly the elements >= the k-th value (ties with it included)
-  const float kth = s.val[min(k, n) - 1];
-  {
-    const bool edge = tid < n && s.val[tid] >= kth && (tid + 1 == n || s.val[tid + 1] < kth);
-    if (edge) s.misc[3] = tid + 1;
-  }
-  __syncthreads();
-  n = s.misc[3];
-  np2 = 1;
-  while (np2 < n) np2 <<= 1;
-  // ---- softmax + top-p + draw over the n candidates
-  const float top = s.val[0];
-  const float inv_t = 1.f / temp;
-  const float pv = (tid < n) ? __expf((s.val[tid] - top) * inv_t) : 0.f;
-  __syncthreads();
-  s.val[tid] = pv;
-  __syncthreads();
-  for (int off = 1; off < np2; off <<= 1) {  // inclusive Hillis-Steele scan
-    const float add = (tid >= off && tid < np2) ? s.val[tid - off] : 0.f;
-    __syncthreads();
-    s.val[tid] += add;
-    __syncthreads();
-  }
-  const float total = s.val[n - 1];
-  if (tid == 0) s.misc[3] = n - 1;
-  __syncthreads();
-  {
-    const float need = pp * total;
-    const bool hit = tid < n && s.val[tid] >= need && (tid == 0 || s.val[tid - 1] < need);
-    if (hit) s.misc[3] = tid;
-  }
-  __syncthreads();
-  const int cut = s.misc[3];
-  const float target = uniform(seed, st, row, 0) * s.val[cut];
-  if (tid <= cut) {
-    const float lo = (tid == 0) ? 0.f : s.val[tid - 1];
-    if (target >= lo && (target < s.val[tid] || tid == cut)) out_tokens[row] = s.idx[tid];
-  }
-}
-
-// Register-resident top-k (rows of up to kRegVec x 8 x 1024 = 131072 tokens, 16-B aligned: the
-// Llama-3 / Mixtral vocabularies).  The same selection as sample_topk with the row read ONCE:
-//   * every 16-B load of the thread's share is issued before the first is used (16 in flight
-//     per lane - the pass runs at the load rate, not at one round trip per 4 vectors) and the
-//     values stay in VGPRs (64 per lane), so the tau0 gather walks registers, not memory;
-//   * candidates (n <= kRankMax, the common case: ~k + a few) are ordered by rank counting
-//     over the LDS list (one barrier) instead of a bitonic network (log^2 n barriers), on the
-//     16-bit keys (a total order: NaN rows cannot collide ranks);
-//   * the softmax prefix sum is one block scan (wave shuffles + wave totals, 2 barriers)
-//     instead of a Hillis-Steele scan over LDS (2 log n barriers).
-// The result is the sample_topk contract (ties with the k-th value kept, exact top-p over the
-// candidates, the same counter-based draw).
-constexpr int kRegVec = 16;
-constexpr int kRankMax = 256;
-
-DRTC_DEVICE void sample_topk_reg(SampShared& s, int* out_tokens, const unsigned short* lr, int V,
-                                 int row, float temp, int k, float pp, uint64_t seed,
-                                 uint64_t st) {
-  const int tid = threadIdx.x;
-  const int nv = V >> 3;
-  u16x8 x[kRegVec];
-#pragma unroll
-  for (int u = 0; u < kRegVec; ++u) {
-    const int v = tid + u * kSampThreads;
-    x[u] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
-    if (v < nv) x[u] = *reinterpret_cast<const u16x8*>(lr + 8 * v);
-  }
-  const int ti = (nv << 3) + tid;  // V % 8 trailing tokens: one per thread at most
-  const unsigned short xt = ti < V ? lr[ti] : (unsigned short)0;
-  unsigned tm = 0;
-#pragma unroll
-  for (int u = 0; u < kRegVec; ++u) {
-    if (tid + u * kSampThreads < nv) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) tm = max(tm, ord16(x[u][j]));
-    }
-  }
-  if (ti < V) tm = max(tm, ord16(xt));
-  // ---- tau0 = k-th largest thread maximum (radix select over LDS, as sample_topk)
-  unsigned* h = &s.hist[0][0];
-  h[tid] = tm;
-  __syncthreads();
-  unsigned prefix = 0, mask = 0;
-  int remaining = k;
-  for (int pass = 8; pass >= 0; pass -= 8) {
-    unsigned* bins = &s.hist[4][0];
-    if (tid < 256) bins[tid] = 0;
-    __syncthreads();
-    const unsigned key = h[tid];
-    if ((key & mask) == prefix) atomicAdd(&bins[(key >> pass) & 255u], 1u);
-    __syncthreads();
-    select_bin(s, bins, remaining);
-    prefix |= (unsigned)s.misc[0] << pass;
-    mask |= 255u << pass;
-    remaining = s.misc[1];
-    __syncthreads();
-  }
-  // ---- gather key >= tau0 from registers (only threads whose max reaches it)
-  if (tid == 0) s.misc[2] = 0;
-  s.val[tid] = -INFINITY;
-  s.idx[tid] = 0x7fffffff;
-  __syncthreads();
-  if (tm >= prefix) {
-#pragma unroll
-    for (int u = 0; u < kRegVec; ++u) {
-      const int v = tid + u * kSampThreads;
-      if (v < nv) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          if (ord16(x[u][j]) >= prefix) {
-            const int slot = atomicAdd(&s.misc[2], 1);
-            if (slot < kCand) { s.val[slot] = bits2f(x[u][j]); s.idx[slot] = 8 * v + j; }
-          }
-        }
-      }
-    }
-    if (ti < V && ord16(xt) >= prefix) {
-      const int slot = atomicAdd(&s.misc[2], 1);
-      if (slot < kCand) { s.val[slot] = bits2f(xt); s.idx[slot] = ti; }
-    }
-  }
-  __syncthreads();
-  int n = s.misc[2];
-  if (n > kCand) {  // heavy ties: exact k-th key by radix select from memory, gather again
-    const unsigned thr = radix_kth(s, lr, V, true, k);
-    n = min(gather_ge(s, lr, V, true, thr), kCand);
-  }
   if (n <= kRankMax) {
-    // ---- rank counting: descending key, ties -> lower index first (unique ranks)
+    // ---- rank counting over the LDS list (one barrier): descending key, ties -> lower
+    // index first; keys (not floats) so NaN rows cannot collide ranks
     float v = -INFINITY;
     int ix = 0x7fffffff, rank = 0;
     if (tid < n) {
@@ -491,6 +347,7 @@ DRTC_DEVICE void sample_topk_reg(SampShared& s, int* out_tokens, const unsigned 
   } else {
     int np2 = 1;
     while (np2 < n) np2 <<= 1;
+    // ---- bitonic sort, descending (ties -> lower index first)
     for (int size = 2; size <= np2; size <<= 1) {
       for (int stride = size >> 1; stride > 0; stride >>= 1) {
         const int j = tid ^ stride;
@@ -676,9 +533,7 @@ __global__ __launch_bounds__(kSampThreads) void sample_kernel(
   const float pp = (top_p && top_p[row] > 0.f && top_p[row] < 1.f) ? top_p[row] : 1.f;
   int k = top_k ? top_k[row] : 0;
   if (k >= V) k = 0;
-  if (k > 0 && vec && V <= kRegVec * 8 * kSampThreads) {
-    sample_topk_reg(s, out_tokens, lr, V, row, temp, min(k, kCand), pp, seed, st);
-  } else if (k > 0) {
+  if (k > 0) {
     sample_topk(s, out_tokens, lr, V, vec, row, temp, min(k, kCand), pp, seed, st);
   } else {
     sample_topp_full(s, out_tokens, lr, V, vec, row, temp, pp, seed, st);

@@ -204,6 +204,9 @@ def linear(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
         N = w.shape[0]
         key = (M, N, K, x.stride(0))
         ent = _activate().get(key)
+        if (sk := w4_dec_splitk(M, N, K)) and x.stride(0) % 8 == 0 and x.data_ptr() % 16 == 0 \
+                and w.data_ptr() % 16 == 0:
+            return mfma_gemm(x, w, "store", variant=W4_VARIANT, splitk=sk, group_m=4)
         if ent is None and (sk := w4_rs_splitk(M, N, K)) and x.stride(0) % 8 == 0 \
                 and x.data_ptr() % 16 == 0:
             return mfma_gemm(x, w, "store", variant=11, splitk=sk, group_m=4)
@@ -460,6 +463,27 @@ W4_RS_MIN_K = int(os.environ.get("DRTC_W4_RS_MIN_K", "8192"))
 W4_RS_CUS = 256  # every workgroup resident: tiles x splitk <= CUs (MI355X)
 
 
+# Full-batch decode projections on gemm_w4 with the last-arriver split-K (variant 7):
+# (N, K) -> K slices, for the decode buckets M >= W4_DEC_MIN_M, where it measured faster
+# than the tuned library with the weights streamed from HBM (scripts/gpu_r3e_probe.sh,
+# w4_probe.py --rotate).  DRTC_W4_DEC="N:K:S,..." replaces the table ("" = off).
+W4_DEC_MIN_M = int(os.environ.get("DRTC_W4_DEC_MIN_M", "768"))
+W4_DEC: dict[tuple[int, int], int] = {}
+if "DRTC_W4_DEC" in os.environ:
+    W4_DEC = {(int(a), int(b)): int(c) for a, b, c in
+              (e.split(":") for e in os.environ["DRTC_W4_DEC"].split(",") if e)}
+
+
+def w4_dec_splitk(M: int, N: int, K: int) -> int:
+    """K slices of the decode-bucket gemm_w4 form for y[M, N] = x[M, K] W^T (0: not taken)."""
+    if not (W4_DEC and _w4_plain and W4_DEC_MIN_M <= M <= DECODE_MAX_M):
+        return 0
+    sk = W4_DEC.get((N, K), 0)
+    if not sk or N % 256 or K % 64 or (K // 64) % sk:
+        return 0
+    return sk
+
+
 def w4_rs_splitk(M: int, N: int, K: int) -> int:
     """Split of the reduce-scatter decode form for y[M, N] = x[M, K] W^T, 0 = not taken."""
     if not (_w4_plain and W4_RS_MIN_M <= M <= DECODE_MAX_M and K >= W4_RS_MIN_K
@@ -527,7 +551,7 @@ def norm_glu(p, w: torch.Tensor, act: str = "silu") -> torch.Tensor:
 
 __all__ = ["linear", "norm_linear", "glu_linear", "norm_glu", "w4_glu_ok", "skinny_linear", "skinny_ok", "skinny_variant",
            "skinny_supports", "mfma_gemm", "midm_gemm", "midm_supported", "dec_gemm", "dec_supported",
-           "tune", "save_entries", "w4_ok", "w4_group_m", "w4_rs_splitk",
+           "tune", "save_entries", "w4_ok", "w4_group_m", "w4_rs_splitk", "w4_dec_splitk",
            "load_table", "reset", "set_enabled", "table_path"]
 
 

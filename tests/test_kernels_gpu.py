@@ -486,8 +486,8 @@ def test_sample_top_k_heavy_ties_fallback(hipk):
     assert torch.isin(out[32:], torch.tensor([5, 900, 31999])).all()
 
 
-def test_sample_topk_register_path_headline_shape(hipk):
-    """Register-resident top-k (rows <= 131072 tokens): the headline sampling mode
+def test_sample_topk_topp_headline_shape(hipk):
+    """Top-k at the headline sampling mode
     (top-k 64, top-p 0.95) on Llama-3-sized rows, as a strided view whose length is
     not a multiple of 8 (the per-thread tail element).  Every draw is inside the
     top-k set and inside the top-p prefix of the candidates sorted by (value desc,
@@ -504,17 +504,23 @@ def test_sample_topk_register_path_headline_shape(hipk):
     lf = logits.float()
     vals, idx = torch.sort(lf, dim=-1, descending=True, stable=True)
     kth = vals[:, K - 1:K]
+    # the kernel's candidate set: every token >= the k-th value (bf16 ties kept), ordered by
+    # (value desc, index asc); top-p keeps the prefix up to the first inclusive mass >= P
+    vals_c, idx_c = vals.cpu(), idx.cpu()
+    allowed = []
+    for b in range(B):
+        n = int((vals_c[b] >= vals_c[b, K - 1]).sum())
+        pr = torch.softmax(vals_c[b, :n].double(), 0)
+        incl = torch.cumsum(pr, 0)
+        cut = int((incl < P * (1 - 1e-5)).sum())  # first index reaching P (fp32 slack)
+        allowed.append(set(idx_c[b, :min(n, cut + 2)].tolist()))
     for i in range(4):
         step.fill_(i)
         out = ops.sample(logits, temp, k, p, seed=13, step=step).long()
         picked = lf.gather(1, out[:, None])
         assert (picked >= kth).all()
-        # exclusive softmax mass (over the top-k candidates) ahead of the pick
-        cand = vals[:, :K]
-        pr = torch.softmax(cand, -1)
-        pos = (idx[:, :K] == out[:, None]).float().argmax(-1)
-        excl = (torch.cumsum(pr, -1) - pr).gather(1, pos[:, None])[:, 0]
-        assert (excl < P + 1e-3).all(), excl.max()
+        bad = [b for b, t in enumerate(out.tolist()) if t not in allowed[b]]
+        assert not bad, bad[:5]
     R = 4096
     row = torch.full((LD,), -30.0)
     row[11], row[70000], row[V - 2] = 2.0, 1.0, 0.0  # V - 2: a tail token of the view
@@ -616,11 +622,15 @@ def test_tuned_linear(hipk, M, N, K):
 
 
 @pytest.mark.parametrize("M,N,K", [(2304, 1024, 512), (4352, 2048, 1536)])
-def test_prefill_tuned_linear_and_residual(hipk, M, N, K):
+def test_prefill_tuned_linear_and_residual(hipk, monkeypatch, M, N, K):
     """Prefill-sized tuned entries (ops.gemm._prefill): a solution tuned at a
     nearby M runs the plain GEMM (beta = 0) and the in-place residual form
-    (beta = 1, y += x @ w.T) through hipBLASLt directly; both match fp32."""
+    (beta = 1, y += x @ w.T) through hipBLASLt directly; both match fp32.
+    (The 4-wave hand GEMM, which takes these shapes by default from 4096 rows,
+    is switched off here: this is the library path's test.)"""
     from drtc_amd.ops import gemm
+
+    monkeypatch.setattr(gemm, "_w4_plain", False)
 
     torch.manual_seed(2)
     Mt = 4096  # entry tuned at another M, applied by nearest-M lookup
