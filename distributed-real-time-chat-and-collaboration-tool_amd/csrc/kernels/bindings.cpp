@@ -29,6 +29,13 @@ PYBIND11_MODULE(_hipk, m) {
                                       P<void>(w), rows, H, eps, x_stride,
                                       out_stride, res_stride, gemma, S(st));
         });
+  m.def("rmsnorm_partials", [](u64 out, u64 residual, u64 part, int sk, int rows, int H, u64 w,
+                               float eps, int out_stride, int res_stride, bool add_residual,
+                               bool gemma, u64 st) {
+    return drtc::launch_rmsnorm_partials(P<void>(out), P<void>(residual), P<const float>(part), sk,
+                                         rows, H, P<const void>(w), eps, out_stride, res_stride,
+                                         add_residual, gemma, S(st));
+  });
   m.def("act_glu", [](u64 out, u64 gu, int64_t T, int I, int gu_stride, int act,
                       u64 st) {
     return drtc::launch_act_glu(P<void>(out), P<void>(gu), T, I, gu_stride, act, S(st));

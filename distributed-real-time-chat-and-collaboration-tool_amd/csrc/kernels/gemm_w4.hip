@@ -59,7 +59,13 @@ constexpr int kW4BBlk = 1040;                  // bytes per 8-row B block
 constexpr int kW4Stage = kW4BOff + 32 * kW4BBlk;  // 66048
 constexpr int kW4Lds = 2 * kW4Stage;
 
-enum { W4_STORE = 0, W4_RESIDUAL = 1, W4_SILU = 2, W4_GELU = 3 };
+// W4_PARTIAL: split-K without a combine in this kernel - slice s writes its fp32 partial
+// tile to plane s of slab [splitk][M][N]; the consumer (rmsnorm_partials_kernel, the
+// residual add + RMSNorm that follows the o / down projection anyway) sums the planes with
+// all CUs at HBM rate.  For the full-batch decode projections (M = 1024, N = 4096: 64
+// tiles of 256 x 256), split-K 4 fills the chip and no single workgroup has to read the
+// other slices' partials (the last-arriver combine read 768 KiB alone: 155 vs 80 us).
+enum { W4_STORE = 0, W4_RESIDUAL = 1, W4_SILU = 2, W4_GELU = 3, W4_PARTIAL = 4 };
 
 struct W4Params {
   bf16_t* c;
@@ -266,7 +272,30 @@ DRTC_DEVICE void w4_st8(bf16_t* p, bf16x4 v) {
 
 template <int EPI, int V>
 DRTC_DEVICE void w4_epilogue(const W4Params& p, f32x4 (&acc)[8][8], int tm, int tn, int wm,
-                             int wn, int l16, int g) {
+                             int wn, int l16, int g, int slice) {
+  if constexpr (EPI == W4_PARTIAL) {
+    // lane: 8 consecutive fp32 columns of 4 rows per fragment i -> two 16-B stores per row
+    // (temporal: the planes are read back right after, from the L2 / MALL)
+    float* plane = p.slab + (int64_t)slice * p.M * p.N;
+    const int n = 256 * tn + 128 * wn + 8 * l16;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = 256 * tm + 128 * wm + 16 * i + 4 * g + r;
+        if (m >= p.M) continue;
+        f32x4 lo, hi;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          lo[j] = acc[i][j][r];
+          hi[j] = acc[i][j + 4][r];
+        }
+        float* dst = plane + (int64_t)m * p.N + n;
+        *reinterpret_cast<f32x4*>(dst) = lo;
+        *reinterpret_cast<f32x4*>(dst + 4) = hi;
+      }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
 #pragma unroll
@@ -606,7 +635,9 @@ __global__ __launch_bounds__(kW4Threads, 1) void gemm_w4_kernel(W4Params p) {
   }
   w4_vmcnt<0>();  // no LDS-DMA may still be landing when the workgroup leaves
 
-  if constexpr ((V & 4) != 0) {
+  if constexpr (EPI == W4_PARTIAL) {
+    // every slice stores its own plane: no combine here
+  } else if constexpr ((V & 4) != 0) {
     if (p.splitk > 1) {
       __syncthreads();
       w4_splitk_rs<EPI, V>(p, acc, tile, slice, tm, tn, wv, lane, l16, g, w4_lds);
@@ -616,7 +647,7 @@ __global__ __launch_bounds__(kW4Threads, 1) void gemm_w4_kernel(W4Params p) {
     __syncthreads();
     if (!w4_splitk(p, acc, tile, slice, w4_lds)) return;
   }
-  w4_epilogue<EPI, V>(p, acc, tm, tn, wm, wn, l16, g);
+  w4_epilogue<EPI, V>(p, acc, tm, tn, wm, wn, l16, g, slice);
 }
 
 template <int EPI, int V>
@@ -673,6 +704,25 @@ int launch_gemm_w4(void* c, const void* a, const void* b, const void* r, int M, 
   // shape contract (checked here so a bad call never reaches the device)
   const bool glu = epi == W4_SILU || epi == W4_GELU;
   if (M <= 0 || N <= 0 || K <= 0 || K % 64 || splitk < 1 || (K / 64) % splitk) return -1;
+  if (epi == W4_PARTIAL) {  // fp32 planes [splitk][M][N] in `slab`, no counters
+    if (N % 256 || lda % 8 || (uintptr_t)a % 16 || (uintptr_t)b % 16 || slab == nullptr ||
+        (uintptr_t)slab % 16 || slab_bytes < (int64_t)splitk * M * N * 4 || (v & 4))
+      return -1;
+    if ((int64_t)min(M, 256) * lda * 2 >= (1ll << 31) || (int64_t)256 * ldb * 2 >= (1ll << 31))
+      return -1;
+    W4Params p{};
+    p.a = (const bf16_t*)a;
+    p.b = (const bf16_t*)b;
+    p.slab = (float*)slab;
+    p.M = M; p.N = N; p.K = K;
+    p.lda = lda; p.ldb = ldb; p.ldc = N;
+    p.tiles_m = (M + 255) / 256;
+    p.tiles_n = N / 256;
+    p.splitk = splitk;
+    p.kt_split = K / 64 / splitk;
+    p.group_m = group_m < 1 ? 4 : group_m;
+    return w4_launch<W4_PARTIAL>(p, v, st);
+  }
   if (glu ? (N % 128 || up_off != N) : (N % 256)) return -1;
   if (lda % 8 || ldb % 8 || (glu ? ldc % 4 : ldc % 8)) return -1;
   if (epi == W4_RESIDUAL && (ldr % 8 || r == nullptr || (uintptr_t)r % 16)) return -1;
@@ -714,7 +764,8 @@ int launch_gemm_w4(void* c, const void* a, const void* b, const void* r, int M, 
 }
 
 int configure_gemm_w4() {
-  return w4_cfg<W4_STORE>() | w4_cfg<W4_RESIDUAL>() | w4_cfg<W4_SILU>() | w4_cfg<W4_GELU>();
+  return w4_cfg<W4_STORE>() | w4_cfg<W4_RESIDUAL>() | w4_cfg<W4_SILU>() | w4_cfg<W4_GELU>() |
+         w4_cfg<W4_PARTIAL>();
 }
 
 }  // namespace drtc

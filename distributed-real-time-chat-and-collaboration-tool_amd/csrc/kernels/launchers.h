@@ -11,6 +11,9 @@
 
 namespace drtc {
 
+int launch_rmsnorm_partials(void* out, void* residual, const float* part, int sk, int rows,
+                            int H, const void* w, float eps, int out_stride, int res_stride,
+                            bool add_residual, bool gemma, hipStream_t st);
 int launch_rmsnorm(void* out, void* residual, const void* x, const void* w,
                    int rows, int H, float eps, int x_stride, int out_stride,
                    int res_stride, bool gemma, hipStream_t st);

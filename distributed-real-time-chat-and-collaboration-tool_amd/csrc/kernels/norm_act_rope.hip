@@ -117,6 +117,105 @@ int launch_rmsnorm(void* out, void* residual, const void* x, const void* w,
   return (int)hipGetLastError();
 }
 
+// RMSNorm over the sum of a split-K GEMM's fp32 partial planes (gemm_w4 W4_PARTIAL):
+//   h = bf16(sum_s part[s] [+ residual]) written into `residual` (or h_out), out = norm(h) * w.
+// The planes are summed in fixed order (deterministic); one rounding of the projection
+// output (accumulator + residual), like the residual-epilogue GEMM forms.
+template <int VPT, bool GEMMA, bool RESID>
+__global__ __launch_bounds__(256) void rmsnorm_partials_kernel(
+    bf16_t* __restrict__ out, bf16_t* __restrict__ residual, const float* __restrict__ part,
+    int sk, int64_t plane, const bf16_t* __restrict__ w, int H, float eps, int out_stride,
+    int res_stride) {
+  const int row = blockIdx.x;
+  const int tid = threadIdx.x;
+  const float* pr = part + (int64_t)row * H;
+  float v[VPT][8];
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int idx = (tid + i * 256) * 8;
+    if (idx < H) {
+      f32x4 a = *reinterpret_cast<const f32x4*>(pr + idx);
+      f32x4 b = *reinterpret_cast<const f32x4*>(pr + idx + 4);
+      for (int s = 1; s < sk; ++s) {
+        a += *reinterpret_cast<const f32x4*>(pr + s * plane + idx);
+        b += *reinterpret_cast<const f32x4*>(pr + s * plane + idx + 4);
+      }
+      bf16_t* rr = residual + (int64_t)row * res_stride + idx;
+      bf16x8 r;
+      if constexpr (RESID) r = load_bf16x8(rr);
+      bf16x8 h;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float x = j < 4 ? a[j] : b[j - 4];
+        if constexpr (RESID) x += bf2f(r[j]);
+        h[j] = f2bf(x);
+        v[i][j] = bf2f(h[j]);
+        ss += v[i][j] * v[i][j];
+      }
+      store_bf16x8(rr, h);
+    }
+  }
+  __shared__ float red[4];
+  ss = wave_sum(ss);
+  if ((tid & 63) == 0) red[tid >> 6] = ss;
+  __syncthreads();
+  const float tot = red[0] + red[1] + red[2] + red[3];
+  const float rstd = rsqrtf(tot / (float)H + eps);
+  bf16_t* orow = out + (int64_t)row * out_stride;
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int idx = (tid + i * 256) * 8;
+    if (idx < H) {
+      bf16x8 wv = load_bf16x8(w + idx);
+      bf16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float ww = bf2f(wv[j]);
+        if constexpr (GEMMA) ww += 1.f;
+        o[j] = f2bf(v[i][j] * rstd * ww);
+      }
+      store_bf16x8(orow + idx, o);
+    }
+  }
+}
+
+// residual: the residual stream (updated in place to h) when add_residual, else the h output.
+int launch_rmsnorm_partials(void* out, void* residual, const float* part, int sk, int rows,
+                            int H, const void* w, float eps, int out_stride, int res_stride,
+                            bool add_residual, bool gemma, hipStream_t st) {
+  const int vpt = (H / 8 + 255) / 256;
+  if (H % 8 || vpt < 1 || vpt > 4 || sk < 1 || part == nullptr || residual == nullptr ||
+      (uintptr_t)part % 16)
+    return -1;
+  if (rows == 0) return 0;
+  const int64_t plane = (int64_t)rows * H;
+  dim3 grid(rows), block(256);
+  auto o = (bf16_t*)out;
+  auto r = (bf16_t*)residual;
+  auto ww = (const bf16_t*)w;
+#define DRTC_RMSP(N, G, R)                                                                   \
+  hipLaunchKernelGGL((rmsnorm_partials_kernel<N, G, R>), grid, block, 0, st, o, r, part, sk, \
+                     plane, ww, H, eps, out_stride, res_stride)
+#define DRTC_RMSP_GR(N)                                \
+  if (gemma) {                                         \
+    if (add_residual) DRTC_RMSP(N, true, true);        \
+    else DRTC_RMSP(N, true, false);                    \
+  } else {                                             \
+    if (add_residual) DRTC_RMSP(N, false, true);       \
+    else DRTC_RMSP(N, false, false);                   \
+  }
+  switch (vpt) {
+    case 1: DRTC_RMSP_GR(1); break;
+    case 2: DRTC_RMSP_GR(2); break;
+    case 3: DRTC_RMSP_GR(3); break;
+    default: DRTC_RMSP_GR(4); break;
+  }
+#undef DRTC_RMSP_GR
+#undef DRTC_RMSP
+  return (int)hipGetLastError();
+}
+
 // ------------------------------------------------------- gated activations
 template <int ACT>  // 0 = SiLU, 1 = tanh-GELU
 __global__ __launch_bounds__(256) void act_glu_kernel(

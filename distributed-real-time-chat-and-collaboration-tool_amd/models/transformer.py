@@ -250,6 +250,9 @@ class TransformerLM:
             res = self._fusable_residual(h, x)
             if res is not None:
                 return ops.linear_residual(h, L["down"], res), True
+            if decode and self.pc.tp_size == 1:
+                # full-batch decode: split-K partial planes summed by the next norm
+                return ops.linear_partials(h, L["down"]), False
             y = ops.linear(h, L["down"])
         else:
             gu = ops.norm_linear(x, L["gate_up"])
@@ -526,10 +529,11 @@ class TransformerLM:
                                                 meta.context_lens, cfg.attn_scale, out=attn_out,
                                                 blocks_per_part=meta.blocks_per_part,
                                                 workspace=meta.workspace)
-            o = ops.linear(a.view(B, sh.hq * D), L["o"])
             if self.pc.tp_size > 1:
+                o = ops.linear(a.view(B, sh.hq * D), L["o"])
                 return o, False, True  # reduced by the next norm (fused all-reduce + add + norm)
-            return o, False
+            # TP = 1: split-K partial planes where configured (summed by the next norm)
+            return ops.linear_partials(a.view(B, sh.hq * D), L["o"]), False
 
         self._ep_begin()
         x = self._layers(self._embed(ids), attn, decode=True)

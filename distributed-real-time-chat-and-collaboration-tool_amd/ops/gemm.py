@@ -298,7 +298,8 @@ def norm_linear(p, w: torch.Tensor) -> torch.Tensor:
     the new residual stream is written by the GEMM.  Otherwise the norm is
     materialised and ``linear`` runs."""
     x, res = p.x, p.residual
-    if (_fuse_norm and p._out is None and p.pc is None and on_gpu(x) and _enabled and x.dim() == 2
+    if (_fuse_norm and p._out is None and p.pc is None and isinstance(x, torch.Tensor)
+            and on_gpu(x) and _enabled and x.dim() == 2
             and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and x.stride(1) == 1
             and w.is_contiguous() and p.w.is_contiguous()
             and (res is None or (res.stride(1) == 1 and res.shape == x.shape))):
@@ -344,7 +345,7 @@ def glu_linear(gu: torch.Tensor, w: torch.Tensor, act: str = "silu") -> torch.Te
 
 
 # ------------------------------------------------------------ hand-written MFMA GEMM
-EPI = {"store": 0, "residual": 1, "silu": 2, "gelu_tanh": 3}
+EPI = {"store": 0, "residual": 1, "silu": 2, "gelu_tanh": 3, "partial": 4}
 _ws_lock = threading.Lock()
 _ws: dict[int, tuple[torch.Tensor, torch.Tensor]] = {}
 WS_SLAB_BYTES = 128 << 20   # fp32 split-K slabs (per device)
@@ -484,6 +485,97 @@ def w4_dec_splitk(M: int, N: int, K: int) -> int:
     return sk
 
 
+# Full-batch decode o / down projections as gemm_w4 split-K WITHOUT an in-kernel combine:
+# every K slice writes an fp32 partial plane and the residual-add + RMSNorm that follows the
+# projection anyway sums the planes (ops.norm.rmsnorm_partials) - all CUs busy in the GEMM
+# (64 tiles x 4 slices at M = 1024, N = 4096) and the reduction spread over every row's
+# workgroup at HBM rate.  (N, K) -> slices; DRTC_W4_PARTIAL="N:K:S,..." replaces the table.
+W4_PARTIAL_MIN_M = int(os.environ.get("DRTC_W4_PARTIAL_MIN_M", "768"))
+W4_PARTIAL: dict[tuple[int, int], int] = {}
+if "DRTC_W4_PARTIAL" in os.environ:
+    W4_PARTIAL = {(int(a), int(b)): int(c) for a, b, c in
+                  (e.split(":") for e in os.environ["DRTC_W4_PARTIAL"].split(",") if e)}
+PARTIALS_BYTES = 64 << 20  # fp32 planes (per device): 4 x 1024 x 4096
+
+
+class Partials:
+    """fp32 split-K partial planes [sk, M, N] standing for the bf16 output of y = x @ w.T
+    (gemm_w4 W4_PARTIAL).  Only ``ops.PendingNorm`` consumes one (materialize() sums the
+    planes inside the residual-add + RMSNorm kernel); the tensor-like attributes serve the
+    dispatch checks that look at a pending norm's input."""
+
+    __slots__ = ("planes", "sk")
+    dtype = torch.bfloat16  # the dtype of the value it stands for
+    is_cuda = True
+
+    def __init__(self, planes: torch.Tensor, sk: int):
+        self.planes, self.sk = planes, sk
+
+    @property
+    def shape(self):
+        return self.planes.shape[1:]
+
+    @property
+    def device(self):
+        return self.planes.device
+
+    def dim(self) -> int:
+        return 2
+
+    def stride(self, d: int | None = None):
+        st = (self.planes.shape[2], 1)
+        return st if d is None else st[d]
+
+    def data_ptr(self) -> int:
+        return self.planes.data_ptr()
+
+
+_pws: dict[int, torch.Tensor] = {}
+
+
+def partials_workspace(dev: torch.device) -> torch.Tensor:
+    """The device's fp32 partial-plane buffer (one producer / consumer pair at a time on the
+    engine's stream; allocated on first use, in the eager run ahead of a graph capture)."""
+    key = dev.index if dev.index is not None else torch.cuda.current_device()
+    buf = _pws.get(key)
+    if buf is None:
+        with _ws_lock:
+            buf = _pws.get(key)
+            if buf is None:
+                buf = torch.empty(PARTIALS_BYTES // 4, dtype=torch.float32, device=dev)
+                _pws[key] = buf
+    return buf
+
+
+def w4_partial_splitk(M: int, N: int, K: int) -> int:
+    if not (W4_PARTIAL and _w4_plain and W4_PARTIAL_MIN_M <= M <= DECODE_MAX_M):
+        return 0
+    sk = W4_PARTIAL.get((N, K), 0)
+    if not sk or N % 256 or K % 64 or (K // 64) % sk or sk * M * N * 4 > PARTIALS_BYTES:
+        return 0
+    return sk
+
+
+def linear_partials(x: torch.Tensor, w: torch.Tensor):
+    """y = x @ w.T for a projection whose output only feeds the next pending norm (decode
+    o / down at TP = 1): a ``Partials`` when the split-K partial-plane form is configured
+    for the shape, else ``linear``'s tensor."""
+    if (on_gpu(x) and x.dim() == 2 and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16
+            and x.stride(1) == 1 and w.is_contiguous() and x.stride(0) % 8 == 0
+            and x.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0):
+        M, K = x.shape
+        N = w.shape[0]
+        sk = w4_partial_splitk(M, N, K)
+        if sk:
+            planes = partials_workspace(x.device)[:sk * M * N].view(sk, M, N)
+            check(hipk().gemm(0, x.data_ptr(), w.data_ptr(), 0, M, N, K, x.stride(0),
+                              w.stride(0), N, 0, EPI["partial"], 0, W4_VARIANT, sk, 4,
+                              planes.data_ptr(), planes.numel() * 4, 0, 0, stream_ptr(x)),
+                  "gemm partial")
+            return Partials(planes, sk)
+    return linear(x, w)
+
+
 def w4_rs_splitk(M: int, N: int, K: int) -> int:
     """Split of the reduce-scatter decode form for y[M, N] = x[M, K] W^T, 0 = not taken."""
     if not (_w4_plain and W4_RS_MIN_M <= M <= DECODE_MAX_M and K >= W4_RS_MIN_K
@@ -552,11 +644,12 @@ def norm_glu(p, w: torch.Tensor, act: str = "silu") -> torch.Tensor:
 __all__ = ["linear", "norm_linear", "glu_linear", "norm_glu", "w4_glu_ok", "skinny_linear", "skinny_ok", "skinny_variant",
            "skinny_supports", "mfma_gemm", "midm_gemm", "midm_supported", "dec_gemm", "dec_supported",
            "tune", "save_entries", "w4_ok", "w4_group_m", "w4_rs_splitk", "w4_dec_splitk",
+           "Partials", "linear_partials", "w4_partial_splitk",
            "load_table", "reset", "set_enabled", "table_path"]
 
 
 # ------------------------------------------------------------------ medium-M decode GEMM
-MIDM_EPI = {"store": 0, "residual": 1, "silu": 2, "gelu_tanh": 3}
+MIDM_EPI = {"store": 0, "residual": 1, "silu": 2, "gelu_tanh": 3, "partial": 4}
 MIDM_MAX_M = 256
 
 
@@ -618,7 +711,7 @@ def midm_gemm(x: torch.Tensor, w: torch.Tensor, epi: str = "store",
 
 
 # ------------------------------------------------------------------ decode-batch GEMM
-DEC_EPI = {"store": 0, "residual": 1, "silu": 2, "gelu_tanh": 3}
+DEC_EPI = {"store": 0, "residual": 1, "silu": 2, "gelu_tanh": 3, "partial": 4}
 
 
 def dec_supported(M: int, N: int, K: int, epi: str = "store") -> bool:

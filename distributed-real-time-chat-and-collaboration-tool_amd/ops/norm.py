@@ -48,6 +48,27 @@ def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float, gemma: bool = False,
     return out
 
 
+def rmsnorm_partials(part, w: torch.Tensor, eps: float, gemma: bool = False,
+                     residual: torch.Tensor | None = None,
+                     out: torch.Tensor | None = None) -> tuple[torch.Tensor, torch.Tensor]:
+    """norm(sum of ``part``'s fp32 planes [+ residual]) * w for an ``ops.gemm.Partials``:
+    returns (out, h) with h = bf16(sum [+ residual]) - written into ``residual`` in place
+    when given (the residual stream), else into a new tensor."""
+    planes = part.planes
+    sk, rows, H = planes.shape
+    assert planes.dtype == torch.float32 and planes.is_contiguous()
+    assert w.shape == (H,) and w.dtype == torch.bfloat16 and w.is_contiguous()
+    add = residual is not None
+    h = residual if add else torch.empty((rows, H), dtype=torch.bfloat16, device=planes.device)
+    assert h.shape == (rows, H) and h.stride(1) == 1
+    if out is None:
+        out = torch.empty((rows, H), dtype=torch.bfloat16, device=planes.device)
+    check(hipk().rmsnorm_partials(out.data_ptr(), h.data_ptr(), planes.data_ptr(), sk, rows, H,
+                                  w.data_ptr(), float(eps), out.stride(0), h.stride(0), add,
+                                  bool(gemma), stream_ptr(planes)), "rmsnorm_partials")
+    return out, h
+
+
 class PendingNorm:
     """A pre-norm sublayer input whose RMSNorm has not run yet: norm(x [+
     residual]) * w.  The consumer either fuses the norm into its projection
@@ -76,6 +97,11 @@ class PendingNorm:
     def materialize(self) -> torch.Tensor:
         if self._out is None:
             res = self.residual
+            if not isinstance(self.x, torch.Tensor):  # split-K partial planes (ops.gemm)
+                self._out, h = rmsnorm_partials(self.x, self.w, self.eps, self.gemma,
+                                                residual=res)
+                self._h, self.x, self.residual = h, h, None
+                return self._out
             if self.pc is not None:
                 self._out = self.pc.reduce_norm(self.x, res, self.w, self.eps, self.gemma)
                 self.pc = None
