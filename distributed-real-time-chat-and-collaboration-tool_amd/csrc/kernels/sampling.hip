@@ -336,6 +336,9 @@ DRTC_DEVICE void sample_topk(SampShared& s, int* out_tokens, const unsigned shor
       v = s.val[tid];
       ix = s.idx[tid];
       const unsigned kv = ord16((unsigned short)(__float_as_uint(v) >> 16));
+      // unrolled: the LDS reads are broadcasts, issued 16 deep instead of one round trip
+      // each (a rolled loop over ~100 candidates was latency-bound: 116.7 vs 105.7 us)
+#pragma unroll 16
       for (int j = 0; j < n; ++j) {
         const unsigned kb = ord16((unsigned short)(__float_as_uint(s.val[j]) >> 16));
         rank += (kb > kv) || (kb == kv && s.idx[j] < ix);

@@ -225,21 +225,24 @@ def test_linear_partials_through_pending_norm(hipk, monkeypatch, M, N, K, sk, ge
     assert torch.equal(o2, out) and torch.equal(r2, r1)
 
 
-def test_decode_with_partials_matches_plain_decode(hipk, monkeypatch):
-    """The engine's full-batch decode with o / down as split-K partial planes (batch 800
-    >= W4_PARTIAL_MIN_M, hipGraphs) produces the same greedy tokens as the library path
-    on the tiny Llama (bf16 rounding differs by one rounding of each projection output)."""
+def test_decode_with_partials_matches_reference(hipk, monkeypatch):
+    """The engine's full-batch decode with o / down as split-K partial planes (batch 800 >=
+    W4_PARTIAL_MIN_M: 3 full 256-row tiles + a 32-row one, hipGraphs): every greedy token is
+    a maximiser (within bf16 tolerance) of the full-sequence reference forward's logits."""
     from drtc_amd.engine import LLMEngine, SamplingParams
     from drtc_amd.models import TINY_LLAMA, TransformerLM
     from drtc_amd.ops import gemm as Gm
 
+    monkeypatch.setattr(Gm, "W4_PARTIAL", {(256, 256): 4, (256, 512): 4})
     prompts = [[1 + (7 * i + j) % 500 for j in range(5 + i % 23)] for i in range(800)]
-    outs = []
-    for table in ({}, {(256, 256): 4, (256, 512): 4}):
-        monkeypatch.setattr(Gm, "W4_PARTIAL", table)
-        m = TransformerLM(TINY_LLAMA, "cuda", seed=21)
-        eng = LLMEngine(m, max_batch=800, max_model_len=256, num_blocks=2048, use_graphs=True)
-        reqs = eng.generate(prompts, SamplingParams.greedy(6, ignore_eos=True))
-        outs.append([r.output_ids for r in reqs])
-    same = sum(a == b for a, b in zip(*outs))
-    assert same >= 0.97 * len(prompts), same
+    m = TransformerLM(TINY_LLAMA, "cuda", seed=21)
+    eng = LLMEngine(m, max_batch=800, max_model_len=256, num_blocks=2048, use_graphs=True)
+    reqs = eng.generate(prompts, SamplingParams.greedy(6, ignore_eos=True))
+    bad = []
+    for i, (p, r) in enumerate(zip(prompts, reqs)):
+        ref = m.forward_reference([p + r.output_ids[:-1]])[0].float()
+        for j, tok in enumerate(r.output_ids):
+            row = ref[len(p) - 1 + j]
+            if row[tok] < row.max() - 0.05 * max(1.0, row.abs().max().item()):
+                bad.append((i, j))
+    assert not bad, bad[:10]
