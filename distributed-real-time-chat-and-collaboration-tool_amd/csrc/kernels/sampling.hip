@@ -13,8 +13,6 @@
 //    back to a 16-bit radix select (two histogram passes) and a ballot-
 //    compacted full gather.
 //    Candidates are bitonic-sorted; all tokens tied with the k-th value stay.
-//    Up to 256 candidates (the common case) are ordered by rank counting (one
-//    barrier) and the softmax prefix sum is one block scan (two barriers).
 //  * top_k == 0       : temperature sampling with EXACT top-p over the whole
 //    vocabulary (no candidate cap).  With p_i ~ exp(x_i / T) and
 //    P = top_p * sum(p), token i is in the nucleus iff the mass of tokens
@@ -41,7 +39,6 @@ constexpr int kSampThreads = 1024;
 constexpr int kSampWaves = kSampThreads / 64;
 constexpr int kCand = 1024;
 constexpr int kMaxRounds = 40;
-constexpr int kRankMax = 256;  // candidates ordered by rank counting up to this many
 
 DRTC_DEVICE unsigned ord16(unsigned short b) {
   return (b & 0x8000u) ? (unsigned)(~b & 0xFFFFu) : (unsigned)(b | 0x8000u);
@@ -327,45 +324,23 @@ DRTC_DEVICE void sample_topk(SampShared& s, int* out_tokens, const unsigned shor
     const unsigned thr = radix_kth(s, lr, V, vec, k);
     n = min(gather_ge(s, lr, V, vec, thr), kCand);
   }
-  if (n <= kRankMax) {
-    // ---- rank counting over the LDS list (one barrier): descending key, ties -> lower
-    // index first; keys (not floats) so NaN rows cannot collide ranks
-    float v = -INFINITY;
-    int ix = 0x7fffffff, rank = 0;
-    if (tid < n) {
-      v = s.val[tid];
-      ix = s.idx[tid];
-      const unsigned kv = ord16((unsigned short)(__float_as_uint(v) >> 16));
-      // unrolled: the LDS reads are broadcasts, issued 16 deep instead of one round trip
-      // each (a rolled loop over ~100 candidates was latency-bound: 116.7 vs 105.7 us)
-#pragma unroll 16
-      for (int j = 0; j < n; ++j) {
-        const unsigned kb = ord16((unsigned short)(__float_as_uint(s.val[j]) >> 16));
-        rank += (kb > kv) || (kb == kv && s.idx[j] < ix);
-      }
-    }
-    __syncthreads();
-    if (tid < n) { s.val[rank] = v; s.idx[rank] = ix; }
-    __syncthreads();
-  } else {
-    int np2 = 1;
-    while (np2 < n) np2 <<= 1;
-    // ---- bitonic sort, descending (ties -> lower index first)
-    for (int size = 2; size <= np2; size <<= 1) {
-      for (int stride = size >> 1; stride > 0; stride >>= 1) {
-        const int j = tid ^ stride;
-        if (tid < np2 && j > tid) {
-          const bool desc = ((tid & size) == 0);
-          const float a = s.val[tid], b = s.val[j];
-          const int ia = s.idx[tid], ib = s.idx[j];
-          const bool a_first = (a > b) || (a == b && ia < ib);
-          if (desc != a_first) {
-            s.val[tid] = b; s.val[j] = a;
-            s.idx[tid] = ib; s.idx[j] = ia;
-          }
+  int np2 = 1;
+  while (np2 < n) np2 <<= 1;
+  // ---- bitonic sort, descending (ties -> lower index first)
+  for (int size = 2; size <= np2; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      const int j = tid ^ stride;
+      if (tid < np2 && j > tid) {
+        const bool desc = ((tid & size) == 0);
+        const float a = s.val[tid], b = s.val[j];
+        const int ia = s.idx[tid], ib = s.idx[j];
+        const bool a_first = (a > b) || (a == b && ia < ib);
+        if (desc != a_first) {
+          s.val[tid] = b; s.val[j] = a;
+          s.idx[tid] = ib; s.idx[j] = ia;
         }
-        __syncthreads();
       }
+      __syncthreads();
     }
   }
   // keep exactly the elements >= the k-th value (ties with it included)
@@ -376,16 +351,24 @@ DRTC_DEVICE void sample_topk(SampShared& s, int* out_tokens, const unsigned shor
   }
   __syncthreads();
   n = s.misc[3];
-  // ---- softmax + inclusive prefix sum (one block scan) + top-p cut + draw
+  np2 = 1;
+  while (np2 < n) np2 <<= 1;
+  // ---- softmax + top-p + draw over the n candidates
   const float top = s.val[0];
-  const float pv = (tid < n) ? __expf((s.val[tid] - top) * (1.f / temp)) : 0.f;
-  float tot;
-  int lastp;
-  const float excl = block_excl_scan(s, pv, tot, lastp);  // barriers inside: val reads done
-  s.val[tid] = excl + pv;
+  const float inv_t = 1.f / temp;
+  const float pv = (tid < n) ? __expf((s.val[tid] - top) * inv_t) : 0.f;
+  __syncthreads();
+  s.val[tid] = pv;
+  __syncthreads();
+  for (int off = 1; off < np2; off <<= 1) {  // inclusive Hillis-Steele scan
+    const float add = (tid >= off && tid < np2) ? s.val[tid - off] : 0.f;
+    __syncthreads();
+    s.val[tid] += add;
+    __syncthreads();
+  }
+  const float total = s.val[n - 1];
   if (tid == 0) s.misc[3] = n - 1;
   __syncthreads();
-  const float total = s.val[n - 1];
   {
     const float need = pp * total;
     const bool hit = tid < n && s.val[tid] >= need && (tid == 0 || s.val[tid - 1] < need);
