@@ -112,9 +112,13 @@ class ChatTokenizer:
         self._bytes = {i: bytes([i - self.byte_base]) for i in range(self.byte_base, self.byte_base + 256)}
 
     def encode(self, text: str, add_bos: bool = True) -> list[int]:
-        out = [self.bos_id] if add_bos else []
         get = self.tok_to_id.get
-        for piece in _PIECE.findall(text):
+        pieces = _PIECE.findall(text)
+        ids = list(map(get, pieces))  # one C-level pass: the serving path's common case
+        if None not in ids:
+            return [self.bos_id, *ids] if add_bos else ids
+        out = [self.bos_id] if add_bos else []
+        for piece in pieces:
             t = get(piece)
             if t is not None:
                 out.append(t)
