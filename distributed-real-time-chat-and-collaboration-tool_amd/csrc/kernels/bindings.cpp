@@ -36,6 +36,12 @@ PYBIND11_MODULE(_hipk, m) {
                                          rows, H, P<const void>(w), eps, out_stride, res_stride,
                                          add_residual, gemma, S(st));
   });
+  m.def("row_rinv", [](u64 rinv, u64 x, int rows, int H, int x_stride, float eps, u64 st) {
+    return drtc::launch_row_rinv(P<float>(rinv), P<const void>(x), rows, H, x_stride, eps, S(st));
+  });
+  m.def("rowsq_rinv", [](u64 rinv, u64 sq, int M, int slots, int H, float eps, u64 st) {
+    return drtc::launch_rowsq_rinv(P<float>(rinv), P<const float>(sq), M, slots, H, eps, S(st));
+  });
   m.def("act_glu", [](u64 out, u64 gu, int64_t T, int I, int gu_stride, int act,
                       u64 st) {
     return drtc::launch_act_glu(P<void>(out), P<void>(gu), T, I, gu_stride, act, S(st));

@@ -65,7 +65,16 @@ constexpr int kW4Lds = 2 * kW4Stage;
 // all CUs at HBM rate.  For the full-batch decode projections (M = 1024, N = 4096: 64
 // tiles of 256 x 256), split-K 4 fills the chip and no single workgroup has to read the
 // other slices' partials (the last-arriver combine read 768 KiB alone: 155 vs 80 us).
-enum { W4_STORE = 0, W4_RESIDUAL = 1, W4_SILU = 2, W4_GELU = 3, W4_PARTIAL = 4 };
+// RMSNorm folded across a prefill layer (TP = 1): the o / down projection's residual epilogue
+// also emits each row's partial sum of squares of the new residual stream h over its 128
+// columns (W4_RESIDUAL_SQ, `slab` = sq[M][N / 128]); a tiny kernel turns them into
+// rinv = rsqrt(mean(h^2) + eps) (rowsq_rinv_kernel); the next qkv / gate_up GEMM reads h
+// itself with the norm weight folded into W and scales each output row by rinv
+// (W4_STORE_RS / W4_SILU_RS / W4_GELU_RS, `slab` = rinv[M]) - no [M, H] normalised copy.
+enum {
+  W4_STORE = 0, W4_RESIDUAL = 1, W4_SILU = 2, W4_GELU = 3, W4_PARTIAL = 4,
+  W4_RESIDUAL_SQ = 5, W4_STORE_RS = 6, W4_SILU_RS = 7, W4_GELU_RS = 8
+};
 
 struct W4Params {
   bf16_t* c;
@@ -82,7 +91,15 @@ struct W4Params {
 };
 
 template <int EPI>
-DRTC_DEVICE constexpr bool w4_glu() { return EPI == W4_SILU || EPI == W4_GELU; }
+DRTC_DEVICE constexpr bool w4_glu() {
+  return EPI == W4_SILU || EPI == W4_GELU || EPI == W4_SILU_RS || EPI == W4_GELU_RS;
+}
+template <int EPI>
+DRTC_DEVICE constexpr bool w4_res() { return EPI == W4_RESIDUAL || EPI == W4_RESIDUAL_SQ; }
+template <int EPI>
+DRTC_DEVICE constexpr bool w4_rs() { return EPI == W4_STORE_RS || EPI == W4_SILU_RS || EPI == W4_GELU_RS; }
+template <int EPI>
+DRTC_DEVICE constexpr int w4_act() { return (EPI == W4_SILU || EPI == W4_SILU_RS) ? 0 : 1; }
 
 // One LDS-DMA wave-instruction: 64 lanes x 16 B from rsrc + voff + soff into LDS bytes
 // [dst, dst + 1024).  Inline asm (hipcc would pin vmcnt / lgkmcnt waits around a builtin
@@ -303,23 +320,25 @@ DRTC_DEVICE void w4_epilogue(const W4Params& p, f32x4 (&acc)[8][8], int tm, int 
       const int m = 256 * tm + 128 * wm + 16 * i + 4 * g + r;
       if (m >= p.M) continue;
       bf16_t* crow = p.c + (int64_t)m * p.ldc;
+      float sc = 1.f;  // folded RMSNorm: this row's rsqrt(mean(h^2) + eps)
+      if constexpr (w4_rs<EPI>()) sc = p.slab[m];
       if constexpr (w4_glu<EPI>()) {
         const int n = 128 * tn + 64 * wn + 4 * l16;
         bf16x4 o;
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-          o[j] = f2bf(act_value<EPI == W4_SILU ? 0 : 1>(acc[i][j][r]) * acc[i][j + 4][r]);
+          o[j] = f2bf(act_value<w4_act<EPI>()>(acc[i][j][r] * sc) * (acc[i][j + 4][r] * sc));
         w4_st8<V>(crow + n, o);
-      } else if constexpr (EPI != W4_RESIDUAL) {
+      } else if constexpr (!w4_res<EPI>()) {
         const int n = 256 * tn + 128 * wn + 8 * l16;
         bf16x8 o;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) o[j] = f2bf(acc[i][j][r]);
+        for (int j = 0; j < 8; ++j) o[j] = f2bf(acc[i][j][r] * sc);
         w4_st16<V>(crow + n, o);
       }
     }
   }
-  if constexpr (EPI == W4_RESIDUAL) {
+  if constexpr (w4_res<EPI>()) {
     // every residual row is loaded before the first store: R may alias C (in-place add into
     // the residual stream), so a load placed after a store could not be hoisted above it and
     // each (load, add, store) would pay a full memory round trip
@@ -337,10 +356,22 @@ DRTC_DEVICE void w4_epilogue(const W4Params& p, f32x4 (&acc)[8][8], int tm, int 
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int m = 256 * tm + 128 * wm + 16 * i + 4 * g + r;
-        if (m >= p.M) continue;
         bf16x8 o;
 #pragma unroll
         for (int j = 0; j < 8; ++j) o[j] = f2bf(acc[i][j][r] + bf2f(rv[i][r][j]));
+        if constexpr (EPI == W4_RESIDUAL_SQ) {
+          // this wave's 128 columns of row m: 8 per lane, reduced over the 16 lanes of the
+          // row (lane bits 0-3); every lane takes part (rows past M computed, not stored)
+          float sq = 0.f;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) sq += bf2f(o[j]) * bf2f(o[j]);
+          sq += __shfl_xor(sq, 1, 64);
+          sq += __shfl_xor(sq, 2, 64);
+          sq += __shfl_xor(sq, 4, 64);
+          sq += __shfl_xor(sq, 8, 64);
+          if (l16 == 0 && m < p.M) p.slab[(int64_t)m * (2 * p.tiles_n) + 2 * tn + wn] = sq;
+        }
+        if (m >= p.M) continue;
         w4_st16<V>(p.c + (int64_t)m * p.ldc + n, o);
       }
   }
@@ -408,13 +439,13 @@ DRTC_DEVICE void w4_epi_frag(const W4Params& p, const f32x4 (&v)[8], int tm, int
       bf16x4 o;
 #pragma unroll
       for (int j = 0; j < 4; ++j)
-        o[j] = f2bf(act_value<EPI == W4_SILU ? 0 : 1>(v[j][r]) * v[j + 4][r]);
+        o[j] = f2bf(act_value<w4_act<EPI>()>(v[j][r]) * v[j + 4][r]);
       w4_st8<V>(p.c + (int64_t)(m0 + r) * p.ldc + n, o);
     }
   } else {
     const int n = 256 * tn + 128 * wn + 8 * l16;
     bf16x8 rv[4];
-    if constexpr (EPI == W4_RESIDUAL) {
+    if constexpr (w4_res<EPI>()) {
 #pragma unroll
       for (int r = 0; r < 4; ++r)
         rv[r] = *reinterpret_cast<const bf16x8*>(p.r + (int64_t)min(m0 + r, p.M - 1) * p.ldr + n);
@@ -426,7 +457,7 @@ DRTC_DEVICE void w4_epi_frag(const W4Params& p, const f32x4 (&v)[8], int tm, int
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         float x = v[j][r];
-        if constexpr (EPI == W4_RESIDUAL) x += bf2f(rv[r][j]);
+        if constexpr (w4_res<EPI>()) x += bf2f(rv[r][j]);
         o[j] = f2bf(x);
       }
       w4_st16<V>(p.c + (int64_t)(m0 + r) * p.ldc + n, o);
@@ -702,8 +733,15 @@ int launch_gemm_w4(void* c, const void* a, const void* b, const void* r, int M, 
                    int group_m, void* slab, int64_t slab_bytes, int* counters, int n_counters,
                    int v, hipStream_t st) {
   // shape contract (checked here so a bad call never reaches the device)
-  const bool glu = epi == W4_SILU || epi == W4_GELU;
+  const bool glu = epi == W4_SILU || epi == W4_GELU || epi == W4_SILU_RS || epi == W4_GELU_RS;
+  const bool res = epi == W4_RESIDUAL || epi == W4_RESIDUAL_SQ;
   if (M <= 0 || N <= 0 || K <= 0 || K % 64 || splitk < 1 || (K / 64) % splitk) return -1;
+  // folded-norm epilogues: `slab` is the side buffer (sq[M][N/128] or rinv[M]), one slice
+  if (epi >= W4_RESIDUAL_SQ) {
+    const int64_t need = epi == W4_RESIDUAL_SQ ? (int64_t)M * (N / 128) * 4 : (int64_t)M * 4;
+    if (epi > W4_GELU_RS || splitk != 1 || (v & 4) || slab == nullptr || slab_bytes < need)
+      return -1;
+  }
   if (epi == W4_PARTIAL) {  // fp32 planes [splitk][M][N] in `slab`, no counters
     if (N % 256 || lda % 8 || (uintptr_t)a % 16 || (uintptr_t)b % 16 || slab == nullptr ||
         (uintptr_t)slab % 16 || slab_bytes < (int64_t)splitk * M * N * 4 || (v & 4))
@@ -725,7 +763,7 @@ int launch_gemm_w4(void* c, const void* a, const void* b, const void* r, int M, 
   }
   if (glu ? (N % 128 || up_off != N) : (N % 256)) return -1;
   if (lda % 8 || ldb % 8 || (glu ? ldc % 4 : ldc % 8)) return -1;
-  if (epi == W4_RESIDUAL && (ldr % 8 || r == nullptr || (uintptr_t)r % 16)) return -1;
+  if (res && (ldr % 8 || r == nullptr || (uintptr_t)r % 16)) return -1;
   if ((uintptr_t)a % 16 || (uintptr_t)b % 16 || (uintptr_t)c % (glu ? 8 : 16)) return -1;
   // 32-bit buffer offsets: every staged row must sit within 2 GiB of its operand base
   if ((int64_t)min(M, 256) * lda * 2 >= (1ll << 31)) return -1;
@@ -744,6 +782,7 @@ int launch_gemm_w4(void* c, const void* a, const void* b, const void* r, int M, 
   p.kt_split = K / 64 / splitk;
   p.up_off = up_off;
   p.group_m = group_m;
+  if (epi >= W4_RESIDUAL_SQ) p.slab = (float*)slab;
   if (splitk > 1) {
     const int64_t tiles = (int64_t)p.tiles_m * p.tiles_n;
     if (slab == nullptr || counters == nullptr || n_counters < 2 * tiles + 1 ||
@@ -759,13 +798,18 @@ int launch_gemm_w4(void* c, const void* a, const void* b, const void* r, int M, 
     case W4_RESIDUAL: return w4_launch<W4_RESIDUAL>(p, v, st);
     case W4_SILU: return w4_launch<W4_SILU>(p, v, st);
     case W4_GELU: return w4_launch<W4_GELU>(p, v, st);
+    case W4_RESIDUAL_SQ: return w4_launch<W4_RESIDUAL_SQ>(p, v, st);
+    case W4_STORE_RS: return w4_launch<W4_STORE_RS>(p, v, st);
+    case W4_SILU_RS: return w4_launch<W4_SILU_RS>(p, v, st);
+    case W4_GELU_RS: return w4_launch<W4_GELU_RS>(p, v, st);
     default: return -1;
   }
 }
 
 int configure_gemm_w4() {
   return w4_cfg<W4_STORE>() | w4_cfg<W4_RESIDUAL>() | w4_cfg<W4_SILU>() | w4_cfg<W4_GELU>() |
-         w4_cfg<W4_PARTIAL>();
+         w4_cfg<W4_PARTIAL>() | w4_cfg<W4_RESIDUAL_SQ>() | w4_cfg<W4_STORE_RS>() |
+         w4_cfg<W4_SILU_RS>() | w4_cfg<W4_GELU_RS>();
 }
 
 }  // namespace drtc

@@ -14,6 +14,10 @@ namespace drtc {
 int launch_rmsnorm_partials(void* out, void* residual, const float* part, int sk, int rows,
                             int H, const void* w, float eps, int out_stride, int res_stride,
                             bool add_residual, bool gemma, hipStream_t st);
+int launch_row_rinv(float* rinv, const void* x, int rows, int H, int x_stride, float eps,
+                    hipStream_t st);
+int launch_rowsq_rinv(float* rinv, const float* sq, int M, int slots, int H, float eps,
+                      hipStream_t st);
 int launch_rmsnorm(void* out, void* residual, const void* x, const void* w,
                    int rows, int H, float eps, int x_stride, int out_stride,
                    int res_stride, bool gemma, hipStream_t st);

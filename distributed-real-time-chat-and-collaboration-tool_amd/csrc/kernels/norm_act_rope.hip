@@ -216,6 +216,71 @@ int launch_rmsnorm_partials(void* out, void* residual, const float* part, int sk
   return (int)hipGetLastError();
 }
 
+// rinv[m] = rsqrt(sum_s sq[m][s] / H + eps): the RMSNorm statistic of rows whose partial
+// sums of squares were emitted by a residual GEMM epilogue (gemm_w4 W4_RESIDUAL_SQ), summed in
+// fixed order (deterministic).
+__global__ __launch_bounds__(256) void rowsq_rinv_kernel(float* __restrict__ rinv,
+                                                         const float* __restrict__ sq, int M,
+                                                         int slots, int H, float eps) {
+  const int m = blockIdx.x * 256 + threadIdx.x;
+  if (m >= M) return;
+  const float* row = sq + (int64_t)m * slots;
+  float t = 0.f;
+  for (int s = 0; s < slots; s += 4) {
+    const f32x4 v = *reinterpret_cast<const f32x4*>(row + s);
+    t += v[0] + v[1] + v[2] + v[3];
+  }
+  rinv[m] = rsqrtf(t / (float)H + eps);
+}
+
+// rinv[row] = rsqrt(mean(x[row]^2) + eps) straight from the rows (a residual stream written
+// by a library GEMM): the RMSNorm's statistic without its normalised [rows, H] output.
+template <int VPT>
+__global__ __launch_bounds__(256) void row_rinv_kernel(float* __restrict__ rinv,
+                                                       const bf16_t* __restrict__ x, int H,
+                                                       int x_stride, float eps) {
+  const int row = blockIdx.x, tid = threadIdx.x;
+  const bf16_t* xr = x + (int64_t)row * x_stride;
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int idx = (tid + i * 256) * 8;
+    if (idx < H) {
+      const bf16x8 a = load_bf16x8(xr + idx);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ss += bf2f(a[j]) * bf2f(a[j]);
+    }
+  }
+  __shared__ float red[4];
+  ss = wave_sum(ss);
+  if ((tid & 63) == 0) red[tid >> 6] = ss;
+  __syncthreads();
+  if (tid == 0) rinv[row] = rsqrtf((red[0] + red[1] + red[2] + red[3]) / (float)H + eps);
+}
+
+int launch_row_rinv(float* rinv, const void* x, int rows, int H, int x_stride, float eps,
+                    hipStream_t st) {
+  const int vpt = (H / 8 + 255) / 256;
+  if (H % 8 || vpt < 1 || vpt > 4 || x_stride % 8) return -1;
+  if (rows == 0) return 0;
+  switch (vpt) {
+    case 1: hipLaunchKernelGGL(row_rinv_kernel<1>, dim3(rows), dim3(256), 0, st, rinv, (const bf16_t*)x, H, x_stride, eps); break;
+    case 2: hipLaunchKernelGGL(row_rinv_kernel<2>, dim3(rows), dim3(256), 0, st, rinv, (const bf16_t*)x, H, x_stride, eps); break;
+    case 3: hipLaunchKernelGGL(row_rinv_kernel<3>, dim3(rows), dim3(256), 0, st, rinv, (const bf16_t*)x, H, x_stride, eps); break;
+    default: hipLaunchKernelGGL(row_rinv_kernel<4>, dim3(rows), dim3(256), 0, st, rinv, (const bf16_t*)x, H, x_stride, eps); break;
+  }
+  return (int)hipGetLastError();
+}
+
+int launch_rowsq_rinv(float* rinv, const float* sq, int M, int slots, int H, float eps,
+                      hipStream_t st) {
+  if (M <= 0) return 0;
+  if (slots % 4 || (uintptr_t)sq % 16) return -1;
+  hipLaunchKernelGGL(rowsq_rinv_kernel, dim3((M + 255) / 256), dim3(256), 0, st, rinv, sq, M,
+                     slots, H, eps);
+  return (int)hipGetLastError();
+}
+
 // ------------------------------------------------------- gated activations
 template <int ACT>  // 0 = SiLU, 1 = tanh-GELU
 __global__ __launch_bounds__(256) void act_glu_kernel(

@@ -213,6 +213,7 @@ class TransformerLM:
                     L["down"] = put(rnd(H, sh.inter))
             self.layers.append(L)
         self.final_norm = norm_w()
+        self.fold_norm_weights()
         if cfg.tie_embeddings:
             v0 = sh.rank * sh.vocab
             self.lm_head = self.embed[v0:v0 + sh.vocab]
@@ -224,10 +225,33 @@ class TransformerLM:
             else:
                 self.lm_head = put(rnd(sh.vocab, H))
 
+    def fold_norm_weights(self) -> None:
+        """Projections with the preceding RMSNorm weight folded into their input columns
+        (``qkv_n`` = W_qkv diag(g_in), ``gate_up_n`` = W_gate_up diag(g_post); Gemma: 1 + w):
+        a prefill pass whose o / down GEMM left the norm's row statistic runs these on the
+        raw residual stream and scales the rows (ops.gemm.rs_linear) instead of writing a
+        normalised copy.  With unit norm weights (random init) they alias the originals -
+        no extra memory.  Call again after loading weights."""
+        g1 = 1.0 if self.cfg.gemma_norm else 0.0
+        for L in self.layers:
+            for name, ln in (("qkv", "ln_in"), ("gate_up", "ln_post")):
+                w = L.get(name)
+                if w is None or w.dim() != 2:  # MoE experts keep the plain norm
+                    continue
+                g = L[ln].float() + g1
+                if bool((g == 1.0).all()):
+                    L[name + "_n"] = w
+                else:
+                    L[name + "_n"] = (w.float() * g[None, :]).to(w.dtype).contiguous()
+
     def weight_bytes(self) -> int:
         n = self.embed.numel() + self.final_norm.numel()
         for L in self.layers:
-            n += sum(t.numel() for t in L.values())
+            seen = set()
+            for t in L.values():
+                if t.data_ptr() not in seen:  # folded-norm aliases counted once
+                    seen.add(t.data_ptr())
+                    n += t.numel()
         if not self.cfg.tie_embeddings:
             n += self.lm_head.numel()
         return n * self.embed.element_size()
@@ -246,10 +270,10 @@ class TransformerLM:
             return self._moe(L, x.materialize(), decode), False
         if ops.w4_glu_ok(x.x, L["gate_up"], self.cfg.act):
             # prefill-sized: gate_up GEMM with the GLU in its epilogue (gemm_w4.hip)
-            h = ops.norm_glu(x, L["gate_up"], self.cfg.act)
+            h = ops.norm_glu(x, L["gate_up"], self.cfg.act, L.get("gate_up_n"))
             res = self._fusable_residual(h, x)
             if res is not None:
-                return ops.linear_residual(h, L["down"], res), True
+                return ops.linear_residual_rinv(h, L["down"], res, self.cfg.rms_eps), True
             if decode and self.pc.tp_size == 1:
                 # full-batch decode: split-K partial planes summed by the next norm
                 return ops.linear_partials(h, L["down"]), False
@@ -358,13 +382,17 @@ class TransformerLM:
             # residual stream in its GEMM epilogue, o IS the new stream;
             # partial = o is still a TP partial sum - the next norm runs the
             # all-reduce fused with the residual add (ParallelContext.reduce_norm)
+            # (o, rinv): the GEMM epilogue also left the next norm's row statistic
             o, added, *part = attn_fn(i, L, x)
+            o, rinv = o if isinstance(o, tuple) else (o, None)
             x = ops.PendingNorm(o, None if added else x.stream(), L["ln_post"], cfg.rms_eps,
-                                cfg.gemma_norm, pc=self.pc if part and part[0] else None)
+                                cfg.gemma_norm, pc=self.pc if part and part[0] else None,
+                                rinv=rinv)
             m, added, *part = self._mlp(L, x, decode)
+            m, rinv = m if isinstance(m, tuple) else (m, None)
             nxt = self.layers[i + 1]["ln_in"] if i + 1 < n else self.final_norm
             x = ops.PendingNorm(m, None if added else x.stream(), nxt, cfg.rms_eps, cfg.gemma_norm,
-                                pc=self.pc if part and part[0] else None)
+                                pc=self.pc if part and part[0] else None, rinv=rinv)
         return x.materialize()
 
     def _logits(self, x: torch.Tensor) -> torch.Tensor:
@@ -382,7 +410,7 @@ class TransformerLM:
         D = cfg.head_dim
 
         def attn(i, L, x):
-            qkv = ops.norm_linear(x, L["qkv"])
+            qkv = ops.norm_linear(x, L["qkv"], L.get("qkv_n"))
             kc, vc = kv_caches[i] if kv_caches is not None else (None, None)
             blockwise_v = kc is not None and meta.v_segs is not None
             ops.rope_kv_(qkv, meta.positions, meta.slots if kc is not None else None,
@@ -405,7 +433,7 @@ class TransformerLM:
                 x.select_rows(meta.last_idx)
             res = self._fusable_residual(a, x)
             if res is not None:
-                return ops.linear_residual(a, L["o"], res), True
+                return ops.linear_residual_rinv(a, L["o"], res, cfg.rms_eps), True
             return self.pc.all_reduce_tp(ops.linear(a, L["o"])), False
 
         last = len(self.layers) - 1

@@ -13,15 +13,17 @@ from .activation import act_glu, act_glu_ref
 from .attention import (KV_BLOCK, DecodeWorkspace, decode_partitioning, paged_decode_attention,
                         paged_decode_attention_rope, set_prefill_persist,
                         paged_decode_ref, prefill_attention, prefill_attention_ref, prefill_tiles)
-from .gemm import (Partials, glu_linear, linear, linear_partials, linear_residual, mfma_gemm,
-                   norm_glu, norm_linear, residual_fusable, w4_glu_ok)
+from .gemm import (Partials, glu_linear, linear, linear_partials, linear_residual,
+                   linear_residual_rinv, mfma_gemm, norm_glu, norm_linear, residual_fusable,
+                   rs_linear, w4_glu_ok)
 from .moe import fused_moe, fused_moe_ref
 from .norm import PendingNorm, rmsnorm, rmsnorm_partials, rmsnorm_ref
 from .rope import build_rope_cache, kv_write_v, kv_write_v_ref, rope_kv_, rope_kv_ref
 from .sampling import sample, sample_ref
 
 __all__ = [
-    "on_gpu", "reference_mode", "linear", "linear_partials", "Partials", "rmsnorm_partials", "norm_linear", "glu_linear", "norm_glu", "w4_glu_ok", "mfma_gemm", "linear_residual", "residual_fusable", "PendingNorm", "fused_moe", "fused_moe_ref",
+    "on_gpu", "reference_mode", "linear", "linear_partials", "Partials", "rmsnorm_partials",
+    "linear_residual_rinv", "rs_linear", "norm_linear", "glu_linear", "norm_glu", "w4_glu_ok", "mfma_gemm", "linear_residual", "residual_fusable", "PendingNorm", "fused_moe", "fused_moe_ref",
     "act_glu", "act_glu_ref", "KV_BLOCK", "DecodeWorkspace", "decode_partitioning",
     "paged_decode_attention", "paged_decode_attention_rope", "paged_decode_ref", "prefill_attention", "prefill_attention_ref",
     "prefill_tiles", "rmsnorm", "rmsnorm_ref", "build_rope_cache", "rope_kv_", "rope_kv_ref",

@@ -289,15 +289,22 @@ def _choice(M: int, N: int, K: int, ldx: int) -> int:
     return ent[1] if M <= SKINNY_MAX_M else 0
 
 
-def norm_linear(p, w: torch.Tensor) -> torch.Tensor:
+def norm_linear(p, w: torch.Tensor, w_folded: torch.Tensor | None = None) -> torch.Tensor:
     """y = rmsnorm(p.x [+ p.residual]) @ w.T for an ``ops.PendingNorm`` p.
 
     When the projection would run on the skinny dot2 kernel anyway (small
     decode batches, measured per shape) the norm is fused into it
     (gemv.hip ``skinny_norm_gemm_kernel``): one launch instead of two, and
-    the new residual stream is written by the GEMM.  Otherwise the norm is
-    materialised and ``linear`` runs."""
+    the new residual stream is written by the GEMM.  When the producer left the
+    norm's row statistic (``p.rinv``) and the caller passes the projection with
+    the norm weight folded in (``w_folded``), the 4-wave GEMM reads the residual
+    stream itself and scales its rows (``rs_linear``: no normalised copy).
+    Otherwise the norm is materialised and ``linear`` runs."""
     x, res = p.x, p.residual
+    if p.rinv is not None and p._out is None and w_folded is not None:
+        y = rs_linear(x, w_folded, p.rinv)
+        if y is not None:
+            return y
     if (_fuse_norm and p._out is None and p.pc is None and isinstance(x, torch.Tensor)
             and on_gpu(x) and _enabled and x.dim() == 2
             and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and x.stride(1) == 1
@@ -345,7 +352,8 @@ def glu_linear(gu: torch.Tensor, w: torch.Tensor, act: str = "silu") -> torch.Te
 
 
 # ------------------------------------------------------------ hand-written MFMA GEMM
-EPI = {"store": 0, "residual": 1, "silu": 2, "gelu_tanh": 3, "partial": 4}
+EPI = {"store": 0, "residual": 1, "silu": 2, "gelu_tanh": 3, "partial": 4, "residual_sq": 5,
+       "store_rs": 6, "silu_rs": 7, "gelu_tanh_rs": 8}
 _ws_lock = threading.Lock()
 _ws: dict[int, tuple[torch.Tensor, torch.Tensor]] = {}
 WS_SLAB_BYTES = 128 << 20   # fp32 split-K slabs (per device)
@@ -379,7 +387,8 @@ def new_gemm_workspace(dev: torch.device) -> tuple[torch.Tensor, torch.Tensor]:
 def mfma_gemm(x: torch.Tensor, w: torch.Tensor, epi: str = "store",
               residual: torch.Tensor | None = None, out: torch.Tensor | None = None,
               variant: int = 2, splitk: int = 1, group_m: int = 8,
-              ws: tuple[torch.Tensor, torch.Tensor] | None = None) -> torch.Tensor:
+              ws: tuple[torch.Tensor, torch.Tensor] | None = None,
+              side: torch.Tensor | None = None) -> torch.Tensor:
     """Hand-written CDNA4 GEMM (csrc/kernels/gemm.hip): y = epi(x @ w.T).
 
     epi "store": y = x @ w.T; "residual": y = x @ w.T + residual (``out`` may
@@ -389,12 +398,15 @@ def mfma_gemm(x: torch.Tensor, w: torch.Tensor, epi: str = "store",
     Shapes: K % 64 == 0, N % 256 == 0 (I % 128 == 0 for the gated forms),
     (K / 64) % splitk == 0; rows of x are unrestricted."""
     M, K = x.shape
-    glu = epi in ("silu", "gelu_tanh")
+    glu = epi in ("silu", "gelu_tanh", "silu_rs", "gelu_tanh_rs")
     N = w.shape[0] // 2 if glu else w.shape[0]
     if out is None:
         out = torch.empty((M, N), dtype=x.dtype, device=x.device)
     st = stream_ptr(x)
     slab, cnt = ((ws or gemm_workspace(x.device)) if splitk > 1 else (None, None))
+    if side is not None:  # folded-norm epilogues (gemm_w4): sq[M][N/128] or rinv[M], fp32
+        assert gemm_w4_variant(variant) and splitk == 1 and side.dtype == torch.float32
+        slab = side
     check(hipk().gemm(out.data_ptr(), x.data_ptr(), w.data_ptr(), ptr(residual), M, N, K,
                       x.stride(0), w.stride(0), out.stride(0),
                       residual.stride(0) if residual is not None else 0, EPI[epi],
@@ -437,6 +449,58 @@ def save_entries(entries: dict[str, dict], path: str | None = None) -> str:
         json.dump(data, f, indent=1, sort_keys=True)
     reset()
     return path
+
+
+def gemm_w4_variant(variant: int) -> bool:
+    return 7 <= variant <= 14
+
+
+# ------------------------------------------------------------ folded RMSNorm (prefill)
+_fold_norm = os.environ.get("DRTC_FOLD_NORM", "1") != "0"
+
+
+def linear_residual_rinv(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor, eps: float):
+    """residual += x @ w.T (in place, ``linear_residual``) and, when the 4-wave hand GEMM takes
+    the shape, the next RMSNorm's row statistic from the same epilogue: returns (h, rinv) with
+    rinv = rsqrt(mean(h^2) + eps) fp32 [M] (each row's partial sums of squares over 128
+    columns from gemm_w4 W4_RESIDUAL_SQ, finished by rowsq_rinv_kernel).  (h, None) when the
+    shape runs elsewhere."""
+    M, K = x.shape
+    N = w.shape[0]
+    if not (_fold_norm and on_gpu(x) and M >= W4_MIN_M and N % 512 == 0):
+        return linear_residual(x, w, residual), None
+    rinv = torch.empty(M, dtype=torch.float32, device=x.device)
+    if not w4_ok(x, w, residual):
+        # a library GEMM (down, K > W4_MAX_K): the statistic from one read of the rows
+        h = linear_residual(x, w, residual)
+        check(hipk().row_rinv(rinv.data_ptr(), h.data_ptr(), M, N, h.stride(0), float(eps),
+                              stream_ptr(x)), "row_rinv")
+        return h, rinv
+    sq = torch.empty((M, N // 128), dtype=torch.float32, device=x.device)
+    mfma_gemm(x, w, "residual_sq", residual=residual, out=residual, variant=W4_VARIANT,
+              group_m=w4_group_m(M, N, K), side=sq)
+    check(hipk().rowsq_rinv(rinv.data_ptr(), sq.data_ptr(), M, N // 128, N, float(eps),
+                            stream_ptr(x)), "rowsq_rinv")
+    return residual, rinv
+
+
+def rs_linear(h: torch.Tensor, w_folded: torch.Tensor, rinv: torch.Tensor,
+              act: str | None = None) -> torch.Tensor | None:
+    """norm(h) @ W.T as (h @ (W diag(g)).T) * rinv[row] on gemm_w4 (``w_folded`` = W with the
+    RMSNorm weight g folded into its columns), with the gated activation in the epilogue when
+    ``act`` is given (``w_folded`` = the fused [gate; up]); None when the shape cannot take it
+    (the caller materialises the norm)."""
+    if act is None:
+        if not w4_ok(h, w_folded):
+            return None
+        M, K = h.shape
+        return mfma_gemm(h, w_folded, "store_rs", variant=W4_VARIANT,
+                         group_m=w4_group_m(M, w_folded.shape[0], K), side=rinv)
+    if not (w4_glu_ok(h, w_folded, act) and h.shape[0] >= W4_MIN_M):
+        return None
+    M, K = h.shape
+    return mfma_gemm(h, w_folded, act + "_rs", variant=W4_VARIANT,
+                     group_m=w4_group_m(M, w_folded.shape[0] // 2, K, glu=True), side=rinv)
 
 
 # ------------------------------------------------------------ 4-wave GEMM dispatch
@@ -627,12 +691,17 @@ def w4_glu_ok(x: torch.Tensor, w: torch.Tensor, act: str) -> bool:
             and x.stride(0) % 8 == 0 and x.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0)
 
 
-def norm_glu(p, w: torch.Tensor, act: str = "silu") -> torch.Tensor:
+def norm_glu(p, w: torch.Tensor, act: str = "silu",
+             w_folded: torch.Tensor | None = None) -> torch.Tensor:
     """h = act(norm(x) @ gate^T) * (norm(x) @ up^T) for an ``ops.PendingNorm`` p and the
     fused [gate; up] weight: on the 4-wave hand GEMM with the GLU in its epilogue when
     ``w4_glu_ok`` (one launch, no [M, 2I] intermediate), else norm_linear + act_glu."""
     from .activation import act_glu
 
+    if p.rinv is not None and p._out is None and w_folded is not None:
+        y = rs_linear(p.x, w_folded, p.rinv, act)  # folded norm (see norm_linear)
+        if y is not None:
+            return y
     if w4_glu_ok(p.x, w, act):
         x = p.materialize()
         M, K = x.shape
@@ -644,12 +713,13 @@ def norm_glu(p, w: torch.Tensor, act: str = "silu") -> torch.Tensor:
 __all__ = ["linear", "norm_linear", "glu_linear", "norm_glu", "w4_glu_ok", "skinny_linear", "skinny_ok", "skinny_variant",
            "skinny_supports", "mfma_gemm", "midm_gemm", "midm_supported", "dec_gemm", "dec_supported",
            "tune", "save_entries", "w4_ok", "w4_group_m", "w4_rs_splitk", "w4_dec_splitk",
-           "Partials", "linear_partials", "w4_partial_splitk",
+           "Partials", "linear_partials", "w4_partial_splitk", "linear_residual_rinv", "rs_linear",
            "load_table", "reset", "set_enabled", "table_path"]
 
 
 # ------------------------------------------------------------------ medium-M decode GEMM
-MIDM_EPI = {"store": 0, "residual": 1, "silu": 2, "gelu_tanh": 3, "partial": 4}
+MIDM_EPI = {"store": 0, "residual": 1, "silu": 2, "gelu_tanh": 3, "partial": 4, "residual_sq": 5,
+       "store_rs": 6, "silu_rs": 7, "gelu_tanh_rs": 8}
 MIDM_MAX_M = 256
 
 
@@ -711,7 +781,8 @@ def midm_gemm(x: torch.Tensor, w: torch.Tensor, epi: str = "store",
 
 
 # ------------------------------------------------------------------ decode-batch GEMM
-DEC_EPI = {"store": 0, "residual": 1, "silu": 2, "gelu_tanh": 3, "partial": 4}
+DEC_EPI = {"store": 0, "residual": 1, "silu": 2, "gelu_tanh": 3, "partial": 4, "residual_sq": 5,
+       "store_rs": 6, "silu_rs": 7, "gelu_tanh_rs": 8}
 
 
 def dec_supported(M: int, N: int, K: int, epi: str = "store") -> bool:

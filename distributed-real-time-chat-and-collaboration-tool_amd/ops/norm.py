@@ -78,17 +78,25 @@ class PendingNorm:
     (x itself when there is no residual), which the next PendingNorm adds to.
     """
 
-    __slots__ = ("x", "residual", "w", "eps", "gemma", "_h", "_out", "pc")
+    __slots__ = ("x", "residual", "w", "eps", "gemma", "_h", "_out", "pc", "rinv")
 
     def __init__(self, x: torch.Tensor, residual: torch.Tensor | None, w: torch.Tensor,
-                 eps: float, gemma: bool, pc=None):
+                 eps: float, gemma: bool, pc=None, rinv: torch.Tensor | None = None):
         """``pc``: a ParallelContext when ``x`` is still a tensor-parallel PARTIAL
         sum: materialize() then runs the all-reduce fused with the residual add
-        and the norm (ParallelContext.reduce_norm)."""
+        and the norm (ParallelContext.reduce_norm).  ``rinv``: x is already the
+        residual stream h and rsqrt(mean(h^2) + eps) per row is known (emitted by
+        the producing GEMM's epilogue): a consumer with the norm weight folded
+        into its projection scales its output rows instead of materialising the
+        norm (``ops.gemm.rs_linear``)."""
         self.x, self.residual, self.w, self.eps, self.gemma = x, residual, w, eps, gemma
         self.pc = pc
         self._h: torch.Tensor | None = None
         self._out: torch.Tensor | None = None
+        self.rinv = rinv
+        if rinv is not None:
+            assert residual is None and pc is None
+            self._h = x
 
     def applied(self, h: torch.Tensor) -> None:
         """Record that a fused consumer computed h = x (+ residual)."""
@@ -122,6 +130,8 @@ class PendingNorm:
         token only once its attention has read (and cached) every position."""
         if self._out is not None:
             self._out = self._out.index_select(0, idx)
+        if self.rinv is not None:
+            self.rinv = self.rinv.index_select(0, idx)
         if self._h is not None:  # x is _h (materialize / applied alias them)
             self._h = self.x = self._h.index_select(0, idx)
             return

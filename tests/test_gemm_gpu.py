@@ -246,3 +246,98 @@ def test_decode_with_partials_matches_reference(hipk, monkeypatch):
             if row[tok] < row.max() - 0.05 * max(1.0, row.abs().max().item()):
                 bad.append((i, j))
     assert not bad, bad[:10]
+
+
+# --------------------------------------------------- RMSNorm folded across a prefill layer
+@pytest.mark.parametrize("M,N,K", [(4096, 512, 1024), (4500, 4096, 4096), (4096, 4096, 14336)])
+def test_linear_residual_rinv(hipk, M, N, K):
+    """residual += x @ w.T with the next norm's row statistic: from the gemm_w4 epilogue
+    (partial sums of squares, W4_RESIDUAL_SQ) or, for the library's long-K shape, from one
+    read of the rows; h and rinv against fp32."""
+    from drtc_amd import ops
+
+    g = torch.Generator(device="cuda").manual_seed(M + K)
+    x = torch.randn(M, K, device="cuda", generator=g).to(torch.bfloat16)
+    w = (torch.randn(N, K, device="cuda", generator=g) / K ** 0.5).to(torch.bfloat16)
+    res = torch.randn(M, N, device="cuda", generator=g).to(torch.bfloat16)
+    h_ref = x.float() @ w.float().t() + res.float()
+    h, rinv = ops.linear_residual_rinv(x, w, res, 1e-5)
+    assert h.data_ptr() == res.data_ptr() and rinv is not None and rinv.shape == (M,)
+    assert _rel(h, h_ref) < 1e-2
+    r_ref = torch.rsqrt(h.float().pow(2).mean(-1) + 1e-5)  # of the stored (bf16) stream
+    assert ((rinv - r_ref).abs() / r_ref).max().item() < 1e-4
+
+
+@pytest.mark.parametrize("act", [None, "silu", "gelu_tanh"])
+@pytest.mark.parametrize("gemma", [False, True])
+def test_rs_linear_equals_norm_then_linear(hipk, act, gemma):
+    """(h @ (W diag(g)).T) * rinv[row] (gemm_w4 *_RS epilogues, the norm weight folded into
+    W) equals the projection of the materialised RMSNorm within bf16 rounding."""
+    from drtc_amd import ops
+
+    M, H, N = 4352, 1024, 1536 if act is None else 2048
+    g = torch.Generator(device="cuda").manual_seed(7)
+    h = torch.randn(M, H, device="cuda", generator=g).to(torch.bfloat16)
+    nw = (torch.rand(H, device="cuda", generator=g) * 0.5 + (0.0 if gemma else 0.75)).to(torch.bfloat16)
+    w = (torch.randn(N, H, device="cuda", generator=g) / H ** 0.5).to(torch.bfloat16)
+    gam = nw.float() + (1.0 if gemma else 0.0)
+    w_f = (w.float() * gam[None, :]).to(torch.bfloat16)
+    rinv = torch.rsqrt(h.float().pow(2).mean(-1) + 1e-6)
+    xn = h.float() * rinv[:, None] * gam[None, :]
+    ref = xn @ w.float().t()
+    if act is not None:
+        I = N // 2
+        gt, up = ref[:, :I], ref[:, I:]
+        ref = (torch.nn.functional.silu(gt) if act == "silu"
+               else torch.nn.functional.gelu(gt, approximate="tanh")) * up
+    y = ops.rs_linear(h, w_f, rinv.contiguous(), act)
+    assert y is not None
+    assert _rel(y, ref) < 2e-2
+    # the engine's path: a PendingNorm carrying rinv
+    p = ops.PendingNorm(h, None, nw, 1e-6, gemma, rinv=rinv.contiguous())
+    y2 = ops.norm_linear(p, w, w_f) if act is None else ops.norm_glu(p, w, act, w_f)
+    assert torch.equal(y2, y) and p._out is None and p.stream().data_ptr() == h.data_ptr()
+
+
+def test_prefill_with_folded_norms_matches_reference(hipk, monkeypatch):
+    """A 2-layer model with H = 512 at a 4.4k-token prefill chunk: o / down leave the norm's
+    row statistic, qkv / gate_up run on the residual stream with folded (non-unit) norm
+    weights; logits agree with the unfolded HIP path and with the fp32 reference path."""
+    from drtc_amd import ops
+    from drtc_amd.models import TINY_LLAMA, TransformerLM
+    from drtc_amd.models.transformer import PrefillMeta
+    from drtc_amd.ops import gemm as Gm
+
+    cfg = TINY_LLAMA.replace(hidden_size=512, intermediate_size=1024, num_heads=8,
+                             num_kv_heads=8, head_dim=64, max_position=512)
+    m = TransformerLM(cfg, "cuda", seed=4)
+    g = torch.Generator().manual_seed(5)
+    for L in m.layers:  # non-unit norm weights: the folded copies are real copies
+        L["ln_in"].copy_((torch.rand(512, generator=g) + 0.5).to(torch.bfloat16))
+        L["ln_post"].copy_((torch.rand(512, generator=g) + 0.5).to(torch.bfloat16))
+    m.fold_norm_weights()
+    assert m.layers[0]["qkv_n"].data_ptr() != m.layers[0]["qkv"].data_ptr()
+    lens = [100 + (7 * i) % 60 for i in range(34)]
+    T = sum(lens)
+    assert T >= 4096
+    ids = torch.randint(3, 500, (T,), device="cuda", dtype=torch.int64)
+    cu = [0]
+    for n in lens:
+        cu.append(cu[-1] + n)
+    pos = torch.cat([torch.arange(n) for n in lens]).to(torch.int32).cuda()
+    last = torch.tensor(cu[1:], dtype=torch.int64, device="cuda") - 1
+
+    def run():
+        meta = PrefillMeta(positions=pos, slots=torch.full((T,), -1, dtype=torch.int64, device="cuda"),
+                           cu_seqlens=torch.tensor(cu, dtype=torch.int32, device="cuda"), cu_host=cu,
+                           tiles=None, last_idx=last, max_len=max(lens))
+        return m.forward_prefill(ids, meta, None).float()
+
+    folded = run()
+    monkeypatch.setattr(Gm, "_fold_norm", False)
+    plain = run()
+    with ops.reference_mode():
+        ref = run()
+    scale = max(1.0, ref.abs().max().item())
+    assert (folded - plain).abs().max().item() < 0.03 * scale
+    assert (folded - ref).abs().max().item() < 0.05 * scale
