@@ -106,6 +106,7 @@ def _worker_main(rank: int, device: str, model_name: str, engine_kw: dict, inq, 
     import torch
 
     from ..engine.engine import EngineLoop, LLMEngine, freeze_gc
+    from ..engine.tokenizer import ChatTokenizer
     from ..models import TransformerLM, get_config
 
     try:
@@ -114,6 +115,9 @@ def _worker_main(rank: int, device: str, model_name: str, engine_kw: dict, inq, 
         cfg = get_config(model_name)
         model = TransformerLM(cfg, device, seed=seed, full_then_shard=False)
         eng = LLMEngine(model, seed=rank, **engine_kw)
+        # prompt text is tokenized (and replies detokenized) here, beside the engine, so the
+        # gRPC front-end's single GIL only carries RPC handling (llm/backends.py ReplicaRouter)
+        tok = ChatTokenizer(cfg.vocab_size, cfg.bos_token_id, cfg.eos_token_id)
         eng.warmup(capture=True)
         freeze_gc()  # this process only serves the engine from here on
         loop = EngineLoop(eng).start()
@@ -128,6 +132,7 @@ def _worker_main(rank: int, device: str, model_name: str, engine_kw: dict, inq, 
     # over ~1k requests, 1000 times a second, that held the GIL against the engine's own
     # host work), and ships each burst of completions as ONE queue message
     done_q: queue.SimpleQueue = queue.SimpleQueue()
+    text_rids: set = set()  # requests submitted as prompt text: reply with text as well
 
     def watcher():
         last_hb = 0.0
@@ -148,7 +153,9 @@ def _worker_main(rank: int, device: str, model_name: str, engine_kw: dict, inq, 
                 out = []
                 for r in batch:
                     if pending.pop(r.request_id, None) is not None:
-                        out.append((r.request_id, (r.output_ids, r.finish_reason)))
+                        text = tok.decode(r.output_ids) if r.request_id in text_rids else None
+                        text_rids.discard(r.request_id)
+                        out.append((r.request_id, (r.output_ids, r.finish_reason, text)))
                 if out:
                     outq.put(("done_batch", rank, out))
             if not loop.alive():  # engine fault: exit so the parent evicts/respawns us
@@ -173,6 +180,9 @@ def _worker_main(rank: int, device: str, model_name: str, engine_kw: dict, inq, 
                 eng.abort(r)
             continue
         rid, ids, prm = msg
+        if isinstance(ids, str):  # prompt text: fit + tokenize here (ReplicaRouter)
+            ids = fit_prompt(tok, ids, eng.max_model_len - prm.max_new_tokens - 1)
+            text_rids.add(rid)
         r = Request(ids, prm, request_id=rid, on_done=done_q.put)
         pending[rid] = r
         try:
@@ -322,6 +332,9 @@ class WorkerPool:
             return min(live, key=lambda i: self.load[i])
 
     def submit(self, worker: int, ids, params):
+        """Queue one request on replica ``worker``: ``ids`` are prompt token ids, or the
+        prompt TEXT (a str), which the replica fits to its context and tokenizes itself and
+        answers with the decoded text as well.  Returns (request id, event, result slot)."""
         rid = f"w{worker}-{next(self._ids)}"
         ev, slot = threading.Event(), []
         with self._lock:
@@ -389,12 +402,13 @@ class ReplicaRouter:
         self.pool.close()
 
     def generate(self, prompts, params, timeout=None):
+        # prompts go to the replicas as text: tokenization and detokenization run in the
+        # engine processes, beside their engines, not in this (gRPC front-end) process
         if isinstance(params, SamplingParams):
             params = [params] * len(prompts)
         jobs = []
         for p, prm in zip(prompts, params):
-            ids = fit_prompt(self.tok, p, self.max_model_len - prm.max_new_tokens - 1)
-            jobs.append([ids, prm, self.pool.submit(self.pool.pick(), ids, prm), 0])
+            jobs.append([p, prm, self.pool.submit(self.pool.pick(), p, prm), 0])
         deadline = None if timeout is None else time.monotonic() + timeout
         outs = []
         try:
@@ -406,7 +420,7 @@ class ReplicaRouter:
                         for j in jobs:  # free the replicas' slots and KV blocks
                             self.pool.abort(j[2][0])
                         raise GenerationError("generation timed out")
-                    ids, reason = slot[0]
+                    ids, reason, *text = slot[0]
                     if reason.startswith(WorkerPool.LOST) and job[3] < self.max_redispatch:
                         self.pool.release(rid)
                         job[3] += 1
@@ -414,7 +428,7 @@ class ReplicaRouter:
                         continue
                     if reason.startswith("error"):
                         raise GenerationError(reason)
-                    outs.append(self.tok.decode(ids))
+                    outs.append(text[0] if text and text[0] is not None else self.tok.decode(ids))
                     break
         finally:
             for job in jobs:

@@ -282,7 +282,8 @@ class TransformerLM:
             gu = ops.norm_linear(x, L["gate_up"])
             res = self._fusable_residual(gu, x)
             if res is not None:
-                return ops.linear_residual(ops.act_glu(gu, self.cfg.act), L["down"], res), True
+                return ops.linear_residual_rinv(ops.act_glu(gu, self.cfg.act), L["down"], res,
+                                                self.cfg.rms_eps), True
             y = ops.glu_linear(gu, L["down"], self.cfg.act)
         if decode and self.pc.tp_size > 1:
             return y, False, True  # reduced by the next norm (fused all-reduce + add + norm)

@@ -456,7 +456,12 @@ def gemm_w4_variant(variant: int) -> bool:
 
 
 # ------------------------------------------------------------ folded RMSNorm (prefill)
-_fold_norm = os.environ.get("DRTC_FOLD_NORM", "1") != "0"
+# Opt-in (DRTC_FOLD_NORM=1): measured 1.1 % SLOWER on the headline than materialising the
+# norm (profiles/r3m: 19,575 / 19,553 vs 19,795 / 19,776 tok/s, one box, temporal stores for
+# the residual stream) - the row statistic (epilogue shuffles + a row-statistic pass for the
+# library's down) and the consumers' reads of the un-normalised stream cost more than the
+# 41 us norm pass they replace.
+_fold_norm = os.environ.get("DRTC_FOLD_NORM", "0") == "1"
 
 
 def linear_residual_rinv(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor, eps: float):
@@ -477,7 +482,9 @@ def linear_residual_rinv(x: torch.Tensor, w: torch.Tensor, residual: torch.Tenso
                               stream_ptr(x)), "row_rinv")
         return h, rinv
     sq = torch.empty((M, N // 128), dtype=torch.float32, device=x.device)
-    mfma_gemm(x, w, "residual_sq", residual=residual, out=residual, variant=W4_VARIANT,
+    # plain (temporal) stores: the next GEMM reads h itself, so h should stay in the MALL
+    # (the non-temporal default would send the consumer's first pass to HBM)
+    mfma_gemm(x, w, "residual_sq", residual=residual, out=residual, variant=W4_VARIANT + 2,
               group_m=w4_group_m(M, N, K), side=sq)
     check(hipk().rowsq_rinv(rinv.data_ptr(), sq.data_ptr(), M, N // 128, N, float(eps),
                             stream_ptr(x)), "rowsq_rinv")

@@ -250,11 +250,14 @@ def test_decode_with_partials_matches_reference(hipk, monkeypatch):
 
 # --------------------------------------------------- RMSNorm folded across a prefill layer
 @pytest.mark.parametrize("M,N,K", [(4096, 512, 1024), (4500, 4096, 4096), (4096, 4096, 14336)])
-def test_linear_residual_rinv(hipk, M, N, K):
+def test_linear_residual_rinv(hipk, monkeypatch, M, N, K):
     """residual += x @ w.T with the next norm's row statistic: from the gemm_w4 epilogue
     (partial sums of squares, W4_RESIDUAL_SQ) or, for the library's long-K shape, from one
     read of the rows; h and rinv against fp32."""
     from drtc_amd import ops
+    from drtc_amd.ops import gemm as Gm
+
+    monkeypatch.setattr(Gm, "_fold_norm", True)
 
     g = torch.Generator(device="cuda").manual_seed(M + K)
     x = torch.randn(M, K, device="cuda", generator=g).to(torch.bfloat16)
@@ -333,6 +336,7 @@ def test_prefill_with_folded_norms_matches_reference(hipk, monkeypatch):
                            tiles=None, last_idx=last, max_len=max(lens))
         return m.forward_prefill(ids, meta, None).float()
 
+    monkeypatch.setattr(Gm, "_fold_norm", True)
     folded = run()
     monkeypatch.setattr(Gm, "_fold_norm", False)
     plain = run()
