@@ -523,7 +523,7 @@ __global__ __launch_bounds__(256, D >= 256 ? 1 : 2) void paged_decode_persist_ke
   const int64_t blk_elems = (int64_t)kBS * D;
 
   struct Item {
-    int it, b, h, ctx, begin, end, nparts;
+    int it, b, h, ctx, begin, end, nparts, pos;  // pos: the step token's position (ROPE)
   };
   // first item >= it (stride W) with work; padded sequences get their zeros
   auto next_item = [&](int it) -> Item {
@@ -545,9 +545,12 @@ __global__ __launch_bounds__(256, D >= 256 ? 1 : 2) void paged_decode_persist_ke
       const int nparts = (nblk + blocks_per_part - 1) / blocks_per_part;
       if (p >= nparts) continue;
       const int begin = p * blocks_per_part;
-      return Item{it, b, h, ctx, begin, min(nblk, begin + blocks_per_part), nparts};
+      // ROPE: the position is read here, one item ahead of its use (the rotation at the
+      // item's start then waits for the cos / sin rows only)
+      const int pos = ROPE ? __builtin_amdgcn_readfirstlane(rope.positions[b]) : 0;
+      return Item{it, b, h, ctx, begin, min(nblk, begin + blocks_per_part), nparts, pos};
     }
-    return Item{n_items, 0, 0, 0, 0, 0, 0};
+    return Item{n_items, 0, 0, 0, 0, 0, 0, 0};
   };
   auto load_q = [&](bf16x8* qf, const Item& A) {
     const bf16_t* qrow = q + (int64_t)A.b * q_stride + (int64_t)(A.h * G + col) * D;
@@ -569,7 +572,7 @@ __global__ __launch_bounds__(256, D >= 256 ? 1 : 2) void paged_decode_persist_ke
   };
   auto rope_q = [&](bf16x8* qf, const Item& A) {
     if constexpr (ROPE)
-      rope_frags<D>(qf, rope.cos_sin, __builtin_amdgcn_readfirstlane(rope.positions[A.b]), g);
+      rope_frags<D>(qf, rope.cos_sin, A.pos, g);
   };
 
   Item A = next_item(blockIdx.x * 4 + wave_id_uniform());
@@ -596,7 +599,7 @@ __global__ __launch_bounds__(256, D >= 256 ? 1 : 2) void paged_decode_persist_ke
         bf16x8 kf[KS];
 #pragma unroll
         for (int s = 0; s < KS; ++s) kf[s] = load_bf16x8(kn + 32 * s + 8 * g);
-        rope_frags<D>(kf, rope.cos_sin, __builtin_amdgcn_readfirstlane(rope.positions[A.b]), g);
+        rope_frags<D>(kf, rope.cos_sin, A.pos, g);
         float dot = 0.f;
 #pragma unroll
         for (int s = 0; s < KS; ++s)
