@@ -759,8 +759,12 @@ class EngineLoop:
                 if self.engine.has_work():
                     self.engine.step()
                 else:
+                    # idle time (no request anywhere in the engine), reported in the
+                    # engine counters: a closed-loop service shows its per-wave turnaround here
+                    t0 = time.perf_counter()
                     self._wake.wait(0.05)
                     self._wake.clear()
+                    self.engine.stats["idle_ms"] += int(1000 * (time.perf_counter() - t0))
         except BaseException as e:  # surface engine faults to callers
             self.error = e
             with self.engine.lock:

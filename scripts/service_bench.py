@@ -165,6 +165,17 @@ def run_open_loop(target, n_requests: int, rate: float, seed: int):
     return lat, errors, t_start, time.time(), []
 
 
+def _delta(before, pool):
+    """Per-replica counter increments since ``before`` (WorkerPool.health() snapshots)."""
+    time.sleep(2 * pool.hb_interval)
+    out = []
+    for b, a in zip(before, pool.health()):
+        out.append({k: a[k] - b.get(k, 0) for k in ("idle_ms", "prefill_steps", "prefill_tokens",
+                                                   "decode_steps", "mixed_steps", "decode_tokens")
+                    if isinstance(a.get(k), int)})
+    return out
+
+
 def _client_main(target, n_requests, threads, seed, q):
     q.put(run_load(target, n_requests, threads, seed))
 
@@ -212,6 +223,10 @@ def main():
         if eng is not None:
             eng.stats.clear()
         METRICS.reset()
+        pool = getattr(backend, "pool", None)
+        if pool is not None:  # replica counters arrive with the heartbeats
+            time.sleep(2 * pool.hb_interval)
+        rs0 = pool.health() if pool is not None else None
         if args.arrival_rate > 0:
             lat, errors, t_s, t_e, fin = run_open_loop(target, args.requests, args.arrival_rate, 1)
             dt = t_e - t_s
@@ -264,6 +279,9 @@ def main():
             "p50_latency_ms": round(1000 * statistics.median(lat), 1),
             "p99_latency_ms": round(1000 * lat[min(len(lat) - 1, int(0.99 * (len(lat) - 1)))], 1),
             "engine_stats": dict(eng.stats) if eng else None,
+            # pool mode: the replicas' counters over the run (idle_ms: time the engine had no
+            # request at all - the closed loop's per-wave turnaround)
+            "replica_delta": _delta(rs0, pool) if pool is not None else None,
             "rpc_metrics": {k: v for k, v in METRICS.snapshot()["histograms"].items()
                             if "SmartReply" in k or k.startswith("engine.")},
         }
