@@ -46,6 +46,7 @@
 #include <utility>
 
 namespace drtc {
+int w4_num_cus();
 namespace {
 
 typedef __attribute__((address_space(3))) void* w4_lds_ptr;
@@ -131,7 +132,7 @@ DRTC_DEVICE bf16x8 w4_rd(const char* lds, int off) {
 }
 
 // Per-wave DMA plan: A rows of instruction i are 32 i + 8 wv + (lane >> 3) of the tile
-// (clamped to the last valid row: one VGPR offset per instruction), B rows 32 i / 16 i
+// (rows past M lie outside the descriptor range: read as 0, never stored), B rows 32 i / 16 i
 // (gated) apart (one VGPR offset + scalar steps).
 struct W4Dma {
   __amdgpu_buffer_rsrc_t ra, rb;
@@ -141,6 +142,8 @@ struct W4Dma {
   unsigned lds_a, lds_b;  // LDS byte address of this wave's first block in stage 0
   const char* abase;      // operand bases (lean form: descriptors rebuilt per tile)
   const char* bbase;
+  unsigned na;            // bytes of this tile's valid A rows from abase: DMA rows past M
+                          // are out of the descriptor's range (read as 0, never stored)
 };
 
 // Per-tile state handed to every step of the unrolled schedule.
@@ -150,6 +153,8 @@ struct W4Tile {
   int ra0, ra1, rb0, rb1;
   unsigned kb;         // K byte offset of tile t + 2 (its DMA goes into stage `cur`)
   __amdgpu_buffer_rsrc_t rak, rbk;  // lean form: descriptors based at K byte kb
+  bool seam;           // persistent step 0 after a full tile's epilogue (its 32 stores are
+                       // younger than the DMA this step waits for)
 };
 
 // Step Q (0..127) of a K tile: MFMA Q, then the memory work scheduled behind it.  Every
@@ -167,11 +172,13 @@ struct W4Tile {
 //   V & 2  plain (temporal) epilogue stores instead of non-temporal ones
 //   V & 4  reduce-scatter split-K (w4_splitk_rs: every slice finishes part of the tile,
 //          all workgroups resident) instead of the last-arriver combine
-template <int V, bool DMA, bool NEXT, int Q>
+template <int V, bool DMA, bool NEXT, bool Z, int Q>
 DRTC_DEVICE void w4_step(f32x4 (&acc)[8][8], bf16x8 (&fa0)[8], bf16x8 (&fb0)[8],
                          bf16x8 (&fa1)[8], bf16x8 (&fb1)[8], const W4Tile& T, const W4Dma& d) {
   constexpr int i = (Q >> 3) & 7, j = Q & 7;
-  if constexpr (Q < 64)
+  if constexpr (Q < 64 && Z)  // first K tile of a persistent tile: accumulate onto 0
+    acc[i][j] = mfma16(fa0[i], fb0[j], (f32x4){0.f, 0.f, 0.f, 0.f});
+  else if constexpr (Q < 64)
     acc[i][j] = mfma16(fa0[i], fb0[j], acc[i][j]);
   else
     acc[i][j] = mfma16(fa1[i], fb1[j], acc[i][j]);
@@ -230,10 +237,18 @@ DRTC_DEVICE void w4_step(f32x4 (&acc)[8][8], bf16x8 (&fa0)[8], bf16x8 (&fb0)[8],
   // half-0 fragments: fa0[0], fb0[0..7], fa0[1..7]
   constexpr int qn = 103;
   if constexpr (NEXT && Q == qn) {
-    if constexpr (DMA)
+    if constexpr (DMA && Z) {
+      // first K step of a persistent tile: the previous tile's epilogue stores sit between
+      // the DMA of K step 1 (needed now) and this step's DMA - do not wait for them
+      if (T.seam)
+        w4_vmcnt<48>();
+      else
+        w4_vmcnt<16>();
+    } else if constexpr (DMA) {
       w4_vmcnt<16>();
-    else
+    } else {
       w4_vmcnt<0>();
+    }
     w4_barrier();
   }
   if constexpr (NEXT && Q > qn && Q <= qn + 16) {
@@ -248,23 +263,24 @@ DRTC_DEVICE void w4_step(f32x4 (&acc)[8][8], bf16x8 (&fa0)[8], bf16x8 (&fb0)[8],
   __builtin_amdgcn_sched_barrier(0);
 }
 
-template <int V, bool DMA, bool NEXT, int... Qs>
+template <int V, bool DMA, bool NEXT, bool Z, int... Qs>
 DRTC_DEVICE void w4_steps(std::integer_sequence<int, Qs...>, f32x4 (&acc)[8][8],
                           bf16x8 (&fa0)[8], bf16x8 (&fb0)[8], bf16x8 (&fa1)[8],
                           bf16x8 (&fb1)[8], const W4Tile& T, const W4Dma& d) {
-  (w4_step<V, DMA, NEXT, Qs>(acc, fa0, fb0, fa1, fb1, T, d), ...);
+  (w4_step<V, DMA, NEXT, Z, Qs>(acc, fa0, fb0, fa1, fb1, T, d), ...);
 }
 
-template <int V, bool DMA, bool NEXT>
+template <int V, bool DMA, bool NEXT, bool Z = false>
 DRTC_DEVICE void w4_tile(f32x4 (&acc)[8][8], bf16x8 (&fa0)[8], bf16x8 (&fb0)[8],
                          bf16x8 (&fa1)[8], bf16x8 (&fb1)[8], const char* lds, int cur, int ra0,
-                         int ra1, int rb0, int rb1, const W4Dma& d, int t2) {
+                         int ra1, int rb0, int rb1, const W4Dma& d, int t2, bool seam = false) {
   W4Tile T{lds, cur, kW4Stage - cur, ra0, ra1, rb0, rb1, (unsigned)t2 * 128u};
-  T.rak = __builtin_amdgcn_make_buffer_rsrc((void*)(d.abase + T.kb), (short)0, 0x7FFFFFFF,
+  T.seam = seam;
+  T.rak = __builtin_amdgcn_make_buffer_rsrc((void*)(d.abase + T.kb), (short)0, (int)(d.na - T.kb),
                                             0x00020000);
   T.rbk = __builtin_amdgcn_make_buffer_rsrc((void*)(d.bbase + T.kb), (short)0, 0x7FFFFFFF,
                                             0x00020000);
-  w4_steps<V, DMA, NEXT>(std::make_integer_sequence<int, 128>{}, acc, fa0, fb0, fa1, fb1, T, d);
+  w4_steps<V, DMA, NEXT, Z>(std::make_integer_sequence<int, 128>{}, acc, fa0, fb0, fa1, fb1, T, d);
 }
 
 // acc[i][j][r] = C[row 128 wm + 16 i + 4 g + r][column of B fragment j, row l16]: lane l16
@@ -550,21 +566,86 @@ DRTC_DEVICE void w4_splitk_rs(const W4Params& p, f32x4 (&acc)[8][8], int tile, i
   }
 }
 
+// Tile coordinates of tile-order index tt (row-grouped: group_m row tiles sweep the columns).
+DRTC_DEVICE void w4_tile_of(const W4Params& p, int tt, int& tm, int& tn) {
+  const int gsize = p.group_m * p.tiles_n;
+  const int first_m = (tt / gsize) * p.group_m;
+  const int gm = min(p.tiles_m - first_m, p.group_m);
+  tm = first_m + (tt % gsize) % gm;
+  tn = (tt % gsize) / gm;
+}
+
+// DMA plan of tile (tm, tn) for this wave (operand bases, per-lane source offsets).
+template <int EPI>
+DRTC_DEVICE void w4_plan(W4Dma& d, const W4Params& p, int tm, int tn, int wv, int lane,
+                         int k_base, unsigned lds0) {
+  const int r8 = lane >> 3;
+  const int chunk = (lane & 7) ^ ((4 * wv + (lane >> 4)) & 7);  // logical chunk of this lane
+  const int rows_a = min(256, p.M - 256 * tm);
+  const bf16_t* abase = p.a + (int64_t)(256 * tm) * p.lda + k_base;
+  d.na = (unsigned)(rows_a * p.lda * 2 - k_base * 2);
+  d.ra = __builtin_amdgcn_make_buffer_rsrc((void*)abase, (short)0, (int)d.na, 0x00020000);
+  // tile-independent lane offsets: rows past the tile's valid rows fall outside `na`
+#pragma unroll
+  for (int s = 0; s < 8; ++s)
+    d.va[s] = (unsigned)((32 * s + 8 * wv + r8) * p.lda * 2 + chunk * 16);
+  // B: fragment j of wave column half h reads LDS rows 128 h + 8 l + j (l = lane & 15),
+  // so lane l16 of the MFMA output holds the 8 CONSECUTIVE columns 8 l16 .. 8 l16 + 7 over
+  // j = 0..7 (16-B epilogue stores).  Plain tiles keep tile row = LDS row.  Gated tiles:
+  // 64 output columns per half, LDS row 128 h + 8 l + j holds the gate row (j < 4) or the
+  // up row (j >= 4) of column 64 h + 4 l + (j & 3): each DMA instruction (8 LDS rows) loads
+  // 4 consecutive gate rows and the 4 matching up rows.  DMA instruction s of wave wv fills
+  // LDS rows 32 s + 8 wv + r8: h = s >> 2, l = 4 (s & 3) + wv, j = r8.
+  const bf16_t* bbase;
+  int brow;
+  if constexpr (w4_glu<EPI>()) {
+    bbase = p.b + (int64_t)(128 * tn) * p.ldb + k_base;
+    brow = 4 * wv + (r8 & 3) + (r8 >= 4 ? p.up_off : 0);
+#pragma unroll
+    for (int s = 0; s < 8; ++s)
+      d.sb[s] = (unsigned)((64 * (s >> 2) + 16 * (s & 3)) * p.ldb * 2);
+  } else {
+    bbase = p.b + (int64_t)(256 * tn) * p.ldb + k_base;
+    brow = 8 * wv + r8;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) d.sb[s] = (unsigned)(32 * s * p.ldb * 2);
+  }
+  d.rb = __builtin_amdgcn_make_buffer_rsrc((void*)bbase, (short)0, 0x7FFFFFFF, 0x00020000);
+  d.abase = reinterpret_cast<const char*>(abase);
+  d.bbase = reinterpret_cast<const char*>(bbase);
+  d.vb = (unsigned)(brow * p.ldb * 2 + (lane & 7) * 16);  // B: chunks in natural order
+  d.lds_a = __builtin_amdgcn_readfirstlane(lds0 + 8 * wv * 128);
+  d.lds_b = __builtin_amdgcn_readfirstlane(lds0 + kW4BOff + wv * kW4BBlk);
+}
+
+// Select of two DMA plans on a wave-uniform condition: only the operand bases and the valid-A
+// extent depend on the tile (lane offsets, B row steps and LDS bases do not; the prologue-only
+// descriptors are not used by the main loop), so the pick is scalar.
+DRTC_DEVICE W4Dma w4_pick(bool first, const W4Dma& x, const W4Dma& y) {
+  W4Dma r = x;
+  r.abase = first ? x.abase : y.abase;
+  r.bbase = first ? x.bbase : y.bbase;
+  r.na = first ? x.na : y.na;
+  return r;
+}
+
+// V & 8: persistent form (split-K 1 only).  min(tiles, CUs) workgroups walk the tile order
+// (tile tt, tt + grid, ...), and the last two K steps of a tile DMA the NEXT tile's first two
+// K tiles into the ring (and the last one reads its first fragments), so a tile seam costs the
+// epilogue only: no workgroup launch, no prologue latency, no drain of the DMA ring.
 template <int EPI, int V>
 __global__ __launch_bounds__(kW4Threads, 1) void gemm_w4_kernel(W4Params p) {
   extern __shared__ __attribute__((aligned(16))) char w4_lds[];
+  constexpr bool kPers = (V & 8) != 0;
   // ---- tile assignment: XCD remap (bijective), split-K slice fastest, grouped rows
   const int nwg = gridDim.x, orig = blockIdx.x;
   const int xcd = orig & 7, qq = nwg >> 3, rmd = nwg & 7;
   const int wgid = (xcd < rmd ? xcd * (qq + 1) : rmd * (qq + 1) + (xcd - rmd) * qq) + (orig >> 3);
-  const int slice = wgid % p.splitk;
-  const int tt = wgid / p.splitk;
-  const int gsize = p.group_m * p.tiles_n;
-  const int first_m = (tt / gsize) * p.group_m;
-  const int gm = min(p.tiles_m - first_m, p.group_m);
-  const int tm = first_m + (tt % gsize) % gm;
-  const int tn = (tt % gsize) / gm;
-  const int tile = tm * p.tiles_n + tn;
+  const int slice = kPers ? 0 : wgid % p.splitk;
+  int tt = kPers ? wgid : wgid / p.splitk;
+  const int ntiles = p.tiles_m * p.tiles_n;
+  int tm, tn;
+  w4_tile_of(p, tt, tm, tn);
 
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -575,45 +656,7 @@ __global__ __launch_bounds__(kW4Threads, 1) void gemm_w4_kernel(W4Params p) {
   // ---- DMA plan
   W4Dma d;
   const unsigned lds0 = (unsigned)(uintptr_t)(w4_lds_ptr)w4_lds;
-  {
-    const int r8 = lane >> 3;
-    const int chunk = (lane & 7) ^ ((4 * wv + (lane >> 4)) & 7);  // logical chunk of this lane
-    const int rows_a = min(256, p.M - 256 * tm);
-    const bf16_t* abase = p.a + (int64_t)(256 * tm) * p.lda + k_base;
-    d.ra = __builtin_amdgcn_make_buffer_rsrc((void*)abase, (short)0, 0x7FFFFFFF, 0x00020000);
-#pragma unroll
-    for (int s = 0; s < 8; ++s) {
-      const int row = min(32 * s + 8 * wv + r8, rows_a - 1);
-      d.va[s] = (unsigned)(row * p.lda * 2 + chunk * 16);
-    }
-    // B: fragment j of wave column half h reads LDS rows 128 h + 8 l + j (l = lane & 15),
-    // so lane l16 of the MFMA output holds the 8 CONSECUTIVE columns 8 l16 .. 8 l16 + 7 over
-    // j = 0..7 (16-B epilogue stores).  Plain tiles keep tile row = LDS row.  Gated tiles:
-    // 64 output columns per half, LDS row 128 h + 8 l + j holds the gate row (j < 4) or the
-    // up row (j >= 4) of column 64 h + 4 l + (j & 3): each DMA instruction (8 LDS rows) loads
-    // 4 consecutive gate rows and the 4 matching up rows.  DMA instruction s of wave wv fills
-    // LDS rows 32 s + 8 wv + r8: h = s >> 2, l = 4 (s & 3) + wv, j = r8.
-    const bf16_t* bbase;
-    int brow;
-    if constexpr (w4_glu<EPI>()) {
-      bbase = p.b + (int64_t)(128 * tn) * p.ldb + k_base;
-      brow = 4 * wv + (r8 & 3) + (r8 >= 4 ? p.up_off : 0);
-#pragma unroll
-      for (int s = 0; s < 8; ++s)
-        d.sb[s] = (unsigned)((64 * (s >> 2) + 16 * (s & 3)) * p.ldb * 2);
-    } else {
-      bbase = p.b + (int64_t)(256 * tn) * p.ldb + k_base;
-      brow = 8 * wv + r8;
-#pragma unroll
-      for (int s = 0; s < 8; ++s) d.sb[s] = (unsigned)(32 * s * p.ldb * 2);
-    }
-    d.rb = __builtin_amdgcn_make_buffer_rsrc((void*)bbase, (short)0, 0x7FFFFFFF, 0x00020000);
-    d.abase = reinterpret_cast<const char*>(abase);
-    d.bbase = reinterpret_cast<const char*>(bbase);
-    d.vb = (unsigned)(brow * p.ldb * 2 + (lane & 7) * 16);  // B: chunks in natural order
-    d.lds_a = __builtin_amdgcn_readfirstlane(lds0 + 8 * wv * 128);
-    d.lds_b = __builtin_amdgcn_readfirstlane(lds0 + kW4BOff + wv * kW4BBlk);
-  }
+  w4_plan<EPI>(d, p, tm, tn, wv, lane, k_base, lds0);
   // fragment read offsets (bytes within a stage): row 128 w + l16 (+ 16 per fragment), the
   // 16-B chunk 4 h + g stored at chunk ^ ((row >> 1) & 7)
   const int fx = (l16 >> 1) & 7;
@@ -655,6 +698,57 @@ __global__ __launch_bounds__(kW4Threads, 1) void gemm_w4_kernel(W4Params p) {
 #pragma unroll
   for (int i = 1; i < 8; ++i) fa0[i] = w4_rd(lds, ra0 + 2048 * i);
 
+  if constexpr (kPers) {
+    // the persistent seam needs two K tiles per tile (the next tile's pair is staged by
+    // this tile's last two steps); the launcher guarantees nk >= 2
+    int par = 0;  // stage parity of this tile's K step 0 (flips after an odd nk)
+    // exactly 32 store instructions per wave in a full tile's epilogue (one per row fragment
+    // i and row r; STORE / RESIDUAL 16 B, GLU 8 B): checked in the disassembly
+    constexpr bool kSeamOk = EPI == W4_STORE || EPI == W4_RESIDUAL || EPI == W4_SILU || EPI == W4_GELU;
+    bool seam = false;
+    for (;;) {
+      const int tnext = tt + nwg;
+      const bool more = tnext < ntiles;
+      int tm2 = tm, tn2 = tn;
+      if (more) w4_tile_of(p, tnext, tm2, tn2);
+      W4Dma dn;
+      w4_plan<EPI>(dn, p, tm2, tn2, wv, lane, 0, lds0);
+      // K step t + 2 of this tile, or step t + 2 - nk of the next one; the very last tile
+      // re-stages its final K tile (valid bytes, never read) as the plain form does.  Step 0
+      // starts the accumulators from 0 (MFMA with a zero C operand: no separate zeroing of the
+      // 256 AGPRs, which hipcc would hoist above the previous tile's epilogue and spill).
+      {
+        const int t2 = 2 < nk ? 2 : (more ? 2 - nk : nk - 1);
+        const W4Dma dd = w4_pick(2 < nk || !more, d, dn);
+        w4_tile<V, true, true, true>(acc, fa0, fb0, fa1, fb1, lds, (par & 1) * kW4Stage, ra0, ra1,
+                                     rb0, rb1, dd, t2, seam);
+      }
+      for (int t = 1; t < nk; ++t) {
+        const bool own = t + 2 < nk;
+        const int t2 = own ? t + 2 : (more ? t + 2 - nk : nk - 1);
+        const W4Dma dd = w4_pick(own || !more, d, dn);
+        w4_tile<V, true, true>(acc, fa0, fb0, fa1, fb1, lds, ((t + par) & 1) * kW4Stage, ra0, ra1,
+                               rb0, rb1, dd, t2);
+      }
+      // one epilogue call site (two would make hipcc copy all 256 accumulators out of the
+      // AGPRs ahead of the branch between them, and spill)
+      if (!more) w4_vmcnt<0>();  // no LDS-DMA may still be landing when the workgroup leaves
+      // the lane index re-derived here (opaque to hipcc): kept live across the K loop it is
+      // spilled, and its reload's vmcnt(0) would wait for the next tile's DMA
+      int ln;
+      asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
+      w4_epilogue<EPI, V>(p, acc, tm, tn, wm, wn, ln & 15, ln >> 4, 0);
+      if (!more) break;
+      seam = kSeamOk && 256 * tm + 256 <= p.M;
+      par ^= nk & 1;
+      tt = tnext;
+      tm = tm2;
+      tn = tn2;
+      d = dn;
+    }
+    return;
+  }
+
   // One loop body for every tile (a single straight-line schedule keeps the 256 accumulators
   // in place in the AGPRs): the last two tiles re-stage the final tile (kb clamped: valid
   // bytes, never read) and the last one reads stale fragments it never uses.
@@ -666,6 +760,7 @@ __global__ __launch_bounds__(kW4Threads, 1) void gemm_w4_kernel(W4Params p) {
   }
   w4_vmcnt<0>();  // no LDS-DMA may still be landing when the workgroup leaves
 
+  const int tile = tm * p.tiles_n + tn;
   if constexpr (EPI == W4_PARTIAL) {
     // every slice stores its own plane: no combine here
   } else if constexpr ((V & 4) != 0) {
@@ -683,10 +778,12 @@ __global__ __launch_bounds__(kW4Threads, 1) void gemm_w4_kernel(W4Params p) {
 
 template <int EPI, int V>
 int w4_launch_v(const W4Params& p, hipStream_t st) {
-  const int nwg = p.tiles_m * p.tiles_n * p.splitk;
+  int nwg = p.tiles_m * p.tiles_n * p.splitk;
+  if constexpr ((V & 8) != 0) nwg = min(nwg, w4_num_cus());
   hipLaunchKernelGGL((gemm_w4_kernel<EPI, V>), dim3(nwg), dim3(kW4Threads), kW4Lds, st, p);
   return (int)hipGetLastError();
 }
+
 
 template <int EPI>
 int w4_launch(const W4Params& p, int v, hipStream_t st) {
@@ -699,6 +796,7 @@ int w4_launch(const W4Params& p, int v, hipStream_t st) {
     case 5: return w4_launch_v<EPI, 5>(p, st);
     case 6: return w4_launch_v<EPI, 6>(p, st);
     case 7: return w4_launch_v<EPI, 7>(p, st);
+    case 8: return w4_launch_v<EPI, 8>(p, st);
     default: return -1;
   }
 }
@@ -712,7 +810,7 @@ template <int EPI>
 int w4_cfg() {
   return w4_cfg_one<EPI, 0>() | w4_cfg_one<EPI, 1>() | w4_cfg_one<EPI, 2>() |
          w4_cfg_one<EPI, 3>() | w4_cfg_one<EPI, 4>() | w4_cfg_one<EPI, 5>() |
-         w4_cfg_one<EPI, 6>() | w4_cfg_one<EPI, 7>();
+         w4_cfg_one<EPI, 6>() | w4_cfg_one<EPI, 7>() | w4_cfg_one<EPI, 8>();
 }
 
 }  // namespace
@@ -762,6 +860,8 @@ int launch_gemm_w4(void* c, const void* a, const void* b, const void* r, int M, 
     return w4_launch<W4_PARTIAL>(p, v, st);
   }
   if (glu ? (N % 128 || up_off != N) : (N % 256)) return -1;
+  // persistent form (v & 8): one slice, and two K tiles per tile for the cross-tile prefetch
+  if ((v & 8) && (v != 8 || splitk != 1 || K / 64 < 2)) return -1;
   if (lda % 8 || ldb % 8 || (glu ? ldc % 4 : ldc % 8)) return -1;
   if (res && (ldr % 8 || r == nullptr || (uintptr_t)r % 16)) return -1;
   if ((uintptr_t)a % 16 || (uintptr_t)b % 16 || (uintptr_t)c % (glu ? 8 : 16)) return -1;

@@ -123,7 +123,7 @@ int launch_gemm(void* c, const void* a, const void* b, const void* r, int M, int
                 hipStream_t st);
 int64_t gemm_workspace_bytes(int64_t M, int64_t N, int splitk);
 // 4-wave hand-scheduled GEMM (gemm_w4.hip): same contract as launch_gemm (gated: up_off == N);
-// launch_gemm variants 7..14 route here (schedule variant v = variant - 7).  Split-K slabs:
+// launch_gemm variants 7..15 route here (schedule variant v = variant - 7; 15 = persistent).  Split-K slabs:
 // 256 KiB per tile and slice.
 int launch_gemm_w4(void* c, const void* a, const void* b, const void* r, int M, int N, int K,
                    int lda, int ldb, int ldc, int ldr, int epi, int up_off, int splitk,

@@ -452,7 +452,7 @@ def save_entries(entries: dict[str, dict], path: str | None = None) -> str:
 
 
 def gemm_w4_variant(variant: int) -> bool:
-    return 7 <= variant <= 14
+    return 7 <= variant <= 15
 
 
 # ------------------------------------------------------------ folded RMSNorm (prefill)

@@ -345,3 +345,39 @@ def test_prefill_with_folded_norms_matches_reference(hipk, monkeypatch):
     scale = max(1.0, ref.abs().max().item())
     assert (folded - plain).abs().max().item() < 0.03 * scale
     assert (folded - ref).abs().max().item() < 0.05 * scale
+
+
+# ------------------------------------------------------ gemm_w4 persistent form (variant 15)
+@pytest.mark.parametrize("epi", ["store", "residual", "silu", "gelu_tanh"])
+@pytest.mark.parametrize("M,N,K", [(8192, 8192, 128), (4500, 4096, 576), (2300, 8192, 192),
+                                   (300, 512, 512), (1, 768, 1024)])
+def test_w4_persistent_matches_fp32(hipk, epi, M, N, K):
+    """Persistent gemm_w4: min(tiles, CUs) workgroups walk the tile order and each tile's
+    last two K steps stage the next tile's first two (odd and even K-tile counts, a partial
+    last row tile, several tiles per workgroup, in-place residual)."""
+    g = torch.Generator(device="cuda").manual_seed(M + 3 * N + 7 * K)
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16, generator=g)
+    w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16, generator=g) * 0.05
+    nout = N // 2 if epi in ("silu", "gelu_tanh") else N
+    res = torch.randn(M, nout, device="cuda", dtype=torch.bfloat16, generator=g) if epi == "residual" else None
+    ref = _ref(x, w, epi, res)
+    if epi == "residual":
+        out = G.mfma_gemm(x, w, epi, residual=res, out=res, variant=15)
+        assert out.data_ptr() == res.data_ptr()
+    else:
+        out = G.mfma_gemm(x, w, epi, variant=15)
+    _check(out, ref)
+    # the same call on the per-tile form agrees bit for bit (same MFMA order per tile)
+    if epi != "residual":
+        _check(out, G.mfma_gemm(x, w, epi, variant=7).float(), tol=1e-6)
+
+
+def test_w4_persistent_rejects_single_k_tile_and_splitk(hipk):
+    x = torch.randn(512, 64, device="cuda", dtype=torch.bfloat16)
+    w = torch.randn(256, 64, device="cuda", dtype=torch.bfloat16)
+    with pytest.raises(RuntimeError):
+        G.mfma_gemm(x, w, variant=15)  # one K tile: nothing to prefetch across the seam
+    x = torch.randn(512, 512, device="cuda", dtype=torch.bfloat16)
+    w = torch.randn(256, 512, device="cuda", dtype=torch.bfloat16)
+    with pytest.raises(RuntimeError):
+        G.mfma_gemm(x, w, variant=15, splitk=2)
