@@ -331,12 +331,13 @@ class WorkerPool:
                 raise GenerationError("no healthy engine replica")
             return min(live, key=lambda i: self.load[i])
 
-    def submit(self, worker: int, ids, params):
+    def submit(self, worker: int, ids, params, ev=None):
         """Queue one request on replica ``worker``: ``ids`` are prompt token ids, or the
         prompt TEXT (a str), which the replica fits to its context and tokenizes itself and
-        answers with the decoded text as well.  Returns (request id, event, result slot)."""
+        answers with the decoded text as well.  Returns (request id, event, result slot);
+        ``ev`` (anything with ``set()``, e.g. a _LoopEvent) replaces the threading.Event."""
         rid = f"w{worker}-{next(self._ids)}"
-        ev, slot = threading.Event(), []
+        ev, slot = (ev if ev is not None else threading.Event()), []
         with self._lock:
             self.futures[rid] = (ev, slot, worker)
             self.load[worker] += 1
@@ -434,6 +435,61 @@ class ReplicaRouter:
             for job in jobs:
                 self.pool.release(job[2][0])
         return outs
+
+    async def agenerate(self, prompt, params, timeout=None):
+        """ReplicaRouter.generate for one prompt as a coroutine (same re-dispatch on a lost
+        replica, same abort on timeout), without a thread blocked per request."""
+        import asyncio
+
+        loop = asyncio.get_running_loop()
+        pool = self.pool
+        deadline = None if timeout is None else time.monotonic() + timeout
+        job = pool.submit(pool.pick(), prompt, params, ev=_LoopEvent(loop))
+        tries = 0
+        try:
+            while True:
+                rid, ev, slot = job
+                left = None if deadline is None else max(0.0, deadline - time.monotonic())
+                try:
+                    await asyncio.wait_for(ev.fut, left)
+                except asyncio.TimeoutError:
+                    pool.abort(rid)  # free the replica's slot and KV blocks
+                    raise GenerationError("generation timed out") from None
+                ids, reason, *text = slot[0]
+                if reason.startswith(WorkerPool.LOST) and tries < self.max_redispatch:
+                    pool.release(rid)
+                    tries += 1
+                    job = pool.submit(pool.pick(), prompt, params, ev=_LoopEvent(loop))
+                    continue
+                if reason.startswith("error"):
+                    raise GenerationError(reason)
+                return text[0] if text and text[0] is not None else self.tok.decode(ids)
+        finally:
+            pool.release(job[0])
+
+
+class _LoopEvent:
+    """Completion signal of one request for an asyncio caller: ``set()`` may run on any
+    thread (the pool's collector, an eviction) and resolves ``fut`` on its loop."""
+
+    __slots__ = ("loop", "fut")
+
+    def __init__(self, loop):
+        self.loop = loop
+        self.fut = loop.create_future()
+
+    def _resolve(self):
+        if not self.fut.done():
+            self.fut.set_result(None)
+
+    def set(self):
+        try:
+            self.loop.call_soon_threadsafe(self._resolve)
+        except RuntimeError:  # loop closed: nobody waits any more
+            pass
+
+    def is_set(self) -> bool:
+        return self.fut.done()
 
 
 def visible_gpus() -> int:

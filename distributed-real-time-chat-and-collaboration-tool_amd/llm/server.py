@@ -27,7 +27,7 @@ from ..protos import LLM_SERVICE, add_servicer
 from ..utils.config import parse_with_config
 from ..utils.logging_utils import setup_logging
 from .backends import ScriptedBackend
-from .service import LLMServicer
+from .service import AsyncLLMServicer, LLMServicer
 
 log = logging.getLogger("drtc_amd.llm.server")
 
@@ -96,6 +96,68 @@ def serve(backend, port: int = 50055, workers: int = 64, bind: str = "[::]", par
     return server
 
 
+class AioServer:
+    """``grpc.aio`` server on its own event-loop thread (the front-end of
+    ``--frontend aio``): every in-flight RPC is a coroutine of that one thread instead of a
+    pool thread blocked on its generation, so 1k concurrent requests cost no thread
+    switching under the GIL.  ``stop(grace)`` mirrors grpc.Server.stop."""
+
+    def __init__(self, backend, port: int, bind: str, params=None):
+        import asyncio
+
+        self.loop = asyncio.new_event_loop()
+        self._ready = threading.Event()
+        self._err = None
+        self._server = None
+        self._thread = threading.Thread(target=self._run, args=(backend, port, bind, params),
+                                        daemon=True, name="llm-aio")
+        self._thread.start()
+        self._ready.wait()
+        if self._err is not None:
+            raise self._err
+
+    def _run(self, backend, port, bind, params):
+        import asyncio
+
+        asyncio.set_event_loop(self.loop)
+
+        async def start():
+            srv = grpc.aio.server()
+            add_servicer(srv, LLM_SERVICE, AsyncLLMServicer(backend, params))
+            if srv.add_insecure_port(f"{bind}:{port}") == 0:
+                raise RuntimeError(f"cannot bind port {port}")
+            await srv.start()
+            return srv
+
+        try:
+            self._server = self.loop.run_until_complete(start())
+        except Exception as e:  # surfaced to the constructor's caller
+            self._err = e
+            self._ready.set()
+            return
+        self._ready.set()
+        self.loop.run_forever()
+
+    def stop(self, grace=None) -> threading.Event:
+        import asyncio
+
+        done = threading.Event()
+        if self._server is not None:
+            fut = asyncio.run_coroutine_threadsafe(self._server.stop(grace), self.loop)
+            try:
+                fut.result(timeout=(grace or 0) + 10)
+            finally:
+                self.loop.call_soon_threadsafe(self.loop.stop)
+                self._thread.join(timeout=10)
+                self._server = None
+        done.set()
+        return done
+
+
+def serve_aio(backend, port: int = 50055, bind: str = "[::]", params=None) -> AioServer:
+    return AioServer(backend, port, bind, params)
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser(description="drtc_amd LLM service (on-GPU inference)")
     ap.add_argument("--port", type=int, default=50055)
@@ -117,6 +179,9 @@ def main(argv=None):
     ap.add_argument("--workers", type=int, default=None,
                     help="gRPC handler threads; each blocks on one generation (default: "
                          "max-batch x replicas + 16, so the engine batch can fill)")
+    ap.add_argument("--frontend", choices=("threads", "aio"), default="threads",
+                    help="gRPC front-end: a handler thread per in-flight RPC, or grpc.aio "
+                         "coroutines on one event-loop thread")
     ap.add_argument("--log-level", default="INFO")
     args = parse_with_config(ap, argv)
     setup_logging(args.log_level)
@@ -124,7 +189,8 @@ def main(argv=None):
         args.max_batch = default_max_batch(args.model, args.tp)
     backend = build_backend(args)
     workers = args.workers or args.max_batch * max(1, args.gpus) + 16
-    server = serve(backend, args.port, workers)
+    server = (serve_aio(backend, args.port) if args.frontend == "aio"
+              else serve(backend, args.port, workers))
     log.info("LLM server on port %d (backend=%s model=%s gpus=%d tp=%d)", args.port, args.backend,
              args.model, args.gpus, args.tp)
     stop = threading.Event()

@@ -91,44 +91,138 @@ class LLMServicer:
                                   answer=P.ANSWER_EMPTY if empty else P.ANSWER_ERROR,
                                   confidence=0.0)
 
-    def GetSmartReply(self, request, context):
+    # Each RPC other than ask-AI is (early answer | prompt, params, parse, fallback); the
+    # thread-pool handlers below and the asyncio ones (AsyncLLMServicer) share these parts.
+    def _smart_parts(self, request):
         msgs = list(request.recent_messages)
+        rid = request.request_id
         if not msgs:
-            return llm_pb.SmartReplyResponse(request_id=request.request_id, suggestions=P.SMART_REPLY_EMPTY)
-        try:
-            text = self._gen("smart_reply", P.smart_reply_prompt(msgs), self.p.smart, context)
-            return llm_pb.SmartReplyResponse(request_id=request.request_id,
-                                             suggestions=P.parse_smart_replies(text))
-        except Exception as e:
-            log.error("smart reply failed: %s", e)
-            return llm_pb.SmartReplyResponse(request_id=request.request_id,
-                                             suggestions=P.SMART_REPLY_FALLBACK)
+            return llm_pb.SmartReplyResponse(request_id=rid, suggestions=P.SMART_REPLY_EMPTY), None
+        return None, ("smart_reply", P.smart_reply_prompt(msgs), self.p.smart,
+                      lambda text: llm_pb.SmartReplyResponse(
+                          request_id=rid, suggestions=P.parse_smart_replies(text)),
+                      lambda: llm_pb.SmartReplyResponse(request_id=rid,
+                                                        suggestions=P.SMART_REPLY_FALLBACK))
 
-    def SummarizeConversation(self, request, context):
+    def _summary_parts(self, request):
         msgs = list(request.messages)
         max_len = request.max_length if request.max_length > 0 else 200
+        rid = request.request_id
         if not msgs:
-            return llm_pb.SummarizeResponse(request_id=request.request_id,
-                                            summary="No messages to summarize", key_points=[])
-        try:
-            text = self._gen("summarize", P.summarize_prompt(msgs, max_len), self.p.summary,
-                             context)
+            return llm_pb.SummarizeResponse(request_id=rid, summary="No messages to summarize",
+                                            key_points=[]), None
+
+        def ok(text):
             summary, points = P.parse_summary(text, msgs, max_len)
-            return llm_pb.SummarizeResponse(request_id=request.request_id, summary=summary,
-                                            key_points=points)
+            return llm_pb.SummarizeResponse(request_id=rid, summary=summary, key_points=points)
+        return None, ("summarize", P.summarize_prompt(msgs, max_len), self.p.summary, ok,
+                      lambda: llm_pb.SummarizeResponse(request_id=rid, summary=P.SUMMARY_ERROR,
+                                                       key_points=[]))
+
+    def _suggest_parts(self, request):
+        msgs = list(request.context)
+        rid = request.request_id
+
+        def ok(text):
+            s, t = P.parse_suggestions(text, request.current_input)
+            return llm_pb.SuggestionsResponse(request_id=rid, suggestions=s, topics=t)
+        return None, ("suggest", P.suggestions_prompt(msgs, request.current_input),
+                      self.p.suggest, ok,
+                      lambda: llm_pb.SuggestionsResponse(request_id=rid,
+                                                         suggestions=P.SUGGEST_ERROR, topics=[]))
+
+    def _run(self, parts, context):
+        early, job = parts
+        if early is not None:
+            return early
+        feature, prompt, params, ok, fail = job
+        try:
+            return ok(self._gen(feature, prompt, params, context))
         except Exception as e:
-            log.error("summarize failed: %s", e)
-            return llm_pb.SummarizeResponse(request_id=request.request_id, summary=P.SUMMARY_ERROR,
-                                            key_points=[])
+            log.error("%s failed: %s", feature, e)
+            return fail()
+
+    def GetSmartReply(self, request, context):
+        return self._run(self._smart_parts(request), context)
+
+    def SummarizeConversation(self, request, context):
+        return self._run(self._summary_parts(request), context)
 
     def GetContextSuggestions(self, request, context):
-        msgs = list(request.context)
+        return self._run(self._suggest_parts(request), context)
+
+
+class AsyncLLMServicer(LLMServicer):
+    """The same four RPCs as coroutines for a ``grpc.aio`` server: one event-loop thread
+    serves every in-flight request (no handler thread per generation), and a replica's
+    completions resolve their futures from the pool's collector thread.  Backends without
+    an ``agenerate`` coroutine run ``generate`` on the loop's default executor."""
+
+    async def _agen(self, feature: str, prompt: str, params: SamplingParams, context=None) -> str:
+        import asyncio
+
+        t0 = time.perf_counter()
+        timeout = self.timeout
+        left = context.time_remaining() if context is not None else None
+        if left is not None:
+            timeout = min(timeout, max(0.05, left))
+        agen = getattr(self.backend, "agenerate", None)
+        if agen is not None:
+            text = await agen(prompt, params, timeout=timeout)
+        else:
+            loop = asyncio.get_running_loop()
+            text = (await loop.run_in_executor(
+                None, lambda: self.backend.generate([prompt], [params], timeout=timeout)))[0]
+        METRICS.observe(f"llm.{feature}.latency_s", time.perf_counter() - t0)
+        METRICS.inc(f"llm.{feature}.requests")
+        return text
+
+    async def _arun(self, parts, context):
+        early, job = parts
+        if early is not None:
+            return early
+        feature, prompt, params, ok, fail = job
         try:
-            text = self._gen("suggest", P.suggestions_prompt(msgs, request.current_input),
-                             self.p.suggest, context)
-            s, t = P.parse_suggestions(text, request.current_input)
-            return llm_pb.SuggestionsResponse(request_id=request.request_id, suggestions=s, topics=t)
+            return ok(await self._agen(feature, prompt, params, context))
         except Exception as e:
-            log.error("suggestions failed: %s", e)
-            return llm_pb.SuggestionsResponse(request_id=request.request_id,
-                                              suggestions=P.SUGGEST_ERROR, topics=[])
+            log.error("%s failed: %s", feature, e)
+            return fail()
+
+    async def GetLLMAnswer(self, request, context):
+        """Ask-AI with the retry + backoff of LLMServicer.GetLLMAnswer (asyncio sleeps)."""
+        import asyncio
+
+        prompt = P.answer_prompt(request.query, list(request.context))
+        empty = False
+        for attempt in range(self.answer_retries):
+            try:
+                answer = P.parse_answer(await self._agen("answer", prompt, self.p.answer, context))
+                if answer:
+                    return llm_pb.LLMResponse(request_id=request.request_id, answer=answer,
+                                              confidence=0.95)
+                empty = True
+                log.warning("empty LLM answer (attempt %d)", attempt + 1)
+            except Exception as e:
+                empty = False
+                log.warning("LLM answer attempt %d/%d failed: %s", attempt + 1,
+                            self.answer_retries, str(e)[:120])
+            if attempt + 1 < self.answer_retries:
+                wait = self.answer_backoff * (2 ** attempt)
+                left = context.time_remaining() if context is not None else None
+                if left is not None and left < wait + 1.0:
+                    break
+                METRICS.inc("llm.answer.retries")
+                await asyncio.sleep(wait)
+        log.error("LLM answer failed after retries")
+        return llm_pb.LLMResponse(request_id=request.request_id,
+                                  answer=P.ANSWER_EMPTY if empty else P.ANSWER_ERROR,
+                                  confidence=0.0)
+
+    async def GetSmartReply(self, request, context):
+        return await self._arun(self._smart_parts(request), context)
+
+    async def SummarizeConversation(self, request, context):
+        return await self._arun(self._summary_parts(request), context)
+
+    async def GetContextSuggestions(self, request, context):
+        return await self._arun(self._suggest_parts(request), context)

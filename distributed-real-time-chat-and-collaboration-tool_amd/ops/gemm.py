@@ -212,7 +212,7 @@ def linear(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
             return mfma_gemm(x, w, "store", variant=11, splitk=sk, group_m=4)
         if ent is None and M > DECODE_MAX_M:
             if w4_ok(x, w):
-                return mfma_gemm(x, w, "store", variant=W4_VARIANT, group_m=w4_group_m(M, N, K))
+                return mfma_gemm(x, w, "store", variant=_w4v(K), group_m=w4_group_m(M, N, K))
             if _prefill_algo(M, N, K, x.stride(0), 0) >= 0:
                 y = torch.empty((M, N), dtype=x.dtype, device=x.device)
                 check(hipk().lt_gemm(y.data_ptr(), x.data_ptr(), w.data_ptr(), M, N, K,
@@ -264,7 +264,7 @@ def linear_residual(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor) ->
     M, K = x.shape
     N = w.shape[0]
     if w4_ok(x, w, residual):
-        return mfma_gemm(x, w, "residual", residual=residual, out=residual, variant=W4_VARIANT,
+        return mfma_gemm(x, w, "residual", residual=residual, out=residual, variant=_w4v(K),
                          group_m=w4_group_m(M, N, K))
     if (_enabled and x.stride(1) == 1 and w.is_contiguous() and residual.stride(0) == N
             and x.dtype == torch.bfloat16):
@@ -501,17 +501,27 @@ def rs_linear(h: torch.Tensor, w_folded: torch.Tensor, rinv: torch.Tensor,
         if not w4_ok(h, w_folded):
             return None
         M, K = h.shape
-        return mfma_gemm(h, w_folded, "store_rs", variant=W4_VARIANT,
+        return mfma_gemm(h, w_folded, "store_rs", variant=_w4v(K),
                          group_m=w4_group_m(M, w_folded.shape[0], K), side=rinv)
     if not (w4_glu_ok(h, w_folded, act) and h.shape[0] >= W4_MIN_M):
         return None
     M, K = h.shape
-    return mfma_gemm(h, w_folded, act + "_rs", variant=W4_VARIANT,
+    return mfma_gemm(h, w_folded, act + "_rs", variant=_w4v(K),
                      group_m=w4_group_m(M, w_folded.shape[0] // 2, K, glu=True), side=rinv)
 
 
 # ------------------------------------------------------------ 4-wave GEMM dispatch
 W4_VARIANT = 7  # gemm_w4.hip through launch_gemm
+# Persistent gemm_w4 (variant 15: min(tiles, CUs) workgroups, the next tile's first K tiles
+# staged during the current tile's last two steps) for the single-slice calls.
+W4_PERSIST = os.environ.get("DRTC_W4_PERSIST", "0") == "1"
+
+
+def _w4v(K: int) -> int:
+    """Schedule variant of a single-slice gemm_w4 call with reduction length K."""
+    return 15 if W4_PERSIST and K >= 128 else W4_VARIANT
+
+
 _w4_glu = os.environ.get("DRTC_W4_GLU", "1") != "0"
 _w4_plain = os.environ.get("DRTC_W4_GEMM", "1") != "0"
 # Prefill-sized passes (M >= W4_MIN_M rows) run the 4-wave hand GEMM (profiles/r3a_w4_gemm.md,
@@ -712,7 +722,7 @@ def norm_glu(p, w: torch.Tensor, act: str = "silu",
     if w4_glu_ok(p.x, w, act):
         x = p.materialize()
         M, K = x.shape
-        return mfma_gemm(x, w, act, variant=W4_VARIANT,
+        return mfma_gemm(x, w, act, variant=_w4v(K),
                          group_m=w4_group_m(M, w.shape[0] // 2, K, glu=True))
     return act_glu(norm_linear(p, w), act)
 

@@ -12,6 +12,7 @@ are identical to those of protoc-generated code for the same contract.
 """
 from __future__ import annotations
 
+import inspect
 import time
 import types
 from dataclasses import dataclass
@@ -181,6 +182,17 @@ def _instrumented(fn, label: str):
     from ..utils.metrics import METRICS
 
     hist, cnt, span = f"rpc.{label}.latency_s", f"rpc.{label}.calls", f"rpc {label}"
+
+    if inspect.iscoroutinefunction(fn):  # grpc.aio handler: coroutines of one loop thread
+        # interleave, so no (thread-stacked) roctx range around the await
+        async def ahandler(request, context):
+            t = time.perf_counter()
+            try:
+                return await fn(request, context)
+            finally:
+                METRICS.observe(hist, time.perf_counter() - t)
+                METRICS.inc(cnt)
+        return ahandler
 
     def handler(request, context):
         t = time.perf_counter()

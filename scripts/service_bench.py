@@ -31,7 +31,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 import grpc  # noqa: E402
 
-from drtc_amd.llm.server import serve as serve_llm  # noqa: E402
+from drtc_amd.llm.server import serve as serve_llm, serve_aio  # noqa: E402
 from drtc_amd.llm.service import FeatureParams  # noqa: E402
 from drtc_amd.protos import LLM_SERVICE, RAFT_SERVICE, llm_pb, make_stub, raft_pb  # noqa: E402
 from drtc_amd.utils.cluster import LocalCluster, free_port  # noqa: E402
@@ -188,6 +188,8 @@ def main():
                     help="run the load clients in this many separate processes (0: threads here)")
     ap.add_argument("--model", default="llama-3-8b")
     ap.add_argument("--mode", choices=("direct", "raft"), default="direct")
+    ap.add_argument("--frontend", choices=("threads", "aio"), default="threads",
+                    help="LLM service front-end (llm/server.py --frontend)")
     ap.add_argument("--requests", type=int, default=1024)
     ap.add_argument("--concurrency", type=int, default=256)
     ap.add_argument("--max-batch", type=int, default=512)
@@ -199,8 +201,11 @@ def main():
     backend, eng = build_backend(args)
     fp = FeatureParams(ignore_eos=True)  # full 48-token budget per reply (random weights)
     port = free_port()
-    llm_srv = serve_llm(backend, port=port, bind="127.0.0.1", params=fp,
-                        workers=args.concurrency + 8)
+    if args.frontend == "aio":
+        llm_srv = serve_aio(backend, port=port, bind="127.0.0.1", params=fp)
+    else:
+        llm_srv = serve_llm(backend, port=port, bind="127.0.0.1", params=fp,
+                            workers=args.concurrency + 8)
     rng = random.Random(0)
     cluster = None
     tmp = tempfile.TemporaryDirectory()
@@ -268,7 +273,7 @@ def main():
                      else f"closed-loop, {args.concurrency} clients"),
             "p50_tpot_ms": round(1000 * tpot["p50"], 1) if "p50" in tpot else None,
             "p99_tpot_ms": round(1000 * tpot["p99"], 1) if "p99" in tpot else None,
-            "backend": args.backend, "model": args.model if args.backend != "scripted" else None,
+            "backend": args.backend, "frontend": args.frontend, "model": args.model if args.backend != "scripted" else None,
             "client_procs": args.client_procs,
             "requests": len(lat), "errors": len(errors), "concurrency": args.concurrency, "seconds": round(dt, 3),
             "requests_per_s": round(len(lat) / dt, 2),

@@ -374,3 +374,64 @@ def test_default_engine_batch_per_model():
     assert default_max_batch("llama-3-70b") == 192      # p50 9.45 s < 10 s ask-AI deadline
     assert default_max_batch("llama-3-70b", tp=8) == 256
     assert default_max_batch("tiny-llama") == 256
+
+
+def test_aio_frontend_serves_all_rpcs_over_a_replica_pool():
+    """--frontend aio: grpc.aio handlers await ReplicaRouter.agenerate (no thread per
+    request); every RPC answers through a tiny-llama replica process, a timed-out
+    coroutine aborts its request on the replica, and the pool's load returns to zero."""
+    import asyncio
+
+    from drtc_amd.engine import SamplingParams
+    from drtc_amd.llm.backends import GenerationError, ReplicaRouter, WorkerPool
+    from drtc_amd.llm.server import serve_aio
+    from drtc_amd.llm.service import FeatureParams
+    from drtc_amd.protos import llm_pb
+
+    kw = dict(max_batch=8, max_model_len=1024, num_blocks=128, use_graphs=False)
+    pool = WorkerPool("tiny-llama", ["cpu"], kw, hb_interval=0.1)
+    srv = None
+    try:
+        router = ReplicaRouter(pool, ChatTokenizer(TINY_LLAMA.vocab_size), 1024)
+        fp = FeatureParams(ignore_eos=True)
+        for f in ("answer", "smart", "summary", "suggest"):
+            setattr(fp, f, SamplingParams(max_new_tokens=6, temperature=1.0, top_k=8,
+                                          top_p=0.95, ignore_eos=True))
+        port = free_port()
+        srv = serve_aio(router, port=port, bind="127.0.0.1", params=fp)
+        stub = _llm_stub(port)
+        msgs = [llm_pb.Message(sender="alice", content="are we shipping today?"),
+                llm_pb.Message(sender="bob", content="after the review")]
+        r = stub.GetSmartReply(llm_pb.SmartReplyRequest(request_id="a", recent_messages=msgs),
+                               timeout=60)
+        assert len(r.suggestions) == 3
+        r = stub.GetLLMAnswer(llm_pb.LLMRequest(request_id="b", query="when is the release?"),
+                              timeout=60)
+        assert r.request_id == "b" and r.answer
+        r = stub.SummarizeConversation(llm_pb.SummarizeRequest(request_id="c", messages=msgs,
+                                                               max_length=80), timeout=60)
+        assert r.summary and r.request_id == "c"
+        r = stub.GetContextSuggestions(llm_pb.ContextRequest(request_id="d", context=msgs,
+                                                             current_input="ok"), timeout=60)
+        assert r.request_id == "d" and len(r.suggestions) >= 1
+        # concurrent RPCs meet in the replica's batch
+        futs = [stub.GetSmartReply.future(llm_pb.SmartReplyRequest(request_id=str(i),
+                                                                   recent_messages=msgs))
+                for i in range(16)]
+        assert all(len(f.result(timeout=120).suggestions) == 3 for f in futs)
+        # a coroutine that times out aborts its request on the replica
+        loop = asyncio.new_event_loop()
+        try:
+            with pytest.raises(GenerationError):
+                loop.run_until_complete(router.agenerate(
+                    "hello " * 20, SamplingParams.greedy(900, ignore_eos=True), timeout=0.2))
+        finally:
+            loop.close()
+        deadline = time.time() + 30
+        while time.time() < deadline and pool.load != [0]:
+            time.sleep(0.1)
+        assert pool.load == [0]
+    finally:
+        if srv is not None:
+            srv.stop(0)
+        pool.close()
