@@ -513,8 +513,12 @@ def rs_linear(h: torch.Tensor, w_folded: torch.Tensor, rinv: torch.Tensor,
 # ------------------------------------------------------------ 4-wave GEMM dispatch
 W4_VARIANT = 7  # gemm_w4.hip through launch_gemm
 # Persistent gemm_w4 (variant 15: min(tiles, CUs) workgroups, the next tile's first K tiles
-# staged during the current tile's last two steps) for the single-slice calls.
-W4_PERSIST = os.environ.get("DRTC_W4_PERSIST", "0") == "1"
+# staged during the current tile's last two steps) for the single-slice calls.  Against the
+# per-tile form in one process (profiles/r3r/probe.log): prefill qkv +0.5 %, o +2.0 %,
+# gate_up+GLU +0.9 %, a 4400-row chunk's gate_up+GLU +2.3 %, decode gate_up+GLU at M = 1024
+# +4.0 % (now level with hipBLASLt + act_glu); headline neutral (19,837 vs 19,836 tok/s, two
+# runs each, one box).  DRTC_W4_PERSIST=0 restores the per-tile form.
+W4_PERSIST = os.environ.get("DRTC_W4_PERSIST", "1") == "1"
 
 
 def _w4v(K: int) -> int:
