@@ -4,12 +4,14 @@
 //                       a cost-12 hash is ~0.25 s and must not stall the
 //                       gRPC server's other threads)
 //   * LogStore        - append-only, CRC-checked Raft log segments
+//   * WordTokenizer   - chat tokenizer encode / decode for ASCII text (GIL released)
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
 #include "bcrypt.h"
 #include "block_allocator.h"
 #include "log_store.h"
+#include "tokenizer.h"
 
 namespace py = pybind11;
 
@@ -79,4 +81,32 @@ PYBIND11_MODULE(_native, m) {
         s.sync();
       })
       .def("close", &drtc::LogStore::close);
+
+  py::class_<drtc::WordTokenizer>(m, "WordTokenizer")
+      .def(py::init<std::vector<std::string>, int32_t, int32_t, std::vector<int32_t>>(),
+           py::arg("vocab"), py::arg("byte_base"), py::arg("bos_id"), py::arg("skip_ids"))
+      .def_property_readonly("vocab_size", &drtc::WordTokenizer::vocab_size)
+      .def("encode",
+           [](const drtc::WordTokenizer& t, const std::string& text, bool add_bos) {
+             std::vector<int32_t> ids;
+             {
+               py::gil_scoped_release nogil;
+               ids = t.encode(text, add_bos);
+             }
+             py::list out(ids.size());
+             for (size_t i = 0; i < ids.size(); ++i)
+               PyList_SET_ITEM(out.ptr(), i, PyLong_FromLong(ids[i]));
+             return out;
+           },
+           py::arg("text"), py::arg("add_bos") = true)
+      .def("decode",
+           [](const drtc::WordTokenizer& t, const std::vector<int64_t>& ids, bool skip_special) {
+             std::string s;
+             {
+               py::gil_scoped_release nogil;
+               s = t.decode(ids, skip_special);
+             }
+             return py::bytes(s);
+           },
+           py::arg("ids"), py::arg("skip_special") = true);
 }

@@ -15,6 +15,8 @@ prompt strings themselves are the reference's, see llm/prompts.py.)
 """
 from __future__ import annotations
 
+import importlib
+import os
 import random
 import re
 
@@ -68,6 +70,19 @@ def _pseudo_words(seed: int):
             yield w
 
 
+def _native_tokenizer(toks, byte_base, bos_id, skip_ids):
+    """drtc_amd._native.WordTokenizer over ``toks``, or None without the native module
+    (DRTC_NATIVE_TOKENIZER=0 forces the Python path)."""
+    if os.environ.get("DRTC_NATIVE_TOKENIZER", "1") == "0":
+        return None
+    try:
+        pkg = __name__.rsplit(".", 2)[0]
+        mod = importlib.import_module(pkg + "._native")
+        return mod.WordTokenizer(toks, byte_base, bos_id, skip_ids)
+    except (ImportError, AttributeError):
+        return None
+
+
 class ChatTokenizer:
     def __init__(self, vocab_size: int, bos_id: int | None = None, eos_id: int | None = None,
                  seed: int = 1234):
@@ -110,8 +125,25 @@ class ChatTokenizer:
         self.bos_id = 1 if bos_id is None else bos_id
         self.eos_id = 2 if eos_id is None else eos_id
         self._bytes = {i: bytes([i - self.byte_base]) for i in range(self.byte_base, self.byte_base + 256)}
+        # native encode / decode (csrc/runtime/tokenizer.cpp, GIL released) for ASCII text;
+        # this class stays the reference (non-ASCII input, no native build)
+        self._nt = _native_tokenizer(toks, self.byte_base, self.bos_id,
+                                     list(range(len(SPECIALS))) + [self.bos_id, self.eos_id])
 
     def encode(self, text: str, add_bos: bool = True) -> list[int]:
+        if self._nt is not None and text.isascii():
+            return self._nt.encode(text, add_bos)
+        return self.encode_py(text, add_bos)
+
+    def decode(self, ids, skip_special: bool = True) -> str:
+        if self._nt is not None:
+            try:
+                return self._nt.decode(ids, skip_special).decode("utf-8", errors="replace")
+            except TypeError:  # ids not convertible to int64 (e.g. a tensor): generic path
+                pass
+        return self.decode_py(ids, skip_special)
+
+    def encode_py(self, text: str, add_bos: bool = True) -> list[int]:
         get = self.tok_to_id.get
         pieces = _PIECE.findall(text)
         ids = list(map(get, pieces))  # one C-level pass: the serving path's common case
@@ -132,7 +164,7 @@ class ChatTokenizer:
             out.extend(self.byte_base + b for b in piece.encode("utf-8"))
         return out
 
-    def decode(self, ids, skip_special: bool = True) -> str:
+    def decode_py(self, ids, skip_special: bool = True) -> str:
         buf = bytearray()
         for i in ids:
             i = int(i)
