@@ -62,20 +62,20 @@ DRTC_DEVICE float uniform(uint64_t seed, uint64_t st, int row, int round) {
 // kUnroll 16-byte loads are issued before any is consumed (a lane streams
 // ~16 vectors of a 128k row: one load in flight would leave the pass
 // latency-bound at about half the HBM rate).
-constexpr int kUnroll = 4;
-template <class F>
+constexpr int kUnroll = 4;  // default U (one workgroup per CU)
+template <int U, class F>
 DRTC_DEVICE void for_row(const unsigned short* lr, int V, bool vec, F&& f) {
   const int tid = threadIdx.x;
   if (vec) {
     const int nv = V >> 3;
-    for (int v = tid; v < nv; v += kUnroll * kSampThreads) {
-      u16x8 x[kUnroll];
+    for (int v = tid; v < nv; v += U * kSampThreads) {
+      u16x8 x[U];
 #pragma unroll
-      for (int u = 0; u < kUnroll; ++u)
+      for (int u = 0; u < U; ++u)
         if (v + u * kSampThreads < nv)
           x[u] = *reinterpret_cast<const u16x8*>(lr + 8 * (v + u * kSampThreads));
 #pragma unroll
-      for (int u = 0; u < kUnroll; ++u) {
+      for (int u = 0; u < U; ++u) {
         if (v + u * kSampThreads < nv) {
 #pragma unroll
           for (int j = 0; j < 8; ++j) f(8 * (v + u * kSampThreads) + j, x[u][j]);
@@ -181,6 +181,7 @@ DRTC_DEVICE void select_bin(SampShared& s, const unsigned* hist, int remaining) 
 
 // Exact key of the k-th largest element by a 16-bit radix select (two
 // histogram passes over the row; per-wave histograms).
+template <int U>
 DRTC_DEVICE unsigned radix_kth(SampShared& s, const unsigned short* lr, int V, bool vec, int k) {
   const int tid = threadIdx.x, wid = tid >> 6;
   unsigned prefix = 0, mask = 0;
@@ -189,7 +190,7 @@ DRTC_DEVICE unsigned radix_kth(SampShared& s, const unsigned short* lr, int V, b
     for (int i = tid; i < kSampWaves * 256; i += kSampThreads) (&s.hist[0][0])[i] = 0;
     __syncthreads();
     unsigned* h = s.hist[wid];
-    for_row(lr, V, vec, [&](int, unsigned short b) {
+    for_row<U>(lr, V, vec, [&](int, unsigned short b) {
       const unsigned key = ord16(b);
       if ((key & mask) == prefix) atomicAdd(&h[(key >> pass) & 255u], 1u);
     });
@@ -212,6 +213,7 @@ DRTC_DEVICE unsigned radix_kth(SampShared& s, const unsigned short* lr, int V, b
 
 // Gather every element with key >= thr into s.val / s.idx (ballot-compacted);
 // returns the number found (may exceed kCand: only the first kCand are kept).
+template <int U>
 DRTC_DEVICE int gather_ge(SampShared& s, const unsigned short* lr, int V, bool vec, unsigned thr) {
   const int tid = threadIdx.x, lane = tid & 63;
   if (tid == 0) s.misc[2] = 0;
@@ -235,17 +237,17 @@ DRTC_DEVICE int gather_ge(SampShared& s, const unsigned short* lr, int V, bool v
   const int w0 = tid & ~63;
   if (vec) {
     const int nv = V >> 3;
-    for (int v0 = w0; v0 < nv; v0 += kUnroll * kSampThreads) {
-      u16x8 x[kUnroll];
-      bool any[kUnroll];
+    for (int v0 = w0; v0 < nv; v0 += U * kSampThreads) {
+      u16x8 x[U];
+      bool any[U];
 #pragma unroll
-      for (int u = 0; u < kUnroll; ++u) {
+      for (int u = 0; u < U; ++u) {
         const int v = v0 + u * kSampThreads + lane;
         x[u] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
         if (v < nv) x[u] = *reinterpret_cast<const u16x8*>(lr + 8 * v);
       }
 #pragma unroll
-      for (int u = 0; u < kUnroll; ++u) {
+      for (int u = 0; u < U; ++u) {
         const int v = v0 + u * kSampThreads + lane;
         any[u] = false;
         if (v < nv) {
@@ -254,7 +256,7 @@ DRTC_DEVICE int gather_ge(SampShared& s, const unsigned short* lr, int V, bool v
         }
       }
 #pragma unroll
-      for (int u = 0; u < kUnroll; ++u) {
+      for (int u = 0; u < U; ++u) {
         if (__ballot(any[u]) == 0) continue;  // wave-uniform
         const int v = v0 + u * kSampThreads + lane;
 #pragma unroll
@@ -277,13 +279,14 @@ DRTC_DEVICE int gather_ge(SampShared& s, const unsigned short* lr, int V, bool v
   return s.misc[2];
 }
 
+template <int U>
 DRTC_DEVICE void sample_topk(SampShared& s, int* out_tokens, const unsigned short* lr, int V,
                              bool vec, int row, float temp, int k, float pp, uint64_t seed,
                              uint64_t st) {
   const int tid = threadIdx.x;
   // ---- pass 1: per-thread max key; tau0 = k-th largest of the thread maxima
   unsigned tm = 0;
-  for_row(lr, V, vec, [&](int, unsigned short b) { tm = max(tm, ord16(b)); });
+  for_row<U>(lr, V, vec, [&](int, unsigned short b) { tm = max(tm, ord16(b)); });
   unsigned* h = &s.hist[0][0];
   h[tid] = tm;  // hist doubles as a 1024-key buffer here
   __syncthreads();
@@ -311,7 +314,7 @@ DRTC_DEVICE void sample_topk(SampShared& s, int* out_tokens, const unsigned shor
   s.idx[tid] = 0x7fffffff;
   __syncthreads();
   if (tm >= prefix) {
-    for_row(lr, V, vec, [&](int i, unsigned short b) {
+    for_row<U>(lr, V, vec, [&](int i, unsigned short b) {
       if (ord16(b) >= prefix) {
         const int slot = atomicAdd(&s.misc[2], 1);
         if (slot < kCand) { s.val[slot] = bits2f(b); s.idx[slot] = i; }
@@ -321,8 +324,8 @@ DRTC_DEVICE void sample_topk(SampShared& s, int* out_tokens, const unsigned shor
   __syncthreads();
   int n = s.misc[2];
   if (n > kCand) {  // heavy ties: exact k-th key by radix select, gather again
-    const unsigned thr = radix_kth(s, lr, V, vec, k);
-    n = min(gather_ge(s, lr, V, vec, thr), kCand);
+    const unsigned thr = radix_kth<U>(s, lr, V, vec, k);
+    n = min(gather_ge<U>(s, lr, V, vec, thr), kCand);
   }
   int np2 = 1;
   while (np2 < n) np2 <<= 1;
@@ -383,6 +386,7 @@ DRTC_DEVICE void sample_topk(SampShared& s, int* out_tokens, const unsigned shor
   }
 }
 
+template <int U>
 DRTC_DEVICE void sample_topp_full(SampShared& s, int* out_tokens, const unsigned short* lr, int V,
                                   bool vec, int row, float temp, float pp, uint64_t seed,
                                   uint64_t st) {
@@ -390,7 +394,7 @@ DRTC_DEVICE void sample_topp_full(SampShared& s, int* out_tokens, const unsigned
   const float inv_t = 1.f / temp;
   // ---- pass 1: row max and per-thread softmax mass (online, 8 at a time)
   float m_t = -INFINITY, s_t = 0.f;
-  for_row(lr, V, vec, [&](int, unsigned short b) {
+  for_row<U>(lr, V, vec, [&](int, unsigned short b) {
     const float x = bits2f(b);
     if (!(x > -INFINITY)) return;  // -inf (masked) or NaN: zero mass
     if (x > m_t) {
@@ -427,7 +431,7 @@ DRTC_DEVICE void sample_topp_full(SampShared& s, int* out_tokens, const unsigned
       float acc = excl;
       int pick = -1, last = -1;
       unsigned pk = 0, lk = 0;
-      for_row(lr, V, vec, [&](int i, unsigned short b) {
+      for_row<U>(lr, V, vec, [&](int i, unsigned short b) {
         const unsigned key = ord16(b);
         const float x = bits2f(b);
         if (pick < 0 && (l_open || key > L) && x > -INFINITY) {
@@ -456,7 +460,7 @@ DRTC_DEVICE void sample_topp_full(SampShared& s, int* out_tokens, const unsigned
     const unsigned t = lo + ((H - lo) >> 1);
     const bool bis = t > lo && t < H && t != kj;
     float a_t = 0.f, f_t = 0.f;
-    for_row(lr, V, vec, [&](int, unsigned short b) {
+    for_row<U>(lr, V, vec, [&](int, unsigned short b) {
       const unsigned key = ord16(b);
       const float w = __expf((bits2f(b) - m) * inv_t);
       a_t += key > kj ? w : 0.f;
@@ -480,11 +484,16 @@ DRTC_DEVICE void sample_topp_full(SampShared& s, int* out_tokens, const unsigned
   }
 }
 
-__global__ __launch_bounds__(kSampThreads) void sample_kernel(
+// OCC = 1: one 1024-thread workgroup per CU (91 VGPRs, 4-deep load unroll); OCC = 2: two
+// (<= 64 VGPRs, 2-deep unroll), so one row's selection tail (scans, block reductions,
+// barriers) overlaps another row's stream on the same CU.
+template <int OCC>
+__global__ __launch_bounds__(kSampThreads, 4 * OCC) void sample_kernel(
     int* __restrict__ out_tokens, const bf16_t* __restrict__ logits, int V,
     int ld, const float* __restrict__ temperature, const int* __restrict__ top_k,
     const float* __restrict__ top_p, uint64_t seed,
     const int64_t* __restrict__ step) {
+  constexpr int U = OCC == 1 ? kUnroll : 2;
   const int row = blockIdx.x;
   const int tid = threadIdx.x;
   const int lane = tid & 63, wid = tid >> 6;
@@ -496,7 +505,7 @@ __global__ __launch_bounds__(kSampThreads) void sample_kernel(
   if (temp <= 0.f) {  // ---------------------------------- greedy argmax
     float best = -INFINITY;
     int bi = 0x7fffffff;
-    for_row(lr, V, vec, [&](int i, unsigned short b) {
+    for_row<U>(lr, V, vec, [&](int i, unsigned short b) {
       const float v = bits2f(b);
       if (v > best || (v == best && i < bi)) { best = v; bi = i; }
     });
@@ -520,9 +529,9 @@ __global__ __launch_bounds__(kSampThreads) void sample_kernel(
   int k = top_k ? top_k[row] : 0;
   if (k >= V) k = 0;
   if (k > 0) {
-    sample_topk(s, out_tokens, lr, V, vec, row, temp, min(k, kCand), pp, seed, st);
+    sample_topk<U>(s, out_tokens, lr, V, vec, row, temp, min(k, kCand), pp, seed, st);
   } else {
-    sample_topp_full(s, out_tokens, lr, V, vec, row, temp, pp, seed, st);
+    sample_topp_full<U>(s, out_tokens, lr, V, vec, row, temp, pp, seed, st);
   }
 }
 
@@ -530,9 +539,19 @@ int launch_sample(int* out_tokens, const void* logits, int B, int V, int ld,
                   const float* temperature, const int* top_k, const float* top_p,
                   uint64_t seed, const int64_t* step, hipStream_t st) {
   if (B == 0) return 0;
-  hipLaunchKernelGGL(sample_kernel, dim3(B), dim3(kSampThreads), 0, st, out_tokens,
-                     (const bf16_t*)logits, V, ld, temperature, top_k, top_p,
-                     seed, step);
+  // two workgroups per CU by default: B = 1024, V = 128k, top-k 64 / top-p 0.95 in 76.5 vs
+  // 106.0 us, greedy 44.8 vs 58.1, full-vocabulary top-p 179 vs 237 (profiles/r3v);
+  // DRTC_SAMPLER_OCC=1 restores one per CU
+  static const int occ = [] {
+    const char* e = getenv("DRTC_SAMPLER_OCC");
+    return e && e[0] == '1' ? 1 : 2;
+  }();
+  if (occ == 2)
+    hipLaunchKernelGGL(sample_kernel<2>, dim3(B), dim3(kSampThreads), 0, st, out_tokens,
+                       (const bf16_t*)logits, V, ld, temperature, top_k, top_p, seed, step);
+  else
+    hipLaunchKernelGGL(sample_kernel<1>, dim3(B), dim3(kSampThreads), 0, st, out_tokens,
+                       (const bf16_t*)logits, V, ld, temperature, top_k, top_p, seed, step);
   return (int)hipGetLastError();
 }
 
