@@ -13,6 +13,7 @@ All expose ``generate(prompts, params, timeout) -> list[str]`` - the role of
 """
 from __future__ import annotations
 
+import asyncio
 import itertools
 import logging
 import multiprocessing as mp
@@ -439,8 +440,6 @@ class ReplicaRouter:
     async def agenerate(self, prompt, params, timeout=None):
         """ReplicaRouter.generate for one prompt as a coroutine (same re-dispatch on a lost
         replica, same abort on timeout), without a thread blocked per request."""
-        import asyncio
-
         loop = asyncio.get_running_loop()
         pool = self.pool
         deadline = None if timeout is None else time.monotonic() + timeout

@@ -15,6 +15,7 @@ Port 50055 and the thread-pool server match the reference.
 """
 from __future__ import annotations
 
+import asyncio
 import argparse
 import logging
 import signal
@@ -103,8 +104,6 @@ class AioServer:
     switching under the GIL.  ``stop(grace)`` mirrors grpc.Server.stop."""
 
     def __init__(self, backend, port: int, bind: str, params=None):
-        import asyncio
-
         self.loop = asyncio.new_event_loop()
         self._ready = threading.Event()
         self._err = None
@@ -117,8 +116,6 @@ class AioServer:
             raise self._err
 
     def _run(self, backend, port, bind, params):
-        import asyncio
-
         asyncio.set_event_loop(self.loop)
 
         async def start():
@@ -139,8 +136,6 @@ class AioServer:
         self.loop.run_forever()
 
     def stop(self, grace=None) -> threading.Event:
-        import asyncio
-
         done = threading.Event()
         if self._server is not None:
             fut = asyncio.run_coroutine_threadsafe(self._server.stop(grace), self.loop)

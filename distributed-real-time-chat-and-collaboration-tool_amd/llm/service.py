@@ -9,6 +9,7 @@ thread pool and meet in the engine's continuous batch.
 """
 from __future__ import annotations
 
+import asyncio
 import logging
 import time
 
@@ -159,8 +160,6 @@ class AsyncLLMServicer(LLMServicer):
     an ``agenerate`` coroutine run ``generate`` on the loop's default executor."""
 
     async def _agen(self, feature: str, prompt: str, params: SamplingParams, context=None) -> str:
-        import asyncio
-
         t0 = time.perf_counter()
         timeout = self.timeout
         left = context.time_remaining() if context is not None else None
@@ -190,8 +189,6 @@ class AsyncLLMServicer(LLMServicer):
 
     async def GetLLMAnswer(self, request, context):
         """Ask-AI with the retry + backoff of LLMServicer.GetLLMAnswer (asyncio sleeps)."""
-        import asyncio
-
         prompt = P.answer_prompt(request.query, list(request.context))
         empty = False
         for attempt in range(self.answer_retries):
