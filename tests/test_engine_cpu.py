@@ -445,3 +445,26 @@ def test_pipelined_decode_continues_across_staggered_finishes():
     assert all(len(o) == 6 + 2 * i for i, o in enumerate(pipe))
     # a finish every other step: most decode steps stay pipelined
     assert st_pipe["decode_steps_pipelined"] >= st_pipe["decode_steps"] // 2, st_pipe
+
+
+def test_request_wait_races_finish():
+    """The completion Event is created by the first wait(): a finish that happens before,
+    during or after that creation always wakes (or short-circuits) the waiter."""
+    import threading
+
+    from drtc_amd.engine.request import Request
+
+    for trial in range(500):
+        r = Request([1])
+        res = []
+        th = threading.Thread(target=lambda: res.append(r.wait(10)))
+        if trial % 2:
+            th.start()
+            r.mark_finished("stop")
+        else:
+            r.mark_finished("stop")
+            th.start()
+        th.join(20)
+        assert res == [True] and r.finish_reason == "stop"
+    r = Request([1])
+    assert r.wait(0.01) is False  # not finished: times out
