@@ -262,6 +262,19 @@ def main() -> None:
     else:
         device = torch.device("cpu")
 
+    # self-verification of the multi-GPU run: which device every rank drives, over which
+    # collective backend, in a communicator of how many ranks.  Under nccl (RCCL) every rank
+    # must own a distinct GPU; rehearsals that time-share one GPU run on gloo.
+    backend = dist.get_backend() if world > 1 else "none"
+    rccl_world = dist.get_world_size() if world > 1 else 1
+    devices = [device.index if device.type == "cuda" else -1]
+    if world > 1:
+        devices = [None] * world
+        dist.all_gather_object(devices, device.index if device.type == "cuda" else -1)
+        if backend == "nccl" and len(set(devices)) != world:
+            log(rank, f"error: ranks share a GPU under nccl: devices {devices}")
+            sys.exit(3)
+
     cfg = get_config(args.model)
     t0 = time.perf_counter()
     tp = args.tp
@@ -369,13 +382,18 @@ def main() -> None:
             "dtype": "bf16",
             "data": f"synthetic chat logs ({n_hist}-message {args.workload} contexts), random-init weights",
             "config": {"model": cfg.name, "global_batch": args.batch * (world // tp),
-                       "seq_len": args.max_new_tokens,
+                       # tokens per sequence: the average prompt plus the generated tokens
+                       "seq_len": round(prompt_tokens / (args.batch * (world // tp) * args.steps)
+                                        + args.max_new_tokens),
                        "parallelism": f"tp{tp}" if tp > 1 else f"dp{world}",
                        "max_new_tokens": args.max_new_tokens,
                        "avg_prompt_tokens": round(prompt_tokens / (args.batch * (world // tp) * args.steps), 1),
                        "sampling": "greedy" if args.greedy else
                        f"t={params.temperature},top_k={params.top_k},top_p={params.top_p}",
                        "graphs": not args.no_graphs},
+            "devices": devices,
+            "backend": backend,
+            "rccl_world": rccl_world,
             "p50_latency_ms": round(1000 * p50, 1),
             "p99_latency_ms": round(1000 * p99, 1),
             "p50_ttft_ms": round(1000 * ttft50, 1),

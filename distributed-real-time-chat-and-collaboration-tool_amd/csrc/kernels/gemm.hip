@@ -696,7 +696,7 @@ int launch_gemm(void* c, const void* a, const void* b, const void* r, int M, int
                 int group_m, void* slab, int64_t slab_bytes, int* counters, int n_counters,
                 hipStream_t st) {
   // shape contract (checked here so a bad call never reaches the device)
-  if (variant >= 7 && variant <= 15)
+  if ((variant >= 7 && variant <= 15) || variant == 31)
     return launch_gemm_w4(c, a, b, r, M, N, K, lda, ldb, ldc, ldr, epi, up_off, splitk, group_m,
                           slab, slab_bytes, counters, n_counters, variant - 7, st);
   const bool glu = epi == EPI_SILU || epi == EPI_GELU;

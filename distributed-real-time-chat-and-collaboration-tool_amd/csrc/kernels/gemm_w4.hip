@@ -89,6 +89,7 @@ struct W4Params {
   int tiles_m, tiles_n, splitk, kt_split;
   int up_off;
   int group_m;
+  int xk;  // K-slice-by-XCD tile order (split-K forms; see gemm_w4_kernel)
 };
 
 template <int EPI>
@@ -641,8 +642,18 @@ __global__ __launch_bounds__(kW4Threads, 1) void gemm_w4_kernel(W4Params p) {
   const int nwg = gridDim.x, orig = blockIdx.x;
   const int xcd = orig & 7, qq = nwg >> 3, rmd = nwg & 7;
   const int wgid = (xcd < rmd ? xcd * (qq + 1) : rmd * (qq + 1) + (xcd - rmd) * qq) + (orig >> 3);
-  const int slice = kPers ? 0 : wgid % p.splitk;
+  int slice = kPers ? 0 : wgid % p.splitk;
   int tt = kPers ? wgid : wgid / p.splitk;
+  if (!kPers && p.xk) {
+    // K-slice-by-XCD order (split-K decode shapes): the 8 block labels b % 8 (one XCD each
+    // under round-robin dispatch - speed only, the map is a bijection of blockIdx) split into
+    // splitk slices x (8 / splitk) tile subsets, so an XCD's 32 workgroups stream ONE K slice
+    // of a compact block of tiles: its L2 holds a quarter of the operand panels the
+    // tile-major order needs.  Host contract: splitk | 8, nwg % 8 == 0, ntiles % (8/splitk) == 0.
+    const int per = nwg >> 3;
+    slice = xcd % p.splitk;
+    tt = (xcd / p.splitk) * per + (orig >> 3);
+  }
   const int ntiles = p.tiles_m * p.tiles_n;
   int tm, tn;
   w4_tile_of(p, tt, tm, tn);
@@ -673,7 +684,11 @@ __global__ __launch_bounds__(kW4Threads, 1) void gemm_w4_kernel(W4Params p) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  const int kst = 0;  // K tiles may run in a rotated order kst, kst + 1, ... (mod nk)
+  // K tiles may run in a rotated order kst, kst + 1, ... (mod nk).  V & 16 (persistent form):
+  // each XCD label b % 8 starts at its own eighth of K, so the eight XCDs reach their tile
+  // seams (the epilogue's store burst, 4 MiB per XCD) at different times while the 32
+  // workgroups of one XCD still stream the same K tile through its L2 in lockstep.
+  const int kst = (V & 16) ? ((orig & 7) * nk) >> 3 : 0;
   const unsigned k0b = (unsigned)kst * 128u, k1b = (unsigned)(kst + 1 < nk ? kst + 1 : 0) * 128u;
   // ---- prologue: tiles 0 and 1 into stages 0 and 1
 #pragma unroll
@@ -718,14 +733,18 @@ __global__ __launch_bounds__(kW4Threads, 1) void gemm_w4_kernel(W4Params p) {
       // starts the accumulators from 0 (MFMA with a zero C operand: no separate zeroing of the
       // 256 AGPRs, which hipcc would hoist above the previous tile's epilogue and spill).
       {
-        const int t2 = 2 < nk ? 2 : (more ? 2 - nk : nk - 1);
+        int t2 = 2 < nk ? 2 : (more ? 2 - nk : nk - 1);
+        t2 += kst;
+        t2 -= t2 >= nk ? nk : 0;
         const W4Dma dd = w4_pick(2 < nk || !more, d, dn);
         w4_tile<V, true, true, true>(acc, fa0, fb0, fa1, fb1, lds, (par & 1) * kW4Stage, ra0, ra1,
                                      rb0, rb1, dd, t2, seam);
       }
       for (int t = 1; t < nk; ++t) {
         const bool own = t + 2 < nk;
-        const int t2 = own ? t + 2 : (more ? t + 2 - nk : nk - 1);
+        int t2 = own ? t + 2 : (more ? t + 2 - nk : nk - 1);
+        t2 += kst;
+        t2 -= t2 >= nk ? nk : 0;
         const W4Dma dd = w4_pick(own || !more, d, dn);
         w4_tile<V, true, true>(acc, fa0, fb0, fa1, fb1, lds, ((t + par) & 1) * kW4Stage, ra0, ra1,
                                rb0, rb1, dd, t2);
@@ -780,6 +799,7 @@ template <int EPI, int V>
 int w4_launch_v(const W4Params& p, hipStream_t st) {
   int nwg = p.tiles_m * p.tiles_n * p.splitk;
   if constexpr ((V & 8) != 0) nwg = min(nwg, w4_num_cus());
+  if constexpr ((V & 16) != 0) nwg -= nwg & 7;  // whole XCD rounds (>= 8: launcher contract)
   hipLaunchKernelGGL((gemm_w4_kernel<EPI, V>), dim3(nwg), dim3(kW4Threads), kW4Lds, st, p);
   return (int)hipGetLastError();
 }
@@ -797,6 +817,7 @@ int w4_launch(const W4Params& p, int v, hipStream_t st) {
     case 6: return w4_launch_v<EPI, 6>(p, st);
     case 7: return w4_launch_v<EPI, 7>(p, st);
     case 8: return w4_launch_v<EPI, 8>(p, st);
+    case 24: return w4_launch_v<EPI, 24>(p, st);
     default: return -1;
   }
 }
@@ -810,7 +831,8 @@ template <int EPI>
 int w4_cfg() {
   return w4_cfg_one<EPI, 0>() | w4_cfg_one<EPI, 1>() | w4_cfg_one<EPI, 2>() |
          w4_cfg_one<EPI, 3>() | w4_cfg_one<EPI, 4>() | w4_cfg_one<EPI, 5>() |
-         w4_cfg_one<EPI, 6>() | w4_cfg_one<EPI, 7>() | w4_cfg_one<EPI, 8>();
+         w4_cfg_one<EPI, 6>() | w4_cfg_one<EPI, 7>() | w4_cfg_one<EPI, 8>() |
+         w4_cfg_one<EPI, 24>();
 }
 
 }  // namespace
@@ -856,18 +878,28 @@ int launch_gemm_w4(void* c, const void* a, const void* b, const void* r, int M, 
     p.tiles_n = N / 256;
     p.splitk = splitk;
     p.kt_split = K / 64 / splitk;
+    if (group_m < 0) {
+      const int64_t tiles = (int64_t)p.tiles_m * p.tiles_n;
+      if (8 % splitk || (tiles * splitk) % 8 || tiles % (8 / splitk)) return -1;
+      p.xk = 1;
+      group_m = -group_m;
+    }
     p.group_m = group_m < 1 ? 4 : group_m;
     return w4_launch<W4_PARTIAL>(p, v, st);
   }
   if (glu ? (N % 128 || up_off != N) : (N % 256)) return -1;
   // persistent form (v & 8): one slice, and two K tiles per tile for the cross-tile prefetch
-  if ((v & 8) && (v != 8 || splitk != 1 || K / 64 < 2)) return -1;
+  if ((v & 8) && ((v != 8 && v != 24) || splitk != 1 || K / 64 < 2)) return -1;
+  if (v == 24 && (int64_t)((M + 255) / 256) * (glu ? N / 128 : N / 256) < 8) return -1;
   if (lda % 8 || ldb % 8 || (glu ? ldc % 4 : ldc % 8)) return -1;
   if (res && (ldr % 8 || r == nullptr || (uintptr_t)r % 16)) return -1;
   if ((uintptr_t)a % 16 || (uintptr_t)b % 16 || (uintptr_t)c % (glu ? 8 : 16)) return -1;
   // 32-bit buffer offsets: every staged row must sit within 2 GiB of its operand base
   if ((int64_t)min(M, 256) * lda * 2 >= (1ll << 31)) return -1;
   if ((int64_t)(glu ? up_off + 128 : 256) * ldb * 2 >= (1ll << 31)) return -1;
+  // group_m < 0: K-slice-by-XCD order with row groups of -group_m (split-K forms only)
+  const bool xk = group_m < 0;
+  if (xk) group_m = -group_m;
   if (group_m < 1) group_m = 8;
   W4Params p{};
   p.c = (bf16_t*)c;
@@ -882,6 +914,12 @@ int launch_gemm_w4(void* c, const void* a, const void* b, const void* r, int M, 
   p.kt_split = K / 64 / splitk;
   p.up_off = up_off;
   p.group_m = group_m;
+  if (xk) {
+    const int64_t tiles = (int64_t)p.tiles_m * p.tiles_n;
+    if ((v & 8) || splitk < 1 || 8 % splitk || (tiles * splitk) % 8 || tiles % (8 / splitk))
+      return -1;
+    p.xk = 1;
+  }
   if (epi >= W4_RESIDUAL_SQ) p.slab = (float*)slab;
   if (splitk > 1) {
     const int64_t tiles = (int64_t)p.tiles_m * p.tiles_n;

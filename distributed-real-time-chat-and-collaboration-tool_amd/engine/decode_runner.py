@@ -94,6 +94,11 @@ class DecodeRunner:
         self._pending: list[dict] = []
         self._step_no = 0
         self.redo_steps = 0
+        # host mirror of ``step_ctr`` (the sampler's RNG stream position): every executed
+        # _forward advances it by one - eager steps, capture warm-ups and graph replays
+        # alike (a capture records the add without running it) - so a redone step can be
+        # given exactly the counter value its first run sampled with
+        self._ctr = 0
 
     # ------------------------------------------------------------------
     def bucket(self, n: int) -> int:
@@ -128,6 +133,8 @@ class DecodeRunner:
         ops.sample(logits, self.temp[:Bb], self.topk[:Bb], self.topp[:Bb], seed=self.seed,
                    step=self.step_ctr, out=self.out[:Bb])
         self.step_ctr.add_(1)
+        if not (self.device.type == "cuda" and torch.cuda.is_current_stream_capturing()):
+            self._ctr += 1
 
     def capture(self, Bb: int) -> None:
         if not self.use_graphs or Bb in self._graphs:
@@ -201,16 +208,18 @@ class DecodeRunner:
             ev0 = torch.cuda.Event(enable_timing=True)
             ev1 = torch.cuda.Event(enable_timing=True)
             ev0.record()
+        ctr = self._ctr  # the RNG counter this step samples with
         with tracing.span("decode.graph_replay" if g is not None else "decode.eager", bucket=Bb):
             if g is not None:
                 g.replay()
+                self._ctr += 1
             else:
                 self._forward(Bb)
         if timing:
             ev1.record()
             self._timing[k] = (ev0, ev1)
         self._readback(n, k)
-        self._pending.append({"n": n, "k": k, "Bb": Bb, "step": self._step_no})
+        self._pending.append({"n": n, "k": k, "Bb": Bb, "step": self._step_no, "ctr": ctr})
         del self._pending[:-2]  # two staging sets: at most two steps in flight
         self._step_no += 1
         return n, k
@@ -234,6 +243,7 @@ class DecodeRunner:
         if self.device.type == "cuda":
             torch.cuda.synchronize(self.device)
         B = self.max_batch
+        saved = self._ctr
         for j, p in enumerate(self._pending[i:]):
             n, k = p["n"], p["k"]
             if j == 0:
@@ -242,12 +252,15 @@ class DecodeRunner:
             self.i32.copy_(self.h_i32[k])
             self.i64.copy_(self.h_i64[k])
             self.f32.copy_(self.h_f32[k])
-            self.step_ctr.fill_(p["step"])
+            # the counter value of the step's first run: the redo samples the same RNG
+            # stream, so the tokens never depend on the capacity
+            self.step_ctr.fill_(p["ctr"])
             with worst_case_capacity(), tracing.span("decode.ep_redo", bucket=p["Bb"]):
                 self._forward(p["Bb"])
             self._readback(n, k)
             self.redo_steps += 1
-        self.step_ctr.fill_(self._step_no)
+        self.step_ctr.fill_(saved)
+        self._ctr = saved
         if self.device.type == "cuda":
             torch.cuda.synchronize(self.device)
 

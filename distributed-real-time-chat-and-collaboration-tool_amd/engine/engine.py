@@ -90,7 +90,8 @@ class LLMEngine:
                                    use_graphs=use_graphs, seed=seed, buckets=buckets)
         self.seed = seed
         self._prefill_step = 0
-        self._h_ovf: dict[int, torch.Tensor] = {}  # EP dropped-pair counts per prefill launch
+        # EP dropped-pair count and sampler step per prefill launch
+        self._h_ovf: dict[int, tuple[torch.Tensor, int]] = {}
         # slot state
         self.bt = np.zeros((max_batch, self.max_blocks), dtype=np.int32)
         self.ctx = np.zeros(max_batch, dtype=np.int32)        # tokens in the KV cache
@@ -389,14 +390,15 @@ class LLMEngine:
         chunk's forward dropped (token, expert) pairs on any EP rank, run it
         again at worst-case capacity (same KV slots, same requests; chunks are
         independent, so the chunks launched after it stay valid)."""
-        ovf = self._h_ovf.pop(id(h_tok), None)
-        if ovf is None or int(ovf[0]) == 0:
+        ent = self._h_ovf.pop(id(h_tok), None)
+        if ent is None or int(ent[0][0]) == 0:
             return h_tok
         from ..parallel.expert_parallel import worst_case_capacity
 
-        self._prefill_step -= 1  # same sampling stream as the first run
+        # the step counter this chunk's first run sampled with (chunks launched after it
+        # advanced the counter already): the redo draws from the same stream
         with worst_case_capacity():
-            _, _, h_tok, ev = self._launch_prefill(batch, n_dec=n_dec)
+            _, _, h_tok, ev = self._launch_prefill(batch, n_dec=n_dec, step=ent[1])
         if ev is not None:
             ev.synchronize()
         self._h_ovf.pop(id(h_tok), None)
@@ -405,11 +407,12 @@ class LLMEngine:
         self.stats["ep_redo_steps"] = self.stats.get("ep_redo_steps", 0) + 1
         return h_tok
 
-    def _launch_prefill(self, batch: list[Request], n_dec: int = 0):
+    def _launch_prefill(self, batch: list[Request], n_dec: int = 0, step: int | None = None):
         """Enqueue one packed prefill of ``batch``.  ``n_dec > 0`` makes it a
         mixed step: one decode row per running slot 0..n_dec-1 (padded to the
         decode bucket) rides in the same forward pass - same GEMM launches,
-        paged attention for those rows - and is sampled with the prefill rows."""
+        paged attention for those rows - and is sampled with the prefill rows.  ``step``:
+        the sampler's step counter for a redo (default: the next one)."""
         dev = self.device
         cuda = dev.type == "cuda"
         # host metadata, vectorised over the batch (a 1024-prompt prefill is
@@ -450,7 +453,9 @@ class LLMEngine:
         seg_blk = blk_tab[s_seq, s_j].astype(np.int32)
         last_idx = np.asarray(cu[1:], dtype=np.int64) - 1
         ts, tq = ops.prefill_tiles(cu)
-        self._prefill_step += 1
+        if step is None:
+            self._prefill_step += 1
+            step = self._prefill_step
         params = np.array([(r.params.temperature, r.params.top_p, r.params.top_k) for r in batch],
                           dtype=np.float64).reshape(nseq, 3)
         dec_i32 = []
@@ -481,7 +486,7 @@ class LLMEngine:
             np.asarray(tq, np.int32), seg_tok, seg_len, seg_blk,
             params[:, 2].astype(np.int32)] + dec_i32))
         h_i64 = torch.from_numpy(np.concatenate([
-            slots, last_idx, np.array([self._prefill_step + (1 << 40)], dtype=np.int64)]))
+            slots, last_idx, np.array([step + (1 << 40)], dtype=np.int64)]))
         h_f32 = torch.from_numpy(params[:, :2].T.astype(np.float32).reshape(-1))
         if cuda:  # pinned staging: the copies stay asynchronous to the host
             h_i32, h_i64, h_f32 = h_i32.pin_memory(), h_i64.pin_memory(), h_f32.pin_memory()
@@ -510,17 +515,17 @@ class LLMEngine:
                            tiles=(d_ts, d_tq), last_idx=t_i64[R:R + ns_all],
                            v_segs=None if n_dec else d_segs, decode=dmeta, n_prefill=Tp,
                            max_len=int(lens_a.max()))
-        step = t_i64[R + ns_all:R + ns_all + 1]
+        d_step = t_i64[R + ns_all:R + ns_all + 1]
         temp, topp = t_f32[:ns_all], t_f32[ns_all:]
         logits = self.model.forward_prefill(d_ids, meta, self.kv)
-        toks = ops.sample(logits, temp, topk, topp, seed=self.seed, step=step)
+        toks = ops.sample(logits, temp, topk, topp, seed=self.seed, step=d_step)
         h_tok = torch.empty(ns_all, dtype=torch.int32, pin_memory=cuda)
         h_tok.copy_(toks, non_blocking=cuda)
         ovf = getattr(self.model, "ep_overflow", None)
         if ovf is not None:  # EP dropped-pair count, read with the tokens
             h_ovf = torch.empty(1, dtype=torch.int32, pin_memory=cuda)
             h_ovf.copy_(ovf.count, non_blocking=cuda)
-            self._h_ovf[id(h_tok)] = h_ovf
+            self._h_ovf[id(h_tok)] = (h_ovf, step)
         ev = None
         if cuda:
             ev = torch.cuda.Event()

@@ -10,6 +10,13 @@ on-node inference:
                      ``--tp N`` runs one tensor-parallel engine over N GPUs
                      (RCCL all-reduce over xGMI), e.g. Llama-3-70B TP=8;
   --backend scripted deterministic format-correct text (no model; CPU tests).
+  --serve FEATURE=MODEL[@GPUS][:tpN] (repeatable) hosts one engine group per feature
+                     on its own GPUs of the node: the per-feature model matrix of
+                     BASELINE.json (Gemma-2B smart reply, Llama-3-8B summarize,
+                     Llama-3-70B TP=8 ask-AI, Mixtral suggestions) behind ONE service
+                     address, e.g. --serve smart=gemma-2b@0 --serve summary=llama-3-8b@1
+                     --serve answer=llama-3-70b@0-7:tp8 --serve suggest=mixtral-8x7b@2,3
+                     (features without a --serve use --model).
 
 Port 50055 and the thread-pool server match the reference.
 """
@@ -51,8 +58,9 @@ def default_max_batch(model: str, tp: int = 1) -> int:
     return b if tp <= 1 else max(b, 256)
 
 
-def build_backend(args):
-    if args.backend == "scripted":
+def build_backend(args, devices: list[int] | None = None):
+    """Backend of one model: ``devices`` pins its GPUs (default 0 .. gpus-1 / tp-1)."""
+    if args.backend == "scripted" or args.model == "scripted":
         return ScriptedBackend()
     from ..engine import ChatTokenizer
     from ..models import get_config
@@ -65,16 +73,16 @@ def build_backend(args):
         from ..parallel.tp_engine import TPEngineGroup
 
         return TPEngineGroup(args.model, args.tp, engine_kw, tok,
-                             custom_allreduce=args.custom_allreduce)
+                             custom_allreduce=args.custom_allreduce, devices=devices)
     import torch
 
-    n = args.gpus
+    n = len(devices) if devices else args.gpus
     if n <= 1 and (getattr(args, "in_process", False) or not torch.cuda.is_available()):
         from ..engine.engine import LLMEngine
         from ..models import TransformerLM
         from .backends import EngineBackend
 
-        dev = "cuda:0" if torch.cuda.is_available() else "cpu"
+        dev = f"cuda:{devices[0] if devices else 0}" if torch.cuda.is_available() else "cpu"
         model = TransformerLM(cfg, dev, seed=1234, full_then_shard=False)
         eng = LLMEngine(model, **engine_kw)
         eng.warmup(capture=True)
@@ -84,8 +92,69 @@ def build_backend(args):
     # engines run in their own processes (one per GPU), so the gRPC handlers,
     # prompt building and tokenization here never contend for the engine
     # loop's GIL (scripts/service_bench.py: in-process 16.4k vs 17.7k tok/s)
-    pool = WorkerPool(args.model, [f"cuda:{i}" for i in range(max(1, n))], engine_kw)
+    pool = WorkerPool(args.model, [f"cuda:{i}" for i in (devices or range(max(1, n)))], engine_kw)
     return ReplicaRouter(pool, tok, args.max_model_len)
+
+
+FEATURES = ("smart", "summary", "answer", "suggest")
+_FEATURE_ALIAS = {"smart_reply": "smart", "summarize": "summary", "ask": "answer",
+                  "suggestions": "suggest"}
+
+
+def parse_serve(spec: str) -> tuple[str, str, list[int] | None, int]:
+    """``FEATURE=MODEL[@GPUS][:tpN]`` -> (feature, model, devices or None, tp); GPUS is a
+    comma list of ids and ranges ("0", "1,2", "0-7")."""
+    feat, eq, rest = spec.partition("=")
+    feat = _FEATURE_ALIAS.get(feat.strip(), feat.strip())
+    if not eq or feat not in FEATURES or not rest:
+        raise ValueError(f"--serve {spec!r}: expected FEATURE=MODEL[@GPUS][:tpN], "
+                         f"FEATURE in {FEATURES}")
+    tp = 1
+    if ":tp" in rest:
+        rest, _, t = rest.rpartition(":tp")
+        tp = int(t)
+    model, _, gpus = rest.partition("@")
+    devices = None
+    if gpus:
+        devices = []
+        for part in gpus.split(","):
+            a, _, b = part.partition("-")
+            devices += list(range(int(a), int(b) + 1)) if b else [int(a)]
+        if len(set(devices)) != len(devices):
+            raise ValueError(f"--serve {spec!r}: a GPU is listed twice")
+        if tp > 1 and len(devices) != tp:
+            raise ValueError(f"--serve {spec!r}: tp{tp} needs exactly {tp} GPUs")
+    return feat, model.strip(), devices, tp
+
+
+def build_feature_backends(args, specs: list[str]):
+    """One backend per distinct (model, GPUs, tp) of the ``--serve`` specs, routed per
+    feature; features without a spec share the ``--model`` backend of ``build_backend``."""
+    from .service import FeatureRouter
+
+    parsed = [parse_serve(s) for s in specs]
+    seen = set()
+    for f, *_ in parsed:
+        if f in seen:
+            raise ValueError(f"feature {f!r} given twice")
+        seen.add(f)
+    made: dict = {}
+    by_feature = {}
+    for feat, model, devices, tp in parsed:
+        key = (model, tuple(devices) if devices else None, tp)
+        if key not in made:
+            sub = argparse.Namespace(**vars(args))
+            sub.model, sub.tp = model, tp
+            sub.gpus = len(devices) if devices and tp == 1 else (1 if tp == 1 else args.gpus)
+            sub.max_batch = args.max_batch or default_max_batch(model, tp)
+            made[key] = build_backend(sub, devices=devices)
+        by_feature[feat] = made[key]
+    default = None
+    if len(by_feature) < len(FEATURES):
+        sub = argparse.Namespace(**vars(args))
+        sub.max_batch = args.max_batch or default_max_batch(args.model, args.tp)
+        default = build_backend(sub)
+    return FeatureRouter(by_feature, default)
 
 
 def serve(backend, port: int = 50055, workers: int = 64, bind: str = "[::]", params=None):
@@ -177,13 +246,24 @@ def main(argv=None):
     ap.add_argument("--frontend", choices=("threads", "aio"), default="threads",
                     help="gRPC front-end: a handler thread per in-flight RPC, or grpc.aio "
                          "coroutines on one event-loop thread")
+    ap.add_argument("--serve", action="append", default=[], metavar="FEATURE=MODEL[@GPUS][:tpN]",
+                    help="host FEATURE (smart | summary | answer | suggest) on its own engine "
+                         "group (repeatable; see the module docstring)")
     ap.add_argument("--log-level", default="INFO")
     args = parse_with_config(ap, argv)
     setup_logging(args.log_level)
-    if not args.max_batch:
-        args.max_batch = default_max_batch(args.model, args.tp)
-    backend = build_backend(args)
-    workers = args.workers or args.max_batch * max(1, args.gpus) + 16
+    if args.serve:
+        backend = build_feature_backends(args, args.serve)
+        # a handler thread per request any of the engine groups can hold at once
+        groups = {(m, tuple(d or ()), tp) for _, m, d, tp in map(parse_serve, args.serve)}
+        slots = sum((args.max_batch or default_max_batch(m, tp)) * (len(d) if d and tp == 1 else 1)
+                    for m, d, tp in groups)
+        workers = args.workers or slots + 16
+    else:
+        if not args.max_batch:
+            args.max_batch = default_max_batch(args.model, args.tp)
+        backend = build_backend(args)
+        workers = args.workers or args.max_batch * max(1, args.gpus) + 16
     server = (serve_aio(backend, args.port) if args.frontend == "aio"
               else serve(backend, args.port, workers))
     log.info("LLM server on port %d (backend=%s model=%s gpus=%d tp=%d)", args.port, args.backend,

@@ -36,6 +36,43 @@ class FeatureParams:
         self.suggest = SamplingParams(max_new_tokens=96, **sdk)
 
 
+def _backend_for(backend, feature: str):
+    """The backend serving ``feature`` (a FeatureRouter hosts one per feature)."""
+    route = getattr(backend, "route", None)
+    return route(feature) if route is not None else backend
+
+
+class FeatureRouter:
+    """One LLM service hosting several models: each feature ("smart", "summary", "answer",
+    "suggest") is served by its own backend (an engine replica pool or a TP group on its
+    share of the node's GPUs), as BASELINE.json assigns a model per feature.  Backends
+    shared by several features are listed once in ``backends``."""
+
+    FEATURES = ("smart", "summary", "answer", "suggest")
+    ALIAS = {"smart_reply": "smart", "summarize": "summary", "ask": "answer"}
+
+    def __init__(self, by_feature: dict, default=None):
+        self.by_feature = dict(by_feature)
+        self.default = default
+        missing = [f for f in self.FEATURES if f not in self.by_feature and default is None]
+        if missing:
+            raise ValueError(f"no backend for features {missing}")
+        uniq = {id(b): b for b in list(self.by_feature.values()) + [default] if b is not None}
+        self.backends = list(uniq.values())
+
+    def route(self, feature: str):
+        return self.by_feature.get(self.ALIAS.get(feature, feature), self.default)
+
+    def generate(self, prompts, params, timeout=None):  # feature-less callers: the default
+        return (self.default or self.by_feature["smart"]).generate(prompts, params, timeout=timeout)
+
+    def close(self) -> None:
+        for b in self.backends:
+            c = getattr(b, "close", None)
+            if c is not None:
+                c()
+
+
 class LLMServicer:
     def __init__(self, backend, params: FeatureParams | None = None, timeout: float = 60.0,
                  answer_retries: int = 3, answer_backoff: float = 1.0):
@@ -56,7 +93,8 @@ class LLMServicer:
         left = context.time_remaining() if context is not None else None
         if left is not None:
             timeout = min(timeout, max(0.05, left))
-        text = self.backend.generate([prompt], [params], timeout=timeout)[0]
+        text = _backend_for(self.backend, feature).generate([prompt], [params],
+                                                            timeout=timeout)[0]
         METRICS.observe(f"llm.{feature}.latency_s", time.perf_counter() - t0)
         METRICS.inc(f"llm.{feature}.requests")
         return text
@@ -165,13 +203,14 @@ class AsyncLLMServicer(LLMServicer):
         left = context.time_remaining() if context is not None else None
         if left is not None:
             timeout = min(timeout, max(0.05, left))
-        agen = getattr(self.backend, "agenerate", None)
+        backend = _backend_for(self.backend, feature)
+        agen = getattr(backend, "agenerate", None)
         if agen is not None:
             text = await agen(prompt, params, timeout=timeout)
         else:
             loop = asyncio.get_running_loop()
             text = (await loop.run_in_executor(
-                None, lambda: self.backend.generate([prompt], [params], timeout=timeout)))[0]
+                None, lambda: backend.generate([prompt], [params], timeout=timeout)))[0]
         METRICS.observe(f"llm.{feature}.latency_s", time.perf_counter() - t0)
         METRICS.inc(f"llm.{feature}.requests")
         return text

@@ -452,7 +452,7 @@ def save_entries(entries: dict[str, dict], path: str | None = None) -> str:
 
 
 def gemm_w4_variant(variant: int) -> bool:
-    return 7 <= variant <= 15
+    return 7 <= variant <= 15 or variant == 31
 
 
 # ------------------------------------------------------------ folded RMSNorm (prefill)

@@ -73,7 +73,13 @@ def sample(logits: torch.Tensor, temperature: torch.Tensor | None = None,
     temperature/top_k/top_p are per-row device tensors (float32 / int32 /
     float32); ``step`` is an int64 device scalar the caller advances."""
     if not on_gpu(logits):
-        r = sample_ref(logits, temperature, top_k, top_p)
+        # counter-based like the HIP sampler: the draws are a function of (seed, step), so a
+        # step re-run with the same counter (EP capacity redo) draws the same tokens
+        gen = None
+        if step is not None:
+            gen = torch.Generator().manual_seed(
+                (seed * 0x9E3779B1 + int(step.reshape(-1)[0])) & 0x7FFFFFFFFFFFFFFF)
+        r = sample_ref(logits, temperature, top_k, top_p, generator=gen)
         if out is not None:
             out.copy_(r)
             return out

@@ -32,8 +32,22 @@ def _free_port() -> int:
     return p
 
 
+def check_devices(devices: list[int], device_count: int, can_access) -> None:
+    """A TP group needs one distinct GPU per rank, every pair peer-accessible over xGMI (the
+    IPC all-reduce maps peer memory; RCCL uses the same links).  Raises on a violation.
+    ``can_access(a, b)``: torch.cuda.can_device_access_peer (hipDeviceCanAccessPeer)."""
+    if len(set(devices)) != len(devices):
+        raise RuntimeError(f"TP ranks share a device: {devices}")
+    bad = [d for d in devices if not 0 <= d < device_count]
+    if bad:
+        raise RuntimeError(f"TP devices {bad} out of range (device_count={device_count})")
+    missing = [(a, b) for a in devices for b in devices if a != b and not can_access(a, b)]
+    if missing:
+        raise RuntimeError(f"no peer access between GPUs {missing[:4]} (hipDeviceCanAccessPeer)")
+
+
 def tp_worker(rank: int, world: int, port: int, model_name: str, engine_kw: dict, inq, outq,
-              custom_ar: bool = True):
+              custom_ar: bool = True, devices: list[int] | None = None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
     import torch
@@ -46,7 +60,16 @@ def tp_worker(rank: int, world: int, port: int, model_name: str, engine_kw: dict
     try:
         init_distributed()
         cpu = dist.new_group(backend="gloo")
-        dev = torch.device("cuda", rank) if torch.cuda.is_available() else torch.device("cpu")
+        devices = list(devices) if devices is not None else list(range(world))
+        dev = torch.device("cpu")
+        if torch.cuda.is_available():
+            n = torch.cuda.device_count()
+            if n >= world:
+                # one process per GPU over distinct, mutually peer-accessible devices
+                check_devices(devices, n, torch.cuda.can_device_access_peer)
+                dev = torch.device("cuda", devices[rank])
+            else:  # rehearsal: ranks time-share the GPUs (gloo / IPC on one card)
+                dev = torch.device("cuda", devices[rank] % n)
         pc = ParallelContext.from_world(tp=True)
         if custom_ar and dev.type == "cuda":
             pc.enable_custom_allreduce()
@@ -125,14 +148,15 @@ class TPEngineGroup:
     """Front-end handle: generate() on a TP group of ``world`` GPUs."""
 
     def __init__(self, model_name: str, world: int, engine_kw: dict, tokenizer,
-                 start_timeout: float = 1800, custom_allreduce: bool = True):
+                 start_timeout: float = 1800, custom_allreduce: bool = True,
+                 devices: list[int] | None = None):
         ctx = mp.get_context("spawn")
         self.inq, self.outq = ctx.Queue(), ctx.Queue()
         port = _free_port()
         self.procs = [ctx.Process(target=tp_worker, daemon=True,
                                   args=(r, world, port, model_name, engine_kw,
                                         self.inq if r == 0 else None, self.outq if r == 0 else None,
-                                        custom_allreduce))
+                                        custom_allreduce, devices))
                       for r in range(world)]
         for p in self.procs:
             p.start()

@@ -244,7 +244,14 @@ class NativeStorage:
         if skip > 0:  # finish an interrupted compaction
             self._rewrite(st["snap_index"] + 1, self.entries)
         self._state = dict(st)
-        self._durable = (st.get("current_term"), st.get("voted_for"))
+        # durable = what the fsynced hard-state file holds.  A data directory from before that
+        # file existed (term / vote only in the state pickle, which save_state now rewrites
+        # without fsync) has none: leave _durable unset so the first save_state writes and
+        # fsyncs the hard state before the unsynced pickle rewrite could tear the only copy
+        if hard is not None and (st.get("current_term"), st.get("voted_for")) == hard:
+            self._durable = hard
+        else:
+            self._durable = (None, None)
         return st, list(self.entries)
 
     def append(self, entries) -> None:

@@ -80,6 +80,10 @@ def main(argv=None) -> None:
     ap.add_argument("--data-root", default=".")
     ap.add_argument("--storage", choices=("native", "pickle"), default="native")
     ap.add_argument("--llm", default="localhost:50055", help="LLM service address ('' disables)")
+    for feat, rpc in (("smart", "GetSmartReply"), ("summary", "SummarizeConversation"),
+                      ("ask", "GetLLMAnswer"), ("suggest", "GetContextSuggestions")):
+        ap.add_argument(f"--llm-{feat}", default=None,
+                        help=f"LLM service address for {rpc} (default: --llm)")
     ap.add_argument("--election-timeout", default="1.5,3.0", help="min,max seconds")
     ap.add_argument("--reference-timing", action="store_true", help="10-15 s election timeout")
     ap.add_argument("--heartbeat", type=float, default=0.05)
@@ -99,6 +103,8 @@ def main(argv=None) -> None:
     lo, hi = (10.0, 15.0) if a.reference_timing else tuple(float(x) for x in a.election_timeout.split(","))
     cfg = NodeConfig(node_id=a.node_id, port=a.port, peers=parse_peers(a.peers), data_root=a.data_root,
                      storage=a.storage, llm_address=a.llm or None,
+                     llm_smart=a.llm_smart, llm_summary=a.llm_summary, llm_ask=a.llm_ask,
+                     llm_suggest=a.llm_suggest,
                      raft=RaftConfig(election_timeout=(lo, hi), heartbeat_interval=a.heartbeat,
                                      local_commit=a.local_commit),
                      token_mode=a.token_mode, bcrypt_rounds=a.bcrypt_rounds, fsync=a.fsync,

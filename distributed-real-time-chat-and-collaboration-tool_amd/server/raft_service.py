@@ -80,6 +80,22 @@ class NodeConfig:
     snapshot_every: int = 0                         # compact the log every N applied entries (0: never)
     llm_timeouts: dict = field(default_factory=lambda: {
         "smart": 20.0, "summary": 10.0, "answer": 10.0, "suggest": 20.0})
+    # per-feature LLM services (None: ``llm_address``, the reference's single LLM server,
+    # ref server/raft_node.py:372).  One node can route each AI RPC to the engine group
+    # serving that feature's model (BASELINE: Gemma-2B smart reply, 8B summarize, 70B ask,
+    # Mixtral suggestions) - ref call sites :2018 / :2084 / :2126 / :2187.
+    llm_smart: str | None = None
+    llm_summary: str | None = None
+    llm_ask: str | None = None
+    llm_suggest: str | None = None
+    forward_timeout_s: float = 5.0                  # follower -> leader forwarded calls
+
+    def llm_routes(self) -> dict:
+        """feature -> LLM service address (the per-feature override or ``llm_address``)."""
+        return {"smart": self.llm_smart or self.llm_address,
+                "summary": self.llm_summary or self.llm_address,
+                "answer": self.llm_ask or self.llm_address,
+                "suggest": self.llm_suggest or self.llm_address}
 
 
 class LLMClient:
@@ -128,7 +144,11 @@ class ChatNode:
                               cfg.raft, fsync=cfg.fsync, seed_defaults=seed if local_seed else None,
                               snapshot_every=cfg.snapshot_every)
         self.state = self.rt.state
-        self.llm = LLMClient(cfg.llm_address)
+        # one client (channel + circuit breaker) per distinct address; features that share
+        # an address share its client
+        by_addr: dict = {}
+        self.llms = {f: by_addr.setdefault(a, LLMClient(a)) for f, a in cfg.llm_routes().items()}
+        self.llm = self.llms["smart"]
         self.genesis_done = threading.Event()
         if not (cfg.seed_defaults and cfg.seed_mode == "log"):
             self.genesis_done.set()
@@ -302,11 +322,13 @@ class ChatNode:
         if not p:
             return raft_pb.StatusResponse(success=False, message="Invalid token")
         name = p["username"]
-        # replicated through the leader, like every other write (the client redirects on
-        # "Not the leader"): the token then stays invalid on every node and after failover.
-        # A follower never revokes node-locally and reports success.
+        # replicated through the leader, like every other write: the token then stays
+        # invalid on every node and after failover.  The reference logs out on ANY node
+        # (ref server/raft_node.py:1751) and its CLI neither redirects a logout nor keeps its
+        # session when one fails (client/chat_client.py:568), so a follower forwards the
+        # call to the leader; either way it drops the session and the presence locally.
         if not self.rt.is_leader():
-            return raft_pb.StatusResponse(success=False, message="Not the leader")
+            return self._forward_logout(request, name)
         err = self._propose("REVOKE_TOKEN", {"username": name,
                                              "token_hash": self._token_hash(request.token),
                                              "exp": int(p.get("exp", 0)), "ts": int(time.time())})
@@ -325,6 +347,31 @@ class ChatNode:
         if err:  # revoked on this node; the replicated revocation did not commit
             return raft_pb.StatusResponse(success=False, message=f"Logout not replicated: {err}")
         return raft_pb.StatusResponse(success=True, message="Logged out")
+
+    def _drop_session(self, token: str, name: str) -> None:
+        with self.rt.state_lock:
+            self.sessions.pop(token, None)
+            u = self.st.users.get(name)
+            if u is not None:
+                u["status"] = "offline"
+                self.st.online_users.discard(name)
+                self.st.dirty.add("users")
+
+    def _forward_logout(self, request, name: str):
+        """Logout received by a follower: relay it to the current leader (which replicates
+        the revocation to every node, this one included); the local session goes either way."""
+        info = self.rt.leader_info()
+        lid = info.get("leader_id")
+        stub = self.rt.stubs.get(lid) if lid is not None else None
+        self._drop_session(request.token, name)
+        if stub is None:
+            return raft_pb.StatusResponse(success=False,
+                                          message="Logout not replicated: no leader known")
+        try:
+            return stub.Logout(request, timeout=self.cfg.forward_timeout_s)
+        except grpc.RpcError as e:
+            return raft_pb.StatusResponse(
+                success=False, message=f"Logout not replicated: leader unreachable ({e.code().name})")
 
     # ------------------------------------------------------------ channels
     def CreateChannel(self, request, context):
@@ -620,11 +667,11 @@ class ChatNode:
         if not self._verify(request.token):
             return raft_pb.SmartReplyResponse(success=False, suggestions=[])
         recent = self._recent(request.channel_id, request.recent_message_count or 5)
-        if not self.llm.available():
+        if not self.llms["smart"].available():
             return raft_pb.SmartReplyResponse(success=True, suggestions=FB_SMART_DOWN)
         try:
             t0 = time.perf_counter()
-            r = self.llm.call("GetSmartReply", llm_pb.SmartReplyRequest(
+            r = self.llms["smart"].call("GetSmartReply", llm_pb.SmartReplyRequest(
                 request_id=str(uuid.uuid4()), recent_messages=recent), self.cfg.llm_timeouts["smart"])
             METRICS.observe("ai.smart_reply.latency_s", time.perf_counter() - t0)
             return raft_pb.SmartReplyResponse(success=True, suggestions=list(r.suggestions))
@@ -639,14 +686,14 @@ class ChatNode:
         if not recent:
             return raft_pb.SummarizeResponse(success=True, summary="No messages to summarize", key_points=[])
         parts = list({m.sender for m in recent})
-        if not self.llm.available():
+        if not self.llms["summary"].available():
             return raft_pb.SummarizeResponse(
                 success=True,
                 summary=f"Conversation with {len(recent)} messages between {', '.join(parts[:3])}",
                 key_points=[f"{len(recent)} messages exchanged", f"{len(parts)} participants",
                             "💡 Tip: Start LLM server for AI-powered summaries: python -m drtc_amd.llm.server"])
         try:
-            r = self.llm.call("SummarizeConversation", llm_pb.SummarizeRequest(
+            r = self.llms["summary"].call("SummarizeConversation", llm_pb.SummarizeRequest(
                 request_id=str(uuid.uuid4()), messages=recent, max_length=200),
                 self.cfg.llm_timeouts["summary"])
             return raft_pb.SummarizeResponse(success=True, summary=r.summary, key_points=list(r.key_points))
@@ -658,10 +705,10 @@ class ChatNode:
     def GetLLMAnswer(self, request, context):
         if not self._verify(request.token):
             return raft_pb.LLMResponse(success=False, answer="Invalid token")
-        if not self.llm.available():
+        if not self.llms["answer"].available():
             return raft_pb.LLMResponse(success=False, answer=LLM_DOWN_ANSWER)
         try:
-            r = self.llm.call("GetLLMAnswer", llm_pb.LLMRequest(
+            r = self.llms["answer"].call("GetLLMAnswer", llm_pb.LLMRequest(
                 request_id=str(uuid.uuid4()), query=request.query, context=list(request.context)),
                 self.cfg.llm_timeouts["answer"])
             return raft_pb.LLMResponse(success=True, answer=r.answer)
@@ -673,11 +720,11 @@ class ChatNode:
         if not self._verify(request.token):
             return raft_pb.ContextSuggestionsResponse(success=False, suggestions=[], topics=[])
         recent = self._recent(request.channel_id, request.context_message_count or 5)
-        if not self.llm.available():
+        if not self.llms["suggest"].available():
             s, t = FB_SUGGEST_DOWN
             return raft_pb.ContextSuggestionsResponse(success=True, suggestions=s, topics=t)
         try:
-            r = self.llm.call("GetContextSuggestions", llm_pb.ContextRequest(
+            r = self.llms["suggest"].call("GetContextSuggestions", llm_pb.ContextRequest(
                 request_id=str(uuid.uuid4()), context=recent, current_input=request.current_input),
                 self.cfg.llm_timeouts["suggest"])
             return raft_pb.ContextSuggestionsResponse(success=True, suggestions=list(r.suggestions),

@@ -58,13 +58,17 @@ def main():
             else:
                 fns[arm] = lambda: ops.linear(x, nxt())
         else:
-            v = int(arm[1:])
+            # "vV" or "vV:splitk:group_m" (group_m < 0: K-slice-by-XCD tile order)
+            f = arm[1:].split(":")
+            v = int(f[0])
+            sk = int(f[1]) if len(f) > 1 else a.splitk
+            gm = int(f[2]) if len(f) > 2 else a.group_m
             if a.epi == "residual":
-                fns[arm] = (lambda v=v: G.mfma_gemm(x, nxt(), "residual", residual=res, out=res,
-                                                    variant=v, splitk=a.splitk, group_m=a.group_m))
+                fns[arm] = (lambda v=v, sk=sk, gm=gm: G.mfma_gemm(
+                    x, nxt(), "residual", residual=res, out=res, variant=v, splitk=sk, group_m=gm))
             else:
-                fns[arm] = (lambda v=v: G.mfma_gemm(x, nxt(), a.epi, out=out, variant=v,
-                                                    splitk=a.splitk, group_m=a.group_m))
+                fns[arm] = (lambda v=v, sk=sk, gm=gm: G.mfma_gemm(
+                    x, nxt(), a.epi, out=out, variant=v, splitk=sk, group_m=gm))
     # correctness of every hand arm against an fp32 reference (one call each)
     ref = x.float() @ w.float().t()
     if a.epi == "residual":

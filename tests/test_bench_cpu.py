@@ -28,6 +28,12 @@ def _check(r: dict, n: int) -> None:
               "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config"):
         assert k in r, k
     assert r["n_gpus"] == n and r["steps"] == 1 and r["warmup"] == 0
+    # self-verification of the multi-rank run: one device entry per rank, the collective
+    # backend and the communicator size as the process group reports them
+    assert len(r["devices"]) == n and r["rccl_world"] == n
+    assert r["backend"] == ("gloo" if n > 1 else "none")
+    # seq_len = average prompt + generated tokens per sequence
+    assert r["config"]["seq_len"] == round(r["config"]["avg_prompt_tokens"] + 4)
     assert r["value"] > 0 and r["higher_is_better"] is True and r["scaling"] == "weak"
     assert r["config"]["global_batch"] == 4 * n
     assert r["config"]["parallelism"] == f"dp{n}"
@@ -100,3 +106,33 @@ def test_bench_world_size_mismatch_is_an_error():
     p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", *ARGS],
                        cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
     assert p.returncode != 0 and not [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+
+
+def _self_launch(n: int, extra: list[str]) -> dict:
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(n), *extra],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    assert p.returncode == 0, p.stderr[-3000:]
+    return _json_line(p.stdout)
+
+
+def test_bench_self_launch_tensor_parallel():
+    """`bench.py --gpus 2 --tp 2`: one TP group over both ranks (all-reduce after o / down),
+    the same requests on every rank: global batch = one replica's, scaling strong."""
+    r = _self_launch(2, ["--tp", "2", *ARGS])
+    assert r["config"]["parallelism"] == "tp2" and r["config"]["global_batch"] == 4
+    assert r["scaling"] == "strong" and r["n_gpus"] == 2 and r["rccl_world"] == 2
+    assert r["backend"] == "gloo" and len(r["devices"]) == 2
+    assert abs(r["value"] - 4 * 4 / (r["ms_per_step"] / 1000)) / r["value"] < 0.05
+
+
+def test_bench_self_launch_tp_ep_mixtral():
+    """Mixtral-shaped MoE over a 4-rank TP group with expert parallelism (the experts split
+    over the ranks, tokens exchanged by all-to-all): the path of the Mixtral EP=8 config."""
+    args = ["--steps", "1", "--warmup", "0", "--model", "tiny-mixtral", "--batch", "4",
+            "--max-new-tokens", "4", "--max-model-len", "1024", "--workload", "suggest"]
+    r = _self_launch(4, ["--tp", "4", *args])
+    assert r["config"]["parallelism"] == "tp4" and r["config"]["model"] == "tiny-mixtral"
+    assert r["rccl_world"] == 4 and len(r["devices"]) == 4
+    assert r["engine_stats"]["decode_tokens"] >= 4 * 3

@@ -280,3 +280,65 @@ def test_cli_send_checks_channel_and_history_auto_logout(cluster):
     sh.token = sh.token[:-4] + "AAAA"  # a token the server rejects
     sh.onecmd("history 5")
     assert "Your session is invalid on this server" in out.getvalue() and sh.token is None
+
+
+def test_per_feature_llm_routing(tmp_path):
+    """Each AI RPC goes to its feature's LLM service (NodeConfig.llm_smart / llm_summary /
+    llm_ask / llm_suggest): one node serving the per-feature model matrix of BASELINE.json."""
+    backends = {f: ScriptedBackend() for f in ("smart", "summary", "ask", "suggest")}
+    ports = {f: free_port() for f in backends}
+    servers = [serve_llm(b, port=ports[f], bind="127.0.0.1") for f, b in backends.items()]
+    try:
+        kw = {f"llm_{f}": f"127.0.0.1:{p}" for f, p in ports.items()}
+        with LocalCluster(3, data_root=str(tmp_path), llm_address=f"127.0.0.1:{free_port()}",
+                          **kw) as c:
+            L = c.leader()
+            s = c.stub(L)
+            tok = c.login(L)
+            s.SendMessage(raft_pb.SendMessageRequest(token=tok, channel_id="general", content="lunch?"))
+            calls = []
+            r = s.GetSmartReply(raft_pb.SmartReplyRequest(token=tok, channel_id="general"))
+            assert list(r.suggestions)[0] == "Sounds good to me"
+            calls.append({f: b.calls for f, b in backends.items()})
+            r = s.SummarizeConversation(raft_pb.SummarizeRequest(token=tok, channel_id="general"))
+            assert r.summary.startswith("The team")
+            calls.append({f: b.calls for f, b in backends.items()})
+            r = s.GetLLMAnswer(raft_pb.LLMRequest(token=tok, query="what is raft?"))
+            assert r.success
+            calls.append({f: b.calls for f, b in backends.items()})
+            r = s.GetContextSuggestions(raft_pb.ContextSuggestionsRequest(
+                token=tok, channel_id="general", current_input="I think"))
+            assert list(r.topics) == ["deadlines", "code review"]
+            calls.append({f: b.calls for f, b in backends.items()})
+            order = ["smart", "summary", "ask", "suggest"]
+            for i, snap in enumerate(calls):  # after RPC i exactly features 0..i were called once
+                assert snap == {f: int(order.index(f) <= i) for f in order}, (i, snap)
+            # the routing holds on every node (a follower serves AI RPCs too)
+            F = next(i for i in c.peers if i != L)
+            deadline = time.time() + 5
+            while time.time() < deadline and not c.stub(F).GetMessages(
+                    raft_pb.GetMessagesRequest(token=tok, channel_id="general")).messages:
+                time.sleep(0.02)  # the follower applies the message
+            r = c.stub(F).GetSmartReply(raft_pb.SmartReplyRequest(token=tok, channel_id="general"))
+            assert r.success and backends["smart"].calls == 2 and backends["ask"].calls == 1
+    finally:
+        for sv in servers:
+            sv.stop(0)
+
+
+def test_logout_on_follower_is_forwarded_to_leader(cluster):
+    """The reference logs out on any node (server/raft_node.py:1751): a follower relays the
+    logout to the leader, whose replicated revocation invalidates the token everywhere."""
+    L = cluster.leader()
+    tok = cluster.login(L)
+    F = next(i for i in cluster.peers if i != L)
+    r = cluster.stub(F).Logout(raft_pb.LogoutRequest(token=tok))
+    assert r.success, r.message
+    deadline = time.time() + 5
+    while time.time() < deadline:
+        ok = [cluster.stub(i).GetOnlineUsers(raft_pb.GetOnlineUsersRequest(token=tok)).success
+              for i in cluster.peers]
+        if not any(ok):
+            break
+        time.sleep(0.05)
+    assert not any(ok)

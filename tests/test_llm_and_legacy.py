@@ -435,3 +435,45 @@ def test_aio_frontend_serves_all_rpcs_over_a_replica_pool():
         if srv is not None:
             srv.stop(0)
         pool.close()
+
+
+def test_llm_server_serves_features_from_separate_backends():
+    """``llm.server --serve FEATURE=MODEL...``: one service address, one engine group per
+    feature (scripted stand-ins here); the feature spec grammar and its errors."""
+    import argparse
+
+    import grpc
+
+    from drtc_amd.llm import server as S
+    from drtc_amd.llm.service import FeatureRouter
+    from drtc_amd.protos import LLM_SERVICE, llm_pb, make_stub
+    from drtc_amd.utils.cluster import free_port
+
+    assert S.parse_serve("smart=gemma-2b@0") == ("smart", "gemma-2b", [0], 1)
+    assert S.parse_serve("ask=llama-3-70b@0-7:tp8") == ("answer", "llama-3-70b", list(range(8)), 8)
+    assert S.parse_serve("suggest=mixtral-8x7b@2,3") == ("suggest", "mixtral-8x7b", [2, 3], 1)
+    for bad in ("smart", "chat=llama-3-8b", "smart=x@0,0", "answer=llama-3-70b@0-3:tp8"):
+        with pytest.raises(ValueError):
+            S.parse_serve(bad)
+    args = argparse.Namespace(backend="engine", model="scripted", tp=1, gpus=1, max_batch=4,
+                              max_model_len=512, no_graphs=True, custom_allreduce=False,
+                              in_process=True)
+    router = S.build_feature_backends(args, ["smart=scripted@0", "summary=scripted@1"])
+    assert isinstance(router, FeatureRouter)
+    assert router.route("smart") is not router.route("summary")
+    assert router.route("answer") is router.route("suggest") is router.default
+    port = free_port()
+    srv = S.serve(router, port=port, bind="127.0.0.1")
+    try:
+        stub = make_stub(grpc.insecure_channel(f"127.0.0.1:{port}"), LLM_SERVICE)
+        msgs = [llm_pb.Message(sender="a", content="lunch?")]
+        stub.GetSmartReply(llm_pb.SmartReplyRequest(request_id="1", recent_messages=msgs), timeout=10)
+        stub.SummarizeConversation(llm_pb.SummarizeRequest(request_id="2", messages=msgs,
+                                                           max_length=200), timeout=10)
+        stub.SummarizeConversation(llm_pb.SummarizeRequest(request_id="3", messages=msgs,
+                                                           max_length=200), timeout=10)
+        stub.GetLLMAnswer(llm_pb.LLMRequest(request_id="4", query="q?"), timeout=10)
+        assert (router.route("smart").calls, router.route("summary").calls,
+                router.default.calls) == (1, 2, 1)
+    finally:
+        srv.stop(0)

@@ -1,5 +1,6 @@
 """Multi-process parallelism on CPU (gloo): EP all-to-all dispatch/combine and
 TP forward equivalence with world_size 2 (the same code runs on RCCL)."""
+import pytest
 import os
 import socket
 import sys
@@ -219,17 +220,21 @@ def _ep_redo_worker(rank, world, port, q):
     model = TransformerLM(TINY_MIXTRAL, "cpu", pc=pc, seed=4)
     prompts = [list(range(5 + i, 29 + 3 * i)) for i in range(6)]
     res = {}
-    for cf in (8.0, 0.2):
-        ep.EP_CF = cf
-        eng = LLMEngine(model, max_batch=8, max_model_len=256, num_blocks=64, use_graphs=False)
-        prm = SamplingParams.greedy(12, ignore_eos=True)
-        reqs = [eng.add_request(Request(list(p), prm)) for p in prompts]
-        while eng.has_work():
-            eng.step()
-        res[cf] = {"out": [r.output_ids for r in reqs],
-                   "prefill_redo": eng.stats.get("ep_redo_steps", 0),
-                   "decode_redo": eng.runner.redo_steps,
-                   "pipelined": eng.stats["decode_steps_pipelined"]}
+    # greedy, and sampled (t > 0: a redo must reuse the RNG counter of the step's first run)
+    for mode, prm in (("greedy", SamplingParams.greedy(12, ignore_eos=True)),
+                      ("sampled", SamplingParams(max_new_tokens=12, temperature=0.9, top_k=8,
+                                                 top_p=0.95, ignore_eos=True))):
+        for cf in (8.0, 0.2):
+            ep.EP_CF = cf
+            eng = LLMEngine(model, max_batch=8, max_model_len=256, num_blocks=64,
+                            use_graphs=False)
+            reqs = [eng.add_request(Request(list(p), prm)) for p in prompts]
+            while eng.has_work():
+                eng.step()
+            res[(mode, cf)] = {"out": [r.output_ids for r in reqs],
+                               "prefill_redo": eng.stats.get("ep_redo_steps", 0),
+                               "decode_redo": eng.runner.redo_steps,
+                               "pipelined": eng.stats["decode_steps_pipelined"]}
     q.put((rank, res))
     dist.destroy_process_group()
 
@@ -290,10 +295,26 @@ def test_tp_mixed_prefill_decode_steps_match_tp1():
 
 def test_ep_capacity_overflow_redo_is_exact():
     res = dict(_run(_ep_redo_worker))
-    for rank in (0, 1):
-        big, small = res[rank][8.0], res[rank][0.2]
-        assert big["prefill_redo"] == big["decode_redo"] == 0
-        assert small["prefill_redo"] > 0 and small["decode_redo"] > 0, small
-        assert small["pipelined"] > 0
-        assert small["out"] == big["out"]
-    assert res[0][0.2]["out"] == res[1][0.2]["out"]
+    for mode in ("greedy", "sampled"):
+        for rank in (0, 1):
+            big, small = res[rank][(mode, 8.0)], res[rank][(mode, 0.2)]
+            assert big["prefill_redo"] == big["decode_redo"] == 0
+            assert small["prefill_redo"] > 0 and small["decode_redo"] > 0, small
+            assert small["pipelined"] > 0
+            assert small["out"] == big["out"], mode
+        assert res[0][(mode, 0.2)]["out"] == res[1][(mode, 0.2)]["out"]
+    # the sampled run really samples (not the greedy tokens)
+    assert res[0][("sampled", 8.0)]["out"] != res[0][("greedy", 8.0)]["out"]
+
+
+def test_tp_device_checks():
+    """A TP group on real GPUs: distinct devices, in range, every pair peer-accessible."""
+    from drtc_amd.parallel.tp_engine import check_devices
+
+    check_devices([0, 1, 2, 3], 8, lambda a, b: True)
+    with pytest.raises(RuntimeError, match="share a device"):
+        check_devices([0, 0], 8, lambda a, b: True)
+    with pytest.raises(RuntimeError, match="out of range"):
+        check_devices([6, 8], 8, lambda a, b: True)
+    with pytest.raises(RuntimeError, match="peer access"):
+        check_devices([0, 1, 2], 8, lambda a, b: {a, b} != {1, 2})

@@ -424,3 +424,26 @@ def test_native_storage_vote_survives_torn_reference_state_file(tmp_path):
     st3.close()
     s, _ = NativeStorage(d, 5001, fsync=True).load()
     assert s["current_term"] == 4 and s["voted_for"] is None
+
+
+def test_native_storage_upgrades_old_dir_without_hard_state(tmp_path):
+    """A data directory written before the hard-state file existed holds term / vote only in
+    the reference state pickle.  The first save_state after the upgrade must write and fsync
+    the hard state (even with term / vote unchanged) before the unsynced pickle rewrite, so a
+    torn pickle afterwards cannot bring back term 0 with no vote."""
+    d = str(tmp_path)
+    state_p = os.path.join(d, "raft_state_port_5002.pkl")
+    hard_p = os.path.join(d, "raft_hardstate_port_5002.pkl")
+    pickle_compat.dump({"current_term": 7, "voted_for": 3, "commit_index": -1,
+                        "last_applied": -1}, state_p)
+    st = NativeStorage(d, 5002, fsync=True)
+    s, _ = st.load()
+    assert s["current_term"] == 7 and s["voted_for"] == 3
+    assert not os.path.exists(hard_p)
+    st.save_state({"commit_index": -1, "last_applied": -1})  # term / vote unchanged
+    assert os.path.exists(hard_p)
+    st.close()
+    with open(state_p, "wb"):
+        pass  # power loss tears the unsynced reference pickle
+    s, _ = NativeStorage(d, 5002, fsync=True).load()
+    assert s["current_term"] == 7 and s["voted_for"] == 3
