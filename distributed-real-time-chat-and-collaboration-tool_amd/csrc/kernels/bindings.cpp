@@ -29,19 +29,6 @@ PYBIND11_MODULE(_hipk, m) {
                                       P<void>(w), rows, H, eps, x_stride,
                                       out_stride, res_stride, gemma, S(st));
         });
-  m.def("rmsnorm_partials", [](u64 out, u64 residual, u64 part, int sk, int rows, int H, u64 w,
-                               float eps, int out_stride, int res_stride, bool add_residual,
-                               bool gemma, u64 st) {
-    return drtc::launch_rmsnorm_partials(P<void>(out), P<void>(residual), P<const float>(part), sk,
-                                         rows, H, P<const void>(w), eps, out_stride, res_stride,
-                                         add_residual, gemma, S(st));
-  });
-  m.def("row_rinv", [](u64 rinv, u64 x, int rows, int H, int x_stride, float eps, u64 st) {
-    return drtc::launch_row_rinv(P<float>(rinv), P<const void>(x), rows, H, x_stride, eps, S(st));
-  });
-  m.def("rowsq_rinv", [](u64 rinv, u64 sq, int M, int slots, int H, float eps, u64 st) {
-    return drtc::launch_rowsq_rinv(P<float>(rinv), P<const float>(sq), M, slots, H, eps, S(st));
-  });
   m.def("act_glu", [](u64 out, u64 gu, int64_t T, int I, int gu_stride, int act,
                       u64 st) {
     return drtc::launch_act_glu(P<void>(out), P<void>(gu), T, I, gu_stride, act, S(st));
@@ -100,19 +87,18 @@ PYBIND11_MODULE(_hipk, m) {
                             P<const void>(w_gu), P<const void>(w_dn), T, H, I, E, k, e_off,
                             e_local, act, P<void>(ws), ws_bytes, variant, S(st));
   });
+  // gemm_w4 (ops.gemm.mfma_gemm): variant 7 + schedule bits (7 per-tile, 9 temporal stores,
+  // 15 persistent, 31 persistent with the per-XCD K rotation)
   m.def("gemm", [](u64 c, u64 a, u64 b, u64 r, int M, int N, int K, int lda, int ldb, int ldc,
                    int ldr, int epi, int up_off, int variant, int splitk, int group_m, u64 slab,
                    int64_t slab_bytes, u64 counters, int n_counters, u64 st) {
-    return drtc::launch_gemm(P<void>(c), P<const void>(a), P<const void>(b), P<const void>(r), M,
-                             N, K, lda, ldb, ldc, ldr, epi, up_off, variant, splitk, group_m,
-                             P<void>(slab), slab_bytes, P<int>(counters), n_counters, S(st));
+    if (variant < 7) return -1;
+    return drtc::launch_gemm_w4(P<void>(c), P<const void>(a), P<const void>(b), P<const void>(r),
+                                M, N, K, lda, ldb, ldc, ldr, epi, up_off, splitk, group_m,
+                                P<void>(slab), slab_bytes, P<int>(counters), n_counters,
+                                variant - 7, S(st));
   });
-  m.def("gemm_workspace_bytes", &drtc::gemm_workspace_bytes);
-  m.def("gemm_dec", [](u64 c, u64 a, u64 b, u64 r, int M, int N, int K, int lda, int ldb, int ldc,
-                       int ldr, int epi, int up_off, int nr, int group_m, u64 st) {
-    return drtc::launch_gemm_dec(P<void>(c), P<const void>(a), P<const void>(b), P<const void>(r),
-                                 M, N, K, lda, ldb, ldc, ldr, epi, up_off, nr, group_m, S(st));
-  });
+  m.def("gemm_workspace_bytes", &drtc::gemm_w4_workspace_bytes);
   m.def("moe_workspace_bytes", &drtc::moe_workspace_bytes);
   m.def("ep_plan", [](u64 topi, int npairs, int e_local, int world, int cap, u64 dst_row,
                       u64 send_pair, u64 send_e, u64 overflow, u64 st) {

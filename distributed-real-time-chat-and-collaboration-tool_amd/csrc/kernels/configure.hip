@@ -9,10 +9,6 @@ int configure_kernels() {
   if (e) return e;
   e = configure_moe();
   if (e) return e;
-  e = configure_gemm();
-  if (e) return e;
-  e = configure_gemm_w4();
-  if (e) return e;
-  return configure_gemm_dec();
+  return configure_gemm_w4();
 }
 }  // namespace drtc

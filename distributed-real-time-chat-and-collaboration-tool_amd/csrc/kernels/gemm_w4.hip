@@ -2,17 +2,17 @@
 //
 //   C[M, N] = epi( A[M, K] . B[N, K]^T )      (A activations, B weights, both K-contiguous)
 //
-// epilogues as gemm.hip: store / + residual (may alias C) / SiLU- or GELU-gated [gate; up].
+// epilogues: store / + residual (may alias C) / SiLU- or GELU-gated [gate; up].
 // This is the GEMM of the engine's prefill and full-batch decode passes (replacing the model
 // hop of ref llm_server/llm_server.py:231 / :287 with on-node compute).
 //
-// Why a second GEMM: the 8-wave kernels of gemm.hip (2 waves per SIMD, 128 x 64 per wave)
-// reach 0.76-0.81x of hipBLASLt on the Llama shapes (profiles/r2a_hand_gemm.md): the PMC
-// pass shows them parked at barriers (SQ_WAIT_ANY 9x the library's) and issuing 1.5x the LDS
-// reads per MFMA.  This kernel uses the layout that reads the least LDS per FLOP - one wave
-// per SIMD, 128 x 128 outputs per wave (64 MFMA 16x16x32 tiles = 256 accumulator registers,
-// the AGPR half of the unified file) - and hides every latency INSIDE the wave with an
-// explicit instruction schedule instead of a partner wave:
+// Why this layout: 8-wave forms (2 waves per SIMD, 128 x 64 per wave; round 2, removed in
+// round 4) reached 0.76-0.81x of hipBLASLt on the Llama shapes (profiles/r2a_hand_gemm.md):
+// parked at barriers (SQ_WAIT_ANY 9x the library's) and issuing 1.5x the LDS reads per
+// MFMA.  This kernel uses the layout that reads the least LDS per FLOP - one wave per SIMD,
+// 128 x 128 outputs per wave (64 MFMA 16x16x32 tiles = 256 accumulator registers, the AGPR
+// half of the unified file) - and hides every latency INSIDE the wave with an explicit
+// instruction schedule instead of a partner wave:
 //
 //   * LDS: 2 stages x [A 256 rows | B 256 rows] x 128 B (one 64-deep K tile) = 129 KiB, filled
 //     by LDS-DMA (buffer_load_dwordx4 ... lds, 1 KiB = 8 rows per wave-instruction).  A: the
@@ -60,22 +60,7 @@ constexpr int kW4BBlk = 1040;                  // bytes per 8-row B block
 constexpr int kW4Stage = kW4BOff + 32 * kW4BBlk;  // 66048
 constexpr int kW4Lds = 2 * kW4Stage;
 
-// W4_PARTIAL: split-K without a combine in this kernel - slice s writes its fp32 partial
-// tile to plane s of slab [splitk][M][N]; the consumer (rmsnorm_partials_kernel, the
-// residual add + RMSNorm that follows the o / down projection anyway) sums the planes with
-// all CUs at HBM rate.  For the full-batch decode projections (M = 1024, N = 4096: 64
-// tiles of 256 x 256), split-K 4 fills the chip and no single workgroup has to read the
-// other slices' partials (the last-arriver combine read 768 KiB alone: 155 vs 80 us).
-// RMSNorm folded across a prefill layer (TP = 1): the o / down projection's residual epilogue
-// also emits each row's partial sum of squares of the new residual stream h over its 128
-// columns (W4_RESIDUAL_SQ, `slab` = sq[M][N / 128]); a tiny kernel turns them into
-// rinv = rsqrt(mean(h^2) + eps) (rowsq_rinv_kernel); the next qkv / gate_up GEMM reads h
-// itself with the norm weight folded into W and scales each output row by rinv
-// (W4_STORE_RS / W4_SILU_RS / W4_GELU_RS, `slab` = rinv[M]) - no [M, H] normalised copy.
-enum {
-  W4_STORE = 0, W4_RESIDUAL = 1, W4_SILU = 2, W4_GELU = 3, W4_PARTIAL = 4,
-  W4_RESIDUAL_SQ = 5, W4_STORE_RS = 6, W4_SILU_RS = 7, W4_GELU_RS = 8
-};
+enum { W4_STORE = 0, W4_RESIDUAL = 1, W4_SILU = 2, W4_GELU = 3 };
 
 struct W4Params {
   bf16_t* c;
@@ -93,15 +78,11 @@ struct W4Params {
 };
 
 template <int EPI>
-DRTC_DEVICE constexpr bool w4_glu() {
-  return EPI == W4_SILU || EPI == W4_GELU || EPI == W4_SILU_RS || EPI == W4_GELU_RS;
-}
+DRTC_DEVICE constexpr bool w4_glu() { return EPI == W4_SILU || EPI == W4_GELU; }
 template <int EPI>
-DRTC_DEVICE constexpr bool w4_res() { return EPI == W4_RESIDUAL || EPI == W4_RESIDUAL_SQ; }
+DRTC_DEVICE constexpr bool w4_res() { return EPI == W4_RESIDUAL; }
 template <int EPI>
-DRTC_DEVICE constexpr bool w4_rs() { return EPI == W4_STORE_RS || EPI == W4_SILU_RS || EPI == W4_GELU_RS; }
-template <int EPI>
-DRTC_DEVICE constexpr int w4_act() { return (EPI == W4_SILU || EPI == W4_SILU_RS) ? 0 : 1; }
+DRTC_DEVICE constexpr int w4_act() { return EPI == W4_SILU ? 0 : 1; }
 
 // One LDS-DMA wave-instruction: 64 lanes x 16 B from rsrc + voff + soff into LDS bytes
 // [dst, dst + 1024).  Inline asm (hipcc would pin vmcnt / lgkmcnt waits around a builtin
@@ -167,12 +148,9 @@ struct W4Tile {
 // the buffer base (descriptor rebuilt once per tile) so the scalar offsets are loop-invariant:
 // one SALU per DMA (nothing else in this kernel uses M0).
 //
-// Schedule variants (launch_gemm variant 7 + V), A/B'd in one binary:
-//   V & 1  two barriers per K tile: both half-1 fragment sets are read first (MFMA 0-31),
-//          one lgkmcnt(0) + barrier frees the whole stage, then all 16 DMAs (MFMA 38-98)
+// Schedule variants (mfma_gemm variant 7 + V):
 //   V & 2  plain (temporal) epilogue stores instead of non-temporal ones
-//   V & 4  reduce-scatter split-K (w4_splitk_rs: every slice finishes part of the tile,
-//          all workgroups resident) instead of the last-arriver combine
+//   V & 8  persistent form (see gemm_w4_kernel); V & 16 its per-XCD K rotation
 template <int V, bool DMA, bool NEXT, bool Z, int Q>
 DRTC_DEVICE void w4_step(f32x4 (&acc)[8][8], bf16x8 (&fa0)[8], bf16x8 (&fb0)[8],
                          bf16x8 (&fa1)[8], bf16x8 (&fb1)[8], const W4Tile& T, const W4Dma& d) {
@@ -183,52 +161,33 @@ DRTC_DEVICE void w4_step(f32x4 (&acc)[8][8], bf16x8 (&fa0)[8], bf16x8 (&fb0)[8],
     acc[i][j] = mfma16(fa0[i], fb0[j], acc[i][j]);
   else
     acc[i][j] = mfma16(fa1[i], fb1[j], acc[i][j]);
-  constexpr bool two = (V & 1) != 0;
   // ---- half 1 of this tile: B fragments (one read per 2 MFMA), then A
   if constexpr (Q < 16 && (Q & 1) == 0) fb1[Q >> 1] = w4_rd(T.lds, T.cur + T.rb1 + 128 * (Q >> 1));
-  if constexpr (two) {
-    if constexpr (Q >= 16 && Q < 32 && (Q & 1) == 0)
-      fa1[(Q - 16) >> 1] = w4_rd(T.lds, T.cur + T.ra1 + 2048 * ((Q - 16) >> 1));
-    if constexpr (Q == 35) {
-      w4_lgkm0();
-      w4_barrier();  // every wave's reads of this stage are done: the stage is free
-    }
-  } else {
-    if constexpr (Q == 21) {
-      w4_lgkm0();
-      w4_barrier();  // every wave's B reads of this stage are done
-    }
-    if constexpr (Q >= 22 && Q < 38 && ((Q - 22) & 3) < 2) {
-      constexpr int a = ((Q - 22) >> 2) * 2 + ((Q - 22) & 1);
-      fa1[a] = w4_rd(T.lds, T.cur + T.ra1 + 2048 * a);
-    }
-    if constexpr (Q == 57) {
-      w4_lgkm0();
-      w4_barrier();  // every wave's A reads of this stage are done
-    }
+  if constexpr (Q == 21) {
+    w4_lgkm0();
+    w4_barrier();  // every wave's B reads of this stage are done
+  }
+  if constexpr (Q >= 22 && Q < 38 && ((Q - 22) & 3) < 2) {
+    constexpr int a = ((Q - 22) >> 2) * 2 + ((Q - 22) & 1);
+    fa1[a] = w4_rd(T.lds, T.cur + T.ra1 + 2048 * a);
+  }
+  if constexpr (Q == 57) {
+    w4_lgkm0();
+    w4_barrier();  // every wave's A reads of this stage are done
   }
   // ---- DMA of tile t + 2 into this stage: B group, then A group, one per 4 MFMA
-  constexpr int qb = two ? 38 : 24, qa = two ? 70 : 60;
-  constexpr bool classic = false;
-  if constexpr (classic && DMA && Q >= qb && Q <= qb + 28 && ((Q - qb) & 3) == 0) {
-    constexpr int s = (Q - qb) >> 2;
-    w4_dma(d.lds_b + T.cur + 4 * kW4BBlk * s, d.vb, d.rb, T.kb + d.sb[s]);
-  }
-  if constexpr (classic && DMA && Q >= qa && Q <= qa + 28 && ((Q - qa) & 3) == 0) {
-    constexpr int s = (Q - qa) >> 2;
-    w4_dma(d.lds_a + T.cur + 4096 * s, d.va[s], d.ra, T.kb);
-  }
-  if constexpr (!classic && DMA && Q == qb - 1)
+  constexpr int qb = 24, qa = 60;
+  if constexpr (DMA && Q == qb - 1)
     asm volatile("s_mov_b32 m0, %0" : : "s"(d.lds_b + T.cur) : "memory");
-  if constexpr (!classic && DMA && Q >= qb && Q <= qb + 28 && ((Q - qb) & 3) == 0) {
+  if constexpr (DMA && Q >= qb && Q <= qb + 28 && ((Q - qb) & 3) == 0) {
     constexpr int s = (Q - qb) >> 2;
     asm volatile("buffer_load_dwordx4 %0, %1, %2 offen lds"
                  : : "v"(d.vb), "s"(T.rbk), "s"(d.sb[s]) : "memory");
     if constexpr (s < 7) asm volatile("s_add_u32 m0, m0, 0x1040" ::: "memory");  // 4 blocks
   }
-  if constexpr (!classic && DMA && Q == qa - 1)
+  if constexpr (DMA && Q == qa - 1)
     asm volatile("s_mov_b32 m0, %0" : : "s"(d.lds_a + T.cur) : "memory");
-  if constexpr (!classic && DMA && Q >= qa && Q <= qa + 28 && ((Q - qa) & 3) == 0) {
+  if constexpr (DMA && Q >= qa && Q <= qa + 28 && ((Q - qa) & 3) == 0) {
     constexpr int s = (Q - qa) >> 2;
     asm volatile("buffer_load_dwordx4 %0, %1, 0 offen lds"
                  : : "v"(d.va[s]), "s"(T.rak) : "memory");
@@ -307,29 +266,6 @@ DRTC_DEVICE void w4_st8(bf16_t* p, bf16x4 v) {
 template <int EPI, int V>
 DRTC_DEVICE void w4_epilogue(const W4Params& p, f32x4 (&acc)[8][8], int tm, int tn, int wm,
                              int wn, int l16, int g, int slice) {
-  if constexpr (EPI == W4_PARTIAL) {
-    // lane: 8 consecutive fp32 columns of 4 rows per fragment i -> two 16-B stores per row
-    // (temporal: the planes are read back right after, from the L2 / MALL)
-    float* plane = p.slab + (int64_t)slice * p.M * p.N;
-    const int n = 256 * tn + 128 * wn + 8 * l16;
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = 256 * tm + 128 * wm + 16 * i + 4 * g + r;
-        if (m >= p.M) continue;
-        f32x4 lo, hi;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          lo[j] = acc[i][j][r];
-          hi[j] = acc[i][j + 4][r];
-        }
-        float* dst = plane + (int64_t)m * p.N + n;
-        *reinterpret_cast<f32x4*>(dst) = lo;
-        *reinterpret_cast<f32x4*>(dst + 4) = hi;
-      }
-    return;
-  }
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
 #pragma unroll
@@ -337,20 +273,18 @@ DRTC_DEVICE void w4_epilogue(const W4Params& p, f32x4 (&acc)[8][8], int tm, int 
       const int m = 256 * tm + 128 * wm + 16 * i + 4 * g + r;
       if (m >= p.M) continue;
       bf16_t* crow = p.c + (int64_t)m * p.ldc;
-      float sc = 1.f;  // folded RMSNorm: this row's rsqrt(mean(h^2) + eps)
-      if constexpr (w4_rs<EPI>()) sc = p.slab[m];
       if constexpr (w4_glu<EPI>()) {
         const int n = 128 * tn + 64 * wn + 4 * l16;
         bf16x4 o;
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-          o[j] = f2bf(act_value<w4_act<EPI>()>(acc[i][j][r] * sc) * (acc[i][j + 4][r] * sc));
+          o[j] = f2bf(act_value<w4_act<EPI>()>(acc[i][j][r]) * acc[i][j + 4][r]);
         w4_st8<V>(crow + n, o);
       } else if constexpr (!w4_res<EPI>()) {
         const int n = 256 * tn + 128 * wn + 8 * l16;
         bf16x8 o;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) o[j] = f2bf(acc[i][j][r] * sc);
+        for (int j = 0; j < 8; ++j) o[j] = f2bf(acc[i][j][r]);
         w4_st16<V>(crow + n, o);
       }
     }
@@ -376,18 +310,6 @@ DRTC_DEVICE void w4_epilogue(const W4Params& p, f32x4 (&acc)[8][8], int tm, int 
         bf16x8 o;
 #pragma unroll
         for (int j = 0; j < 8; ++j) o[j] = f2bf(acc[i][j][r] + bf2f(rv[i][r][j]));
-        if constexpr (EPI == W4_RESIDUAL_SQ) {
-          // this wave's 128 columns of row m: 8 per lane, reduced over the 16 lanes of the
-          // row (lane bits 0-3); every lane takes part (rows past M computed, not stored)
-          float sq = 0.f;
-#pragma unroll
-          for (int j = 0; j < 8; ++j) sq += bf2f(o[j]) * bf2f(o[j]);
-          sq += __shfl_xor(sq, 1, 64);
-          sq += __shfl_xor(sq, 2, 64);
-          sq += __shfl_xor(sq, 4, 64);
-          sq += __shfl_xor(sq, 8, 64);
-          if (l16 == 0 && m < p.M) p.slab[(int64_t)m * (2 * p.tiles_n) + 2 * tn + wn] = sq;
-        }
         if (m >= p.M) continue;
         w4_st16<V>(p.c + (int64_t)m * p.ldc + n, o);
       }
@@ -439,132 +361,6 @@ DRTC_DEVICE bool w4_splitk(const W4Params& p, f32x4 (&acc)[8][8], int tile, int 
                                                          0, kSc1));
   }
   return true;
-}
-
-// Output rows 256 tm + 128 wm + 16 i + 4 g + r (r = 0..3) of one row fragment i of a wave
-// block (wm, wn), from its 8 accumulators over the B fragments j (used by the reduce-scatter
-// split-K, where a block is finished by other waves than the one that computed it).
-template <int EPI, int V>
-DRTC_DEVICE void w4_epi_frag(const W4Params& p, const f32x4 (&v)[8], int tm, int tn, int wm,
-                             int wn, int i, int l16, int g) {
-  const int m0 = 256 * tm + 128 * wm + 16 * i + 4 * g;
-  if constexpr (w4_glu<EPI>()) {
-    const int n = 128 * tn + 64 * wn + 4 * l16;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      if (m0 + r >= p.M) continue;
-      bf16x4 o;
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        o[j] = f2bf(act_value<w4_act<EPI>()>(v[j][r]) * v[j + 4][r]);
-      w4_st8<V>(p.c + (int64_t)(m0 + r) * p.ldc + n, o);
-    }
-  } else {
-    const int n = 256 * tn + 128 * wn + 8 * l16;
-    bf16x8 rv[4];
-    if constexpr (w4_res<EPI>()) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        rv[r] = *reinterpret_cast<const bf16x8*>(p.r + (int64_t)min(m0 + r, p.M - 1) * p.ldr + n);
-    }
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      if (m0 + r >= p.M) continue;
-      bf16x8 o;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        float x = v[j][r];
-        if constexpr (w4_res<EPI>()) x += bf2f(rv[r][j]);
-        o[j] = f2bf(x);
-      }
-      w4_st16<V>(p.c + (int64_t)(m0 + r) * p.ldc + n, o);
-    }
-  }
-}
-
-// Reduce-scatter split-K (launch_gemm variant 11, splitk 2 or 4, every workgroup resident:
-// tiles x splitk <= CUs).  The tile's four 128 x 128 wave blocks are owned by the slices
-// (block b by slice b % splitk).  Every wave that does not own its block writes its fp32
-// partial (64 KiB) write-through (sc1) to slab[tile][b][slice]; the owner waves stage theirs
-// in LDS.  One lane per workgroup then adds to the tile's arrival counter (after every
-// storing wave's vmcnt(0) and a workgroup barrier) and polls it (sc1) until all slices
-// arrived - bounded, with the error word set on a timeout.  Each workgroup then finishes its
-// owned blocks with all four waves (8 row fragments per block spread over the waves), reading
-// the other slices' partials with sc1 loads only.  The last workgroup to leave re-arms the
-// counters.  Per workgroup 192 KiB written and 192 KiB read, in parallel on every CU, instead
-// of one last arriver reading (splitk - 1) x 256 KiB alone.
-template <int EPI, int V>
-DRTC_DEVICE void w4_splitk_rs(const W4Params& p, f32x4 (&acc)[8][8], int tile, int slice,
-                              int tm, int tn, int wv, int lane, int l16, int g, char* lds) {
-  constexpr int kSc1 = 16;
-  constexpr int kBlk = 64 * 64 * 16;  // one wave's partial block: 64 KiB
-  const int sk = p.splitk;
-  const __amdgpu_buffer_rsrc_t slab = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(reinterpret_cast<char*>(p.slab) + (int64_t)tile * 4 * sk * kBlk), (short)0,
-      4 * sk * kBlk, 0x00020000);
-  f32x4* L = reinterpret_cast<f32x4*>(lds);
-  if (wv % sk == slice) {  // owner: stage in LDS, slot wv / sk
-    f32x4* mine = L + (wv / sk) * 64 * 64 + lane;
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) mine[(i * 8 + j) * 64] = acc[i][j];
-  } else {
-    const int base = (wv * sk + slice) * kBlk + lane * 16;
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), slab,
-                                               base + (i * 8 + j) * 1024, 0, kSc1);
-  }
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-  __syncthreads();
-  int* arrive = p.counters + 2 * tile;
-  int* depart = arrive + 1;
-  if (threadIdx.x == 0) {
-    __hip_atomic_fetch_add(arrive, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    int spins = 0;
-    while (__hip_atomic_load(arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < sk) {
-      __builtin_amdgcn_s_sleep(1);
-      if (++spins > (1 << 24)) {  // a slice never arrived: give up (never hang the GPU)
-        __hip_atomic_store(p.counters + p.tiles_m * p.tiles_n * 2, 1, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-    }
-  }
-  __syncthreads();
-  // owned blocks b = bi * sk + slice (bi < 4 / sk); row fragments f = bi * 8 + i, split evenly
-  // over the four waves
-  const int per = 8 * (4 / sk) / 4;
-  for (int f = wv * per; f < (wv + 1) * per; ++f) {
-    const int bi = f >> 3, i = f & 7, b = bi * sk + slice;
-    f32x4 v[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = L[(bi * 64 + i * 8 + j) * 64 + lane];
-    for (int s2 = 0; s2 < sk; ++s2) {
-      if (s2 == slice) continue;
-      const int src = (b * sk + s2) * kBlk + (i * 8) * 1024 + lane * 16;
-      f32x4 w[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        w[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(slab, src + j * 1024,
-                                                                               0, kSc1));
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] += w[j];
-    }
-    w4_epi_frag<EPI, V>(p, v, tm, tn, b >> 1, b & 1, i, l16, g);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const int t = __hip_atomic_fetch_add(depart, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (t == sk - 1) {  // every slice of the tile has read the slabs: re-arm
-      __hip_atomic_store(arrive, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(depart, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
 }
 
 // Tile coordinates of tile-order index tt (row-grouped: group_m row tiles sweep the columns).
@@ -779,18 +575,9 @@ __global__ __launch_bounds__(kW4Threads, 1) void gemm_w4_kernel(W4Params p) {
   }
   w4_vmcnt<0>();  // no LDS-DMA may still be landing when the workgroup leaves
 
-  const int tile = tm * p.tiles_n + tn;
-  if constexpr (EPI == W4_PARTIAL) {
-    // every slice stores its own plane: no combine here
-  } else if constexpr ((V & 4) != 0) {
-    if (p.splitk > 1) {
-      __syncthreads();
-      w4_splitk_rs<EPI, V>(p, acc, tile, slice, tm, tn, wv, lane, l16, g, w4_lds);
-      return;
-    }
-  } else if (p.splitk > 1) {
+  if (p.splitk > 1) {
     __syncthreads();
-    if (!w4_splitk(p, acc, tile, slice, w4_lds)) return;
+    if (!w4_splitk(p, acc, tm * p.tiles_n + tn, slice, w4_lds)) return;
   }
   w4_epilogue<EPI, V>(p, acc, tm, tn, wm, wn, l16, g, slice);
 }
@@ -804,18 +591,13 @@ int w4_launch_v(const W4Params& p, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
-
+// schedule variants built: 0 per-tile (split-K capable), 2 the same with temporal stores,
+// 8 persistent, 24 persistent with the per-XCD K rotation
 template <int EPI>
 int w4_launch(const W4Params& p, int v, hipStream_t st) {
   switch (v) {
     case 0: return w4_launch_v<EPI, 0>(p, st);
-    case 1: return w4_launch_v<EPI, 1>(p, st);
     case 2: return w4_launch_v<EPI, 2>(p, st);
-    case 3: return w4_launch_v<EPI, 3>(p, st);
-    case 4: return w4_launch_v<EPI, 4>(p, st);
-    case 5: return w4_launch_v<EPI, 5>(p, st);
-    case 6: return w4_launch_v<EPI, 6>(p, st);
-    case 7: return w4_launch_v<EPI, 7>(p, st);
     case 8: return w4_launch_v<EPI, 8>(p, st);
     case 24: return w4_launch_v<EPI, 24>(p, st);
     default: return -1;
@@ -829,9 +611,7 @@ int w4_cfg_one() {
 }
 template <int EPI>
 int w4_cfg() {
-  return w4_cfg_one<EPI, 0>() | w4_cfg_one<EPI, 1>() | w4_cfg_one<EPI, 2>() |
-         w4_cfg_one<EPI, 3>() | w4_cfg_one<EPI, 4>() | w4_cfg_one<EPI, 5>() |
-         w4_cfg_one<EPI, 6>() | w4_cfg_one<EPI, 7>() | w4_cfg_one<EPI, 8>() |
+  return w4_cfg_one<EPI, 0>() | w4_cfg_one<EPI, 2>() | w4_cfg_one<EPI, 8>() |
          w4_cfg_one<EPI, 24>();
 }
 
@@ -853,40 +633,10 @@ int launch_gemm_w4(void* c, const void* a, const void* b, const void* r, int M, 
                    int group_m, void* slab, int64_t slab_bytes, int* counters, int n_counters,
                    int v, hipStream_t st) {
   // shape contract (checked here so a bad call never reaches the device)
-  const bool glu = epi == W4_SILU || epi == W4_GELU || epi == W4_SILU_RS || epi == W4_GELU_RS;
-  const bool res = epi == W4_RESIDUAL || epi == W4_RESIDUAL_SQ;
+  const bool glu = epi == W4_SILU || epi == W4_GELU;
+  const bool res = epi == W4_RESIDUAL;
+  if (epi < W4_STORE || epi > W4_GELU) return -1;
   if (M <= 0 || N <= 0 || K <= 0 || K % 64 || splitk < 1 || (K / 64) % splitk) return -1;
-  // folded-norm epilogues: `slab` is the side buffer (sq[M][N/128] or rinv[M]), one slice
-  if (epi >= W4_RESIDUAL_SQ) {
-    const int64_t need = epi == W4_RESIDUAL_SQ ? (int64_t)M * (N / 128) * 4 : (int64_t)M * 4;
-    if (epi > W4_GELU_RS || splitk != 1 || (v & 4) || slab == nullptr || slab_bytes < need)
-      return -1;
-  }
-  if (epi == W4_PARTIAL) {  // fp32 planes [splitk][M][N] in `slab`, no counters
-    if (N % 256 || lda % 8 || (uintptr_t)a % 16 || (uintptr_t)b % 16 || slab == nullptr ||
-        (uintptr_t)slab % 16 || slab_bytes < (int64_t)splitk * M * N * 4 || (v & 4))
-      return -1;
-    if ((int64_t)min(M, 256) * lda * 2 >= (1ll << 31) || (int64_t)256 * ldb * 2 >= (1ll << 31))
-      return -1;
-    W4Params p{};
-    p.a = (const bf16_t*)a;
-    p.b = (const bf16_t*)b;
-    p.slab = (float*)slab;
-    p.M = M; p.N = N; p.K = K;
-    p.lda = lda; p.ldb = ldb; p.ldc = N;
-    p.tiles_m = (M + 255) / 256;
-    p.tiles_n = N / 256;
-    p.splitk = splitk;
-    p.kt_split = K / 64 / splitk;
-    if (group_m < 0) {
-      const int64_t tiles = (int64_t)p.tiles_m * p.tiles_n;
-      if (8 % splitk || (tiles * splitk) % 8 || tiles % (8 / splitk)) return -1;
-      p.xk = 1;
-      group_m = -group_m;
-    }
-    p.group_m = group_m < 1 ? 4 : group_m;
-    return w4_launch<W4_PARTIAL>(p, v, st);
-  }
   if (glu ? (N % 128 || up_off != N) : (N % 256)) return -1;
   // persistent form (v & 8): one slice, and two K tiles per tile for the cross-tile prefetch
   if ((v & 8) && ((v != 8 && v != 24) || splitk != 1 || K / 64 < 2)) return -1;
@@ -916,18 +666,14 @@ int launch_gemm_w4(void* c, const void* a, const void* b, const void* r, int M, 
   p.group_m = group_m;
   if (xk) {
     const int64_t tiles = (int64_t)p.tiles_m * p.tiles_n;
-    if ((v & 8) || splitk < 1 || 8 % splitk || (tiles * splitk) % 8 || tiles % (8 / splitk))
-      return -1;
+    if ((v & 8) || 8 % splitk || (tiles * splitk) % 8 || tiles % (8 / splitk)) return -1;
     p.xk = 1;
   }
-  if (epi >= W4_RESIDUAL_SQ) p.slab = (float*)slab;
   if (splitk > 1) {
     const int64_t tiles = (int64_t)p.tiles_m * p.tiles_n;
-    if (slab == nullptr || counters == nullptr || n_counters < 2 * tiles + 1 ||
+    if (slab == nullptr || counters == nullptr || n_counters < tiles ||
         slab_bytes < tiles * splitk * 64ll * kW4Threads * 16)
       return -2;
-    // reduce-scatter form: 2 or 4 slices, and every workgroup resident at once (one per CU)
-    if ((v & 4) && ((splitk != 2 && splitk != 4) || tiles * splitk > w4_num_cus())) return -1;
     p.slab = (float*)slab;
     p.counters = counters;
   }
@@ -935,19 +681,17 @@ int launch_gemm_w4(void* c, const void* a, const void* b, const void* r, int M, 
     case W4_STORE: return w4_launch<W4_STORE>(p, v, st);
     case W4_RESIDUAL: return w4_launch<W4_RESIDUAL>(p, v, st);
     case W4_SILU: return w4_launch<W4_SILU>(p, v, st);
-    case W4_GELU: return w4_launch<W4_GELU>(p, v, st);
-    case W4_RESIDUAL_SQ: return w4_launch<W4_RESIDUAL_SQ>(p, v, st);
-    case W4_STORE_RS: return w4_launch<W4_STORE_RS>(p, v, st);
-    case W4_SILU_RS: return w4_launch<W4_SILU_RS>(p, v, st);
-    case W4_GELU_RS: return w4_launch<W4_GELU_RS>(p, v, st);
-    default: return -1;
+    default: return w4_launch<W4_GELU>(p, v, st);
   }
 }
 
+int64_t gemm_w4_workspace_bytes(int64_t M, int64_t N, int splitk) {
+  // fp32 split-K slabs: 256 KiB per 256 x 256 tile and slice
+  return splitk > 1 ? ((M + 255) / 256) * (N / 256) * splitk * 64ll * kW4Threads * 16 : 0;
+}
+
 int configure_gemm_w4() {
-  return w4_cfg<W4_STORE>() | w4_cfg<W4_RESIDUAL>() | w4_cfg<W4_SILU>() | w4_cfg<W4_GELU>() |
-         w4_cfg<W4_PARTIAL>() | w4_cfg<W4_RESIDUAL_SQ>() | w4_cfg<W4_STORE_RS>() |
-         w4_cfg<W4_SILU_RS>() | w4_cfg<W4_GELU_RS>();
+  return w4_cfg<W4_STORE>() | w4_cfg<W4_RESIDUAL>() | w4_cfg<W4_SILU>() | w4_cfg<W4_GELU>();
 }
 
 }  // namespace drtc

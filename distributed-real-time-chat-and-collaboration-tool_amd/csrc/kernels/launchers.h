@@ -11,13 +11,6 @@
 
 namespace drtc {
 
-int launch_rmsnorm_partials(void* out, void* residual, const float* part, int sk, int rows,
-                            int H, const void* w, float eps, int out_stride, int res_stride,
-                            bool add_residual, bool gemma, hipStream_t st);
-int launch_row_rinv(float* rinv, const void* x, int rows, int H, int x_stride, float eps,
-                    hipStream_t st);
-int launch_rowsq_rinv(float* rinv, const float* sq, int M, int slots, int H, float eps,
-                      hipStream_t st);
 int launch_rmsnorm(void* out, void* residual, const void* x, const void* w,
                    int rows, int H, float eps, int x_stride, int out_stride,
                    int res_stride, bool gemma, hipStream_t st);
@@ -114,21 +107,16 @@ int launch_skinny_norm_gemm(void* y, void* h_out, const void* x, const void* res
                             const void* w, int M, int N, int K, int ldx, int ldr, int ldh,
                             int ldy, float eps, bool gemma, hipStream_t st);
 
-// Hand-written MFMA GEMM (gemm.hip): c[M,N] = epi(a[M,K] . b[N,K]^T); epi 0 store, 1 + r
-// (residual, may alias c), 2/3 SiLU/GELU gated (b rows [0,up_off) gate, [up_off,2 up_off) up,
-// N = up_off).  variant = pipeline (1..3); splitk > 1 needs slab + counters (zeroed once).
-int launch_gemm(void* c, const void* a, const void* b, const void* r, int M, int N, int K,
-                int lda, int ldb, int ldc, int ldr, int epi, int up_off, int variant, int splitk,
-                int group_m, void* slab, int64_t slab_bytes, int* counters, int n_counters,
-                hipStream_t st);
-int64_t gemm_workspace_bytes(int64_t M, int64_t N, int splitk);
-// 4-wave hand-scheduled GEMM (gemm_w4.hip): same contract as launch_gemm (gated: up_off == N);
-// launch_gemm variants 7..15 route here (schedule variant v = variant - 7; 15 = persistent).  Split-K slabs:
-// 256 KiB per tile and slice.
+// 4-wave hand-scheduled GEMM (gemm_w4.hip): c[M,N] = epi(a[M,K] . b[N,K]^T); epi 0 store,
+// 1 + r (residual, may alias c), 2/3 SiLU/GELU gated (b rows [0,up_off) gate, [up_off, 2 up_off)
+// up, N = up_off).  v = schedule bits (0 per-tile, 2 temporal stores, 8 persistent, 24
+// persistent + per-XCD K rotation); splitk > 1 (per-tile form) needs slab + counters (zeroed
+// once): 256 KiB of slab per tile and slice.
 int launch_gemm_w4(void* c, const void* a, const void* b, const void* r, int M, int N, int K,
                    int lda, int ldb, int ldc, int ldr, int epi, int up_off, int splitk,
                    int group_m, void* slab, int64_t slab_bytes, int* counters, int n_counters,
                    int v, hipStream_t st);
+int64_t gemm_w4_workspace_bytes(int64_t M, int64_t N, int splitk);
 int configure_gemm_w4();
 
 // Raise the dynamic-LDS ceiling of the kernels that need > 64 KiB (head_dim
@@ -142,12 +130,5 @@ int launch_midm_gemm(void* y, const void* x, const void* w, const void* res, int
                      int K, int ldx, int ldy, int ldr, int epi, int S, void* slab,
                      int64_t slab_bytes, hipStream_t st);
 int configure_moe();
-int configure_gemm();
-// Decode-batch GEMM (gemm_dec.hip): 128 x 128 tiles, intra-workgroup K split over two wave
-// groups; epi as launch_gemm (N = columns of C; gated: up_off == N); nr = LDS regions 4/6/8.
-int launch_gemm_dec(void* c, const void* a, const void* b, const void* r, int M, int N, int K,
-                    int lda, int ldb, int ldc, int ldr, int epi, int up_off, int nr, int group_m,
-                    hipStream_t st);
-int configure_gemm_dec();
 
 }  // namespace drtc

@@ -117,170 +117,6 @@ int launch_rmsnorm(void* out, void* residual, const void* x, const void* w,
   return (int)hipGetLastError();
 }
 
-// RMSNorm over the sum of a split-K GEMM's fp32 partial planes (gemm_w4 W4_PARTIAL):
-//   h = bf16(sum_s part[s] [+ residual]) written into `residual` (or h_out), out = norm(h) * w.
-// The planes are summed in fixed order (deterministic); one rounding of the projection
-// output (accumulator + residual), like the residual-epilogue GEMM forms.
-template <int VPT, bool GEMMA, bool RESID>
-__global__ __launch_bounds__(256) void rmsnorm_partials_kernel(
-    bf16_t* __restrict__ out, bf16_t* __restrict__ residual, const float* __restrict__ part,
-    int sk, int64_t plane, const bf16_t* __restrict__ w, int H, float eps, int out_stride,
-    int res_stride) {
-  const int row = blockIdx.x;
-  const int tid = threadIdx.x;
-  const float* pr = part + (int64_t)row * H;
-  float v[VPT][8];
-  float ss = 0.f;
-#pragma unroll
-  for (int i = 0; i < VPT; ++i) {
-    const int idx = (tid + i * 256) * 8;
-    if (idx < H) {
-      f32x4 a = *reinterpret_cast<const f32x4*>(pr + idx);
-      f32x4 b = *reinterpret_cast<const f32x4*>(pr + idx + 4);
-      for (int s = 1; s < sk; ++s) {
-        a += *reinterpret_cast<const f32x4*>(pr + s * plane + idx);
-        b += *reinterpret_cast<const f32x4*>(pr + s * plane + idx + 4);
-      }
-      bf16_t* rr = residual + (int64_t)row * res_stride + idx;
-      bf16x8 r;
-      if constexpr (RESID) r = load_bf16x8(rr);
-      bf16x8 h;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        float x = j < 4 ? a[j] : b[j - 4];
-        if constexpr (RESID) x += bf2f(r[j]);
-        h[j] = f2bf(x);
-        v[i][j] = bf2f(h[j]);
-        ss += v[i][j] * v[i][j];
-      }
-      store_bf16x8(rr, h);
-    }
-  }
-  __shared__ float red[4];
-  ss = wave_sum(ss);
-  if ((tid & 63) == 0) red[tid >> 6] = ss;
-  __syncthreads();
-  const float tot = red[0] + red[1] + red[2] + red[3];
-  const float rstd = rsqrtf(tot / (float)H + eps);
-  bf16_t* orow = out + (int64_t)row * out_stride;
-#pragma unroll
-  for (int i = 0; i < VPT; ++i) {
-    const int idx = (tid + i * 256) * 8;
-    if (idx < H) {
-      bf16x8 wv = load_bf16x8(w + idx);
-      bf16x8 o;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        float ww = bf2f(wv[j]);
-        if constexpr (GEMMA) ww += 1.f;
-        o[j] = f2bf(v[i][j] * rstd * ww);
-      }
-      store_bf16x8(orow + idx, o);
-    }
-  }
-}
-
-// residual: the residual stream (updated in place to h) when add_residual, else the h output.
-int launch_rmsnorm_partials(void* out, void* residual, const float* part, int sk, int rows,
-                            int H, const void* w, float eps, int out_stride, int res_stride,
-                            bool add_residual, bool gemma, hipStream_t st) {
-  const int vpt = (H / 8 + 255) / 256;
-  if (H % 8 || vpt < 1 || vpt > 4 || sk < 1 || part == nullptr || residual == nullptr ||
-      (uintptr_t)part % 16)
-    return -1;
-  if (rows == 0) return 0;
-  const int64_t plane = (int64_t)rows * H;
-  dim3 grid(rows), block(256);
-  auto o = (bf16_t*)out;
-  auto r = (bf16_t*)residual;
-  auto ww = (const bf16_t*)w;
-#define DRTC_RMSP(N, G, R)                                                                   \
-  hipLaunchKernelGGL((rmsnorm_partials_kernel<N, G, R>), grid, block, 0, st, o, r, part, sk, \
-                     plane, ww, H, eps, out_stride, res_stride)
-#define DRTC_RMSP_GR(N)                                \
-  if (gemma) {                                         \
-    if (add_residual) DRTC_RMSP(N, true, true);        \
-    else DRTC_RMSP(N, true, false);                    \
-  } else {                                             \
-    if (add_residual) DRTC_RMSP(N, false, true);       \
-    else DRTC_RMSP(N, false, false);                   \
-  }
-  switch (vpt) {
-    case 1: DRTC_RMSP_GR(1); break;
-    case 2: DRTC_RMSP_GR(2); break;
-    case 3: DRTC_RMSP_GR(3); break;
-    default: DRTC_RMSP_GR(4); break;
-  }
-#undef DRTC_RMSP_GR
-#undef DRTC_RMSP
-  return (int)hipGetLastError();
-}
-
-// rinv[m] = rsqrt(sum_s sq[m][s] / H + eps): the RMSNorm statistic of rows whose partial
-// sums of squares were emitted by a residual GEMM epilogue (gemm_w4 W4_RESIDUAL_SQ), summed in
-// fixed order (deterministic).
-__global__ __launch_bounds__(256) void rowsq_rinv_kernel(float* __restrict__ rinv,
-                                                         const float* __restrict__ sq, int M,
-                                                         int slots, int H, float eps) {
-  const int m = blockIdx.x * 256 + threadIdx.x;
-  if (m >= M) return;
-  const float* row = sq + (int64_t)m * slots;
-  float t = 0.f;
-  for (int s = 0; s < slots; s += 4) {
-    const f32x4 v = *reinterpret_cast<const f32x4*>(row + s);
-    t += v[0] + v[1] + v[2] + v[3];
-  }
-  rinv[m] = rsqrtf(t / (float)H + eps);
-}
-
-// rinv[row] = rsqrt(mean(x[row]^2) + eps) straight from the rows (a residual stream written
-// by a library GEMM): the RMSNorm's statistic without its normalised [rows, H] output.
-template <int VPT>
-__global__ __launch_bounds__(256) void row_rinv_kernel(float* __restrict__ rinv,
-                                                       const bf16_t* __restrict__ x, int H,
-                                                       int x_stride, float eps) {
-  const int row = blockIdx.x, tid = threadIdx.x;
-  const bf16_t* xr = x + (int64_t)row * x_stride;
-  float ss = 0.f;
-#pragma unroll
-  for (int i = 0; i < VPT; ++i) {
-    const int idx = (tid + i * 256) * 8;
-    if (idx < H) {
-      const bf16x8 a = load_bf16x8(xr + idx);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) ss += bf2f(a[j]) * bf2f(a[j]);
-    }
-  }
-  __shared__ float red[4];
-  ss = wave_sum(ss);
-  if ((tid & 63) == 0) red[tid >> 6] = ss;
-  __syncthreads();
-  if (tid == 0) rinv[row] = rsqrtf((red[0] + red[1] + red[2] + red[3]) / (float)H + eps);
-}
-
-int launch_row_rinv(float* rinv, const void* x, int rows, int H, int x_stride, float eps,
-                    hipStream_t st) {
-  const int vpt = (H / 8 + 255) / 256;
-  if (H % 8 || vpt < 1 || vpt > 4 || x_stride % 8) return -1;
-  if (rows == 0) return 0;
-  switch (vpt) {
-    case 1: hipLaunchKernelGGL(row_rinv_kernel<1>, dim3(rows), dim3(256), 0, st, rinv, (const bf16_t*)x, H, x_stride, eps); break;
-    case 2: hipLaunchKernelGGL(row_rinv_kernel<2>, dim3(rows), dim3(256), 0, st, rinv, (const bf16_t*)x, H, x_stride, eps); break;
-    case 3: hipLaunchKernelGGL(row_rinv_kernel<3>, dim3(rows), dim3(256), 0, st, rinv, (const bf16_t*)x, H, x_stride, eps); break;
-    default: hipLaunchKernelGGL(row_rinv_kernel<4>, dim3(rows), dim3(256), 0, st, rinv, (const bf16_t*)x, H, x_stride, eps); break;
-  }
-  return (int)hipGetLastError();
-}
-
-int launch_rowsq_rinv(float* rinv, const float* sq, int M, int slots, int H, float eps,
-                      hipStream_t st) {
-  if (M <= 0) return 0;
-  if (slots % 4 || (uintptr_t)sq % 16) return -1;
-  hipLaunchKernelGGL(rowsq_rinv_kernel, dim3((M + 255) / 256), dim3(256), 0, st, rinv, sq, M,
-                     slots, H, eps);
-  return (int)hipGetLastError();
-}
-
 // ------------------------------------------------------- gated activations
 template <int ACT>  // 0 = SiLU, 1 = tanh-GELU
 __global__ __launch_bounds__(256) void act_glu_kernel(

@@ -29,8 +29,8 @@ from .. import ops
 from ..utils import tracing
 from ..models.transformer import DecodeMeta, TransformerLM
 
-DEFAULT_BUCKETS = (1, 2, 4, 8, 16, 24, 32, 48, 64, 96, 128, 160, 192, 224, 256, 320, 384,
-                   448, 512, 640, 768, 896, 1024)
+# hipGraph batch buckets: the decode M the GEMM tuning table measured (ops/gemm.py)
+DEFAULT_BUCKETS = ops.gemm.DECODE_BUCKETS
 
 
 class DecodeRunner:

@@ -1,11 +1,15 @@
 """Decoder-only transformer (Llama-3 / Gemma / Mixtral families), inference-only.
 
 MI355X-first layout decisions
-  * fused projections: one QKV GEMM and one gate|up GEMM per layer
-    (hipBLASLt via ``ops.linear``: per-shape tuned solutions for the decode
-    buckets); everything between the GEMMs is a fused HIP
-    kernel: add+RMSNorm, RoPE + paged-KV write (in place on the QKV output),
-    MFMA attention reading q/k/v straight out of the QKV buffer, act*up;
+  * fused projections: one QKV GEMM and one gate|up GEMM per layer, routed by
+    ``ops.linear`` (ops/gemm.py): the hand-written 4-wave MFMA GEMM (gemm_w4.hip)
+    for prefill passes - gate_up with the SiLU/GELU-GLU and o / down with the
+    residual add in the epilogue - and for the full-batch decode gate_up + GLU;
+    skinny / medium-M hand kernels and per-shape tuned hipBLASLt solutions for
+    the other decode buckets.  Between the GEMMs every op is a fused HIP kernel:
+    add+RMSNorm, RoPE + paged-KV write (in place on the QKV output; in decode
+    inside the attention launch), MFMA attention reading q/k/v straight out of
+    the QKV buffer;
   * tensor parallel over RCCL: heads / intermediate columns sharded, one
     all-reduce after o_proj and one after down_proj (or the MoE combine),
     vocab-parallel LM head + all-gather;
@@ -213,7 +217,6 @@ class TransformerLM:
                     L["down"] = put(rnd(H, sh.inter))
             self.layers.append(L)
         self.final_norm = norm_w()
-        self.fold_norm_weights()
         if cfg.tie_embeddings:
             v0 = sh.rank * sh.vocab
             self.lm_head = self.embed[v0:v0 + sh.vocab]
@@ -225,33 +228,10 @@ class TransformerLM:
             else:
                 self.lm_head = put(rnd(sh.vocab, H))
 
-    def fold_norm_weights(self) -> None:
-        """Projections with the preceding RMSNorm weight folded into their input columns
-        (``qkv_n`` = W_qkv diag(g_in), ``gate_up_n`` = W_gate_up diag(g_post); Gemma: 1 + w):
-        a prefill pass whose o / down GEMM left the norm's row statistic runs these on the
-        raw residual stream and scales the rows (ops.gemm.rs_linear) instead of writing a
-        normalised copy.  With unit norm weights (random init) they alias the originals -
-        no extra memory.  Call again after loading weights."""
-        g1 = 1.0 if self.cfg.gemma_norm else 0.0
-        for L in self.layers:
-            for name, ln in (("qkv", "ln_in"), ("gate_up", "ln_post")):
-                w = L.get(name)
-                if w is None or w.dim() != 2:  # MoE experts keep the plain norm
-                    continue
-                g = L[ln].float() + g1
-                if bool((g == 1.0).all()):
-                    L[name + "_n"] = w
-                else:
-                    L[name + "_n"] = (w.float() * g[None, :]).to(w.dtype).contiguous()
-
     def weight_bytes(self) -> int:
         n = self.embed.numel() + self.final_norm.numel()
         for L in self.layers:
-            seen = set()
-            for t in L.values():
-                if t.data_ptr() not in seen:  # folded-norm aliases counted once
-                    seen.add(t.data_ptr())
-                    n += t.numel()
+            n += sum(t.numel() for t in L.values())
         if not self.cfg.tie_embeddings:
             n += self.lm_head.numel()
         return n * self.embed.element_size()
@@ -269,21 +249,17 @@ class TransformerLM:
         if self.cfg.is_moe:
             return self._moe(L, x.materialize(), decode), False
         if ops.w4_glu_ok(x.x, L["gate_up"], self.cfg.act):
-            # prefill-sized: gate_up GEMM with the GLU in its epilogue (gemm_w4.hip)
-            h = ops.norm_glu(x, L["gate_up"], self.cfg.act, L.get("gate_up_n"))
+            # prefill / full-batch decode: gate_up GEMM with the GLU in its epilogue (gemm_w4)
+            h = ops.norm_glu(x, L["gate_up"], self.cfg.act)
             res = self._fusable_residual(h, x)
             if res is not None:
-                return ops.linear_residual_rinv(h, L["down"], res, self.cfg.rms_eps), True
-            if decode and self.pc.tp_size == 1:
-                # full-batch decode: split-K partial planes summed by the next norm
-                return ops.linear_partials(h, L["down"]), False
+                return ops.linear_residual(h, L["down"], res), True
             y = ops.linear(h, L["down"])
         else:
             gu = ops.norm_linear(x, L["gate_up"])
             res = self._fusable_residual(gu, x)
             if res is not None:
-                return ops.linear_residual_rinv(ops.act_glu(gu, self.cfg.act), L["down"], res,
-                                                self.cfg.rms_eps), True
+                return ops.linear_residual(ops.act_glu(gu, self.cfg.act), L["down"], res), True
             y = ops.glu_linear(gu, L["down"], self.cfg.act)
         if decode and self.pc.tp_size > 1:
             return y, False, True  # reduced by the next norm (fused all-reduce + add + norm)
@@ -383,17 +359,13 @@ class TransformerLM:
             # residual stream in its GEMM epilogue, o IS the new stream;
             # partial = o is still a TP partial sum - the next norm runs the
             # all-reduce fused with the residual add (ParallelContext.reduce_norm)
-            # (o, rinv): the GEMM epilogue also left the next norm's row statistic
             o, added, *part = attn_fn(i, L, x)
-            o, rinv = o if isinstance(o, tuple) else (o, None)
             x = ops.PendingNorm(o, None if added else x.stream(), L["ln_post"], cfg.rms_eps,
-                                cfg.gemma_norm, pc=self.pc if part and part[0] else None,
-                                rinv=rinv)
+                                cfg.gemma_norm, pc=self.pc if part and part[0] else None)
             m, added, *part = self._mlp(L, x, decode)
-            m, rinv = m if isinstance(m, tuple) else (m, None)
             nxt = self.layers[i + 1]["ln_in"] if i + 1 < n else self.final_norm
             x = ops.PendingNorm(m, None if added else x.stream(), nxt, cfg.rms_eps, cfg.gemma_norm,
-                                pc=self.pc if part and part[0] else None, rinv=rinv)
+                                pc=self.pc if part and part[0] else None)
         return x.materialize()
 
     def _logits(self, x: torch.Tensor) -> torch.Tensor:
@@ -411,7 +383,7 @@ class TransformerLM:
         D = cfg.head_dim
 
         def attn(i, L, x):
-            qkv = ops.norm_linear(x, L["qkv"], L.get("qkv_n"))
+            qkv = ops.norm_linear(x, L["qkv"])
             kc, vc = kv_caches[i] if kv_caches is not None else (None, None)
             blockwise_v = kc is not None and meta.v_segs is not None
             ops.rope_kv_(qkv, meta.positions, meta.slots if kc is not None else None,
@@ -434,7 +406,7 @@ class TransformerLM:
                 x.select_rows(meta.last_idx)
             res = self._fusable_residual(a, x)
             if res is not None:
-                return ops.linear_residual_rinv(a, L["o"], res, cfg.rms_eps), True
+                return ops.linear_residual(a, L["o"], res), True
             return self.pc.all_reduce_tp(ops.linear(a, L["o"])), False
 
         last = len(self.layers) - 1
@@ -534,7 +506,7 @@ class TransformerLM:
             else:
                 xg = pc.all_gather_rows(x.materialize())
                 if ops.w4_glu_ok(xg, L["gate_up"], cfg.act):
-                    h = ops.mfma_gemm(xg, L["gate_up"], cfg.act, variant=7)
+                    h = ops.mfma_gemm(xg, L["gate_up"], cfg.act, variant=7, group_m=8)
                 else:
                     h = ops.act_glu(ops.linear(xg, L["gate_up"]), cfg.act)
                 m_rows = pc.reduce_scatter_rows(ops.linear(h, L["down"]))
@@ -558,11 +530,10 @@ class TransformerLM:
                                                 meta.context_lens, cfg.attn_scale, out=attn_out,
                                                 blocks_per_part=meta.blocks_per_part,
                                                 workspace=meta.workspace)
+            o = ops.linear(a.view(B, sh.hq * D), L["o"])
             if self.pc.tp_size > 1:
-                o = ops.linear(a.view(B, sh.hq * D), L["o"])
                 return o, False, True  # reduced by the next norm (fused all-reduce + add + norm)
-            # TP = 1: split-K partial planes where configured (summed by the next norm)
-            return ops.linear_partials(a.view(B, sh.hq * D), L["o"]), False
+            return o, False
 
         self._ep_begin()
         x = self._layers(self._embed(ids), attn, decode=True)

@@ -48,27 +48,6 @@ def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float, gemma: bool = False,
     return out
 
 
-def rmsnorm_partials(part, w: torch.Tensor, eps: float, gemma: bool = False,
-                     residual: torch.Tensor | None = None,
-                     out: torch.Tensor | None = None) -> tuple[torch.Tensor, torch.Tensor]:
-    """norm(sum of ``part``'s fp32 planes [+ residual]) * w for an ``ops.gemm.Partials``:
-    returns (out, h) with h = bf16(sum [+ residual]) - written into ``residual`` in place
-    when given (the residual stream), else into a new tensor."""
-    planes = part.planes
-    sk, rows, H = planes.shape
-    assert planes.dtype == torch.float32 and planes.is_contiguous()
-    assert w.shape == (H,) and w.dtype == torch.bfloat16 and w.is_contiguous()
-    add = residual is not None
-    h = residual if add else torch.empty((rows, H), dtype=torch.bfloat16, device=planes.device)
-    assert h.shape == (rows, H) and h.stride(1) == 1
-    if out is None:
-        out = torch.empty((rows, H), dtype=torch.bfloat16, device=planes.device)
-    check(hipk().rmsnorm_partials(out.data_ptr(), h.data_ptr(), planes.data_ptr(), sk, rows, H,
-                                  w.data_ptr(), float(eps), out.stride(0), h.stride(0), add,
-                                  bool(gemma), stream_ptr(planes)), "rmsnorm_partials")
-    return out, h
-
-
 class PendingNorm:
     """A pre-norm sublayer input whose RMSNorm has not run yet: norm(x [+
     residual]) * w.  The consumer either fuses the norm into its projection
@@ -78,25 +57,17 @@ class PendingNorm:
     (x itself when there is no residual), which the next PendingNorm adds to.
     """
 
-    __slots__ = ("x", "residual", "w", "eps", "gemma", "_h", "_out", "pc", "rinv")
+    __slots__ = ("x", "residual", "w", "eps", "gemma", "_h", "_out", "pc")
 
     def __init__(self, x: torch.Tensor, residual: torch.Tensor | None, w: torch.Tensor,
-                 eps: float, gemma: bool, pc=None, rinv: torch.Tensor | None = None):
+                 eps: float, gemma: bool, pc=None):
         """``pc``: a ParallelContext when ``x`` is still a tensor-parallel PARTIAL
         sum: materialize() then runs the all-reduce fused with the residual add
-        and the norm (ParallelContext.reduce_norm).  ``rinv``: x is already the
-        residual stream h and rsqrt(mean(h^2) + eps) per row is known (emitted by
-        the producing GEMM's epilogue): a consumer with the norm weight folded
-        into its projection scales its output rows instead of materialising the
-        norm (``ops.gemm.rs_linear``)."""
+        and the norm (ParallelContext.reduce_norm)."""
         self.x, self.residual, self.w, self.eps, self.gemma = x, residual, w, eps, gemma
         self.pc = pc
         self._h: torch.Tensor | None = None
         self._out: torch.Tensor | None = None
-        self.rinv = rinv
-        if rinv is not None:
-            assert residual is None and pc is None
-            self._h = x
 
     def applied(self, h: torch.Tensor) -> None:
         """Record that a fused consumer computed h = x (+ residual)."""
@@ -105,11 +76,6 @@ class PendingNorm:
     def materialize(self) -> torch.Tensor:
         if self._out is None:
             res = self.residual
-            if not isinstance(self.x, torch.Tensor):  # split-K partial planes (ops.gemm)
-                self._out, h = rmsnorm_partials(self.x, self.w, self.eps, self.gemma,
-                                                residual=res)
-                self._h, self.x, self.residual = h, h, None
-                return self._out
             if self.pc is not None:
                 self._out = self.pc.reduce_norm(self.x, res, self.w, self.eps, self.gemma)
                 self.pc = None
@@ -130,8 +96,6 @@ class PendingNorm:
         token only once its attention has read (and cached) every position."""
         if self._out is not None:
             self._out = self._out.index_select(0, idx)
-        if self.rinv is not None:
-            self.rinv = self.rinv.index_select(0, idx)
         if self._h is not None:  # x is _h (materialize / applied alias them)
             self._h = self.x = self._h.index_select(0, idx)
             return

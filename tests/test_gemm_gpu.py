@@ -1,8 +1,9 @@
-"""Hand-written CDNA4 GEMM (csrc/kernels/gemm.hip) vs a PyTorch fp32 reference of the
-same op, including the fused epilogues (residual add in place, SiLU / tanh-GELU
-gating of a [gate; up] weight), split-K with the in-launch last-arriver combine,
-row tails (M not a multiple of the 256-row tile), every pipeline variant, and
-hipGraph replay (split-K counters re-arm themselves between replays)."""
+"""Hand-written CDNA4 GEMMs vs a PyTorch fp32 reference of the same op: gemm_w4.hip (the
+4-wave MFMA GEMM) with every fused epilogue (residual add in place, SiLU / tanh-GELU gating
+of a [gate; up] weight), split-K with the in-launch last-arriver combine in both tile
+orders, row tails (M not a multiple of the 256-row tile), the persistent forms and hipGraph
+replay (split-K counters re-arm themselves between replays); gemm_midm.hip; and the
+projection router of ops.linear."""
 import pytest
 import torch
 import torch.nn.functional as F
@@ -29,7 +30,7 @@ def _check(out, ref, tol=1.5e-2):
     assert err <= tol * max(scale, 1e-3), (err, scale)
 
 
-@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 7])
+@pytest.mark.parametrize("variant", [7, 9])
 @pytest.mark.parametrize("epi", ["store", "residual", "silu", "gelu_tanh"])
 @pytest.mark.parametrize("M,N,K,splitk", [(256, 256, 256, 1), (300, 512, 512, 2), (1, 768, 1024, 4),
                                           (1024, 1024, 2048, 2), (515, 256, 384, 3)])
@@ -44,7 +45,7 @@ def test_mfma_gemm_matches_fp32(hipk, variant, epi, M, N, K, splitk):
     _check(out, ref)
 
 
-@pytest.mark.parametrize("variant", [1, 5, 7])
+@pytest.mark.parametrize("variant", [7, 9])
 def test_mfma_gemm_residual_in_place_and_strided(hipk, variant):
     """o / down projection adding into the residual stream in place; x is a
     column slice of a wider buffer (row stride > K)."""
@@ -59,7 +60,7 @@ def test_mfma_gemm_residual_in_place_and_strided(hipk, variant):
     _check(h, ref)
 
 
-@pytest.mark.parametrize("variant", [5, 7])
+@pytest.mark.parametrize("variant", [7, 9])
 def test_mfma_gemm_graph_replay_splitk(hipk, variant):
     """Split-K inside a hipGraph: counters are re-armed by each tile's last
     arriver, so replays with new inputs stay exact."""
@@ -164,11 +165,12 @@ def test_linear_dispatches_midm_from_table(hipk):
 
 
 @pytest.mark.parametrize("epi", ["store", "residual", "silu"])
-@pytest.mark.parametrize("M,N,K,splitk", [(1024, 1024, 1024, 4), (300, 512, 2048, 2), (1024, 2048, 4096, 4),
-                                          (700, 768, 1536, 4)])
-def test_w4_reduce_scatter_splitk(hipk, epi, M, N, K, splitk):
-    """gemm_w4's reduce-scatter split-K (variant 11): every slice finishes part of the tile
-    from the others' write-through partials; counters re-arm for the next call (run twice)."""
+@pytest.mark.parametrize("M,N,K,splitk,gm", [(1024, 4096, 4096, 4, -4), (1024, 4096, 4096, 2, -2),
+                                             (512, 2048, 1024, 8, -2), (1000, 1024, 2048, 4, -1)])
+def test_w4_splitk_xcd_slice_order(hipk, epi, M, N, K, splitk, gm):
+    """Split-K in the K-slice-by-XCD tile order (group_m < 0: the block labels b % 8 split
+    into K slices x tile subsets): every (tile, slice) pair is computed exactly once whatever
+    the placement; counters re-arm (run twice)."""
     g = torch.Generator(device="cuda").manual_seed(M + N + K + splitk)
     x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16, generator=g)
     w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16, generator=g) * 0.05
@@ -177,184 +179,22 @@ def test_w4_reduce_scatter_splitk(hipk, epi, M, N, K, splitk):
     ref = _ref(x, w, epi, res)
     for _ in range(2):
         r_in = res.clone() if res is not None else None
-        out = G.mfma_gemm(x, w, epi, residual=r_in, out=r_in, variant=11, splitk=splitk)
+        out = G.mfma_gemm(x, w, epi, residual=r_in, out=r_in, variant=7, splitk=splitk,
+                          group_m=gm)
         torch.cuda.synchronize()
         _check(out, ref)
 
 
-# ------------------------------------------- split-K partial planes summed by the next norm
-@pytest.mark.parametrize("M,N,K,sk", [(800, 512, 1024, 4), (1024, 4096, 14336, 4),
-                                      (1024, 4096, 4096, 4), (777, 256, 512, 2)])
-@pytest.mark.parametrize("gemma", [False, True])
-def test_linear_partials_through_pending_norm(hipk, monkeypatch, M, N, K, sk, gemma):
-    """gemm_w4 W4_PARTIAL + rmsnorm_partials (decode o / down at TP = 1): the pending norm
-    of the planes equals norm(x @ w.T + residual) in fp32 within bf16 rounding, the
-    residual stream is updated in place to h, and the pair replays from a hipGraph."""
-    from drtc_amd import ops
-    from drtc_amd.ops import gemm as Gm
-
-    monkeypatch.setattr(Gm, "W4_PARTIAL", {(N, K): sk})
-    g = torch.Generator(device="cuda").manual_seed(M + N + K)
-    x = torch.randn(M, K, device="cuda", generator=g).to(torch.bfloat16)
-    w = (torch.randn(N, K, device="cuda", generator=g) / K ** 0.5).to(torch.bfloat16)
-    res = torch.randn(M, N, device="cuda", generator=g).to(torch.bfloat16)
-    nw = (torch.rand(N, device="cuda", generator=g) + 0.5).to(torch.bfloat16)
-    h_ref = x.float() @ w.float().t() + res.float()
-    hf = h_ref.to(torch.bfloat16).float()
-    ww = nw.float() + (1.0 if gemma else 0.0)
-    out_ref = hf * torch.rsqrt(hf.pow(2).mean(-1, keepdim=True) + 1e-5) * ww
-    part = ops.linear_partials(x, w)
-    assert isinstance(part, ops.Partials) and part.sk == sk and tuple(part.shape) == (M, N)
-    r1 = res.clone()
-    p = ops.PendingNorm(part, r1, nw, 1e-5, gemma)
-    out = p.materialize()
-    torch.cuda.synchronize()
-    assert p.stream().data_ptr() == r1.data_ptr()
-    assert _rel(r1, h_ref) < 1e-2
-    assert _rel(out, out_ref) < 2e-2
-    # graph capture of the producer / consumer pair, replayed on fresh inputs
-    r2 = res.clone()
-    o2 = torch.empty_like(out)
-    gr = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(gr):
-        pp = ops.PendingNorm(ops.linear_partials(x, w), r2, nw, 1e-5, gemma)
-        o2.copy_(pp.materialize())
-    r2.copy_(res)
-    gr.replay()
-    torch.cuda.synchronize()
-    assert torch.equal(o2, out) and torch.equal(r2, r1)
-
-
-def test_decode_with_partials_matches_reference(hipk, monkeypatch):
-    """The engine's full-batch decode with o / down as split-K partial planes (batch 800 >=
-    W4_PARTIAL_MIN_M: 3 full 256-row tiles + a 32-row one, hipGraphs): every greedy token is
-    a maximiser (within bf16 tolerance) of the full-sequence reference forward's logits."""
-    from drtc_amd.engine import LLMEngine, SamplingParams
-    from drtc_amd.models import TINY_LLAMA, TransformerLM
-    from drtc_amd.ops import gemm as Gm
-
-    monkeypatch.setattr(Gm, "W4_PARTIAL", {(256, 256): 4, (256, 512): 4})
-    prompts = [[1 + (7 * i + j) % 500 for j in range(5 + i % 23)] for i in range(800)]
-    m = TransformerLM(TINY_LLAMA, "cuda", seed=21)
-    eng = LLMEngine(m, max_batch=800, max_model_len=256, num_blocks=2048, use_graphs=True)
-    reqs = eng.generate(prompts, SamplingParams.greedy(6, ignore_eos=True))
-    bad = []
-    for i, (p, r) in enumerate(zip(prompts, reqs)):
-        ref = m.forward_reference([p + r.output_ids[:-1]])[0].float()
-        for j, tok in enumerate(r.output_ids):
-            row = ref[len(p) - 1 + j]
-            if row[tok] < row.max() - 0.05 * max(1.0, row.abs().max().item()):
-                bad.append((i, j))
-    assert not bad, bad[:10]
-
-
-# --------------------------------------------------- RMSNorm folded across a prefill layer
-@pytest.mark.parametrize("M,N,K", [(4096, 512, 1024), (4500, 4096, 4096), (4096, 4096, 14336)])
-def test_linear_residual_rinv(hipk, monkeypatch, M, N, K):
-    """residual += x @ w.T with the next norm's row statistic: from the gemm_w4 epilogue
-    (partial sums of squares, W4_RESIDUAL_SQ) or, for the library's long-K shape, from one
-    read of the rows; h and rinv against fp32."""
-    from drtc_amd import ops
-    from drtc_amd.ops import gemm as Gm
-
-    monkeypatch.setattr(Gm, "_fold_norm", True)
-
-    g = torch.Generator(device="cuda").manual_seed(M + K)
-    x = torch.randn(M, K, device="cuda", generator=g).to(torch.bfloat16)
-    w = (torch.randn(N, K, device="cuda", generator=g) / K ** 0.5).to(torch.bfloat16)
-    res = torch.randn(M, N, device="cuda", generator=g).to(torch.bfloat16)
-    h_ref = x.float() @ w.float().t() + res.float()
-    h, rinv = ops.linear_residual_rinv(x, w, res, 1e-5)
-    assert h.data_ptr() == res.data_ptr() and rinv is not None and rinv.shape == (M,)
-    assert _rel(h, h_ref) < 1e-2
-    r_ref = torch.rsqrt(h.float().pow(2).mean(-1) + 1e-5)  # of the stored (bf16) stream
-    assert ((rinv - r_ref).abs() / r_ref).max().item() < 1e-4
-
-
-@pytest.mark.parametrize("act", [None, "silu", "gelu_tanh"])
-@pytest.mark.parametrize("gemma", [False, True])
-def test_rs_linear_equals_norm_then_linear(hipk, act, gemma):
-    """(h @ (W diag(g)).T) * rinv[row] (gemm_w4 *_RS epilogues, the norm weight folded into
-    W) equals the projection of the materialised RMSNorm within bf16 rounding."""
-    from drtc_amd import ops
-
-    M, H, N = 4352, 1024, 1536 if act is None else 2048
-    g = torch.Generator(device="cuda").manual_seed(7)
-    h = torch.randn(M, H, device="cuda", generator=g).to(torch.bfloat16)
-    nw = (torch.rand(H, device="cuda", generator=g) * 0.5 + (0.0 if gemma else 0.75)).to(torch.bfloat16)
-    w = (torch.randn(N, H, device="cuda", generator=g) / H ** 0.5).to(torch.bfloat16)
-    gam = nw.float() + (1.0 if gemma else 0.0)
-    w_f = (w.float() * gam[None, :]).to(torch.bfloat16)
-    rinv = torch.rsqrt(h.float().pow(2).mean(-1) + 1e-6)
-    xn = h.float() * rinv[:, None] * gam[None, :]
-    ref = xn @ w.float().t()
-    if act is not None:
-        I = N // 2
-        gt, up = ref[:, :I], ref[:, I:]
-        ref = (torch.nn.functional.silu(gt) if act == "silu"
-               else torch.nn.functional.gelu(gt, approximate="tanh")) * up
-    y = ops.rs_linear(h, w_f, rinv.contiguous(), act)
-    assert y is not None
-    assert _rel(y, ref) < 2e-2
-    # the engine's path: a PendingNorm carrying rinv
-    p = ops.PendingNorm(h, None, nw, 1e-6, gemma, rinv=rinv.contiguous())
-    y2 = ops.norm_linear(p, w, w_f) if act is None else ops.norm_glu(p, w, act, w_f)
-    assert torch.equal(y2, y) and p._out is None and p.stream().data_ptr() == h.data_ptr()
-
-
-def test_prefill_with_folded_norms_matches_reference(hipk, monkeypatch):
-    """A 2-layer model with H = 512 at a 4.4k-token prefill chunk: o / down leave the norm's
-    row statistic, qkv / gate_up run on the residual stream with folded (non-unit) norm
-    weights; logits agree with the unfolded HIP path and with the fp32 reference path."""
-    from drtc_amd import ops
-    from drtc_amd.models import TINY_LLAMA, TransformerLM
-    from drtc_amd.models.transformer import PrefillMeta
-    from drtc_amd.ops import gemm as Gm
-
-    cfg = TINY_LLAMA.replace(hidden_size=512, intermediate_size=1024, num_heads=8,
-                             num_kv_heads=8, head_dim=64, max_position=512)
-    m = TransformerLM(cfg, "cuda", seed=4)
-    g = torch.Generator().manual_seed(5)
-    for L in m.layers:  # non-unit norm weights: the folded copies are real copies
-        L["ln_in"].copy_((torch.rand(512, generator=g) + 0.5).to(torch.bfloat16))
-        L["ln_post"].copy_((torch.rand(512, generator=g) + 0.5).to(torch.bfloat16))
-    m.fold_norm_weights()
-    assert m.layers[0]["qkv_n"].data_ptr() != m.layers[0]["qkv"].data_ptr()
-    lens = [100 + (7 * i) % 60 for i in range(34)]
-    T = sum(lens)
-    assert T >= 4096
-    ids = torch.randint(3, 500, (T,), device="cuda", dtype=torch.int64)
-    cu = [0]
-    for n in lens:
-        cu.append(cu[-1] + n)
-    pos = torch.cat([torch.arange(n) for n in lens]).to(torch.int32).cuda()
-    last = torch.tensor(cu[1:], dtype=torch.int64, device="cuda") - 1
-
-    def run():
-        meta = PrefillMeta(positions=pos, slots=torch.full((T,), -1, dtype=torch.int64, device="cuda"),
-                           cu_seqlens=torch.tensor(cu, dtype=torch.int32, device="cuda"), cu_host=cu,
-                           tiles=None, last_idx=last, max_len=max(lens))
-        return m.forward_prefill(ids, meta, None).float()
-
-    monkeypatch.setattr(Gm, "_fold_norm", True)
-    folded = run()
-    monkeypatch.setattr(Gm, "_fold_norm", False)
-    plain = run()
-    with ops.reference_mode():
-        ref = run()
-    scale = max(1.0, ref.abs().max().item())
-    assert (folded - plain).abs().max().item() < 0.03 * scale
-    assert (folded - ref).abs().max().item() < 0.05 * scale
-
-
-# ------------------------------------------------------ gemm_w4 persistent form (variant 15)
+# ------------------------------------------------------ gemm_w4 persistent forms (15 / 31)
+@pytest.mark.parametrize("variant", [15, 31])
 @pytest.mark.parametrize("epi", ["store", "residual", "silu", "gelu_tanh"])
 @pytest.mark.parametrize("M,N,K", [(8192, 8192, 128), (4500, 4096, 576), (2300, 8192, 192),
-                                   (300, 512, 512), (1, 768, 1024)])
-def test_w4_persistent_matches_fp32(hipk, epi, M, N, K):
+                                   (1024, 4096, 1088), (2048, 2048, 512)])
+def test_w4_persistent_matches_fp32(hipk, variant, epi, M, N, K):
     """Persistent gemm_w4: min(tiles, CUs) workgroups walk the tile order and each tile's
     last two K steps stage the next tile's first two (odd and even K-tile counts, a partial
-    last row tile, several tiles per workgroup, in-place residual)."""
+    last row tile, several tiles per workgroup, in-place residual).  Variant 31 runs each
+    XCD label's K loop from its own eighth of K (wrapping), so its sums are reordered."""
     g = torch.Generator(device="cuda").manual_seed(M + 3 * N + 7 * K)
     x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16, generator=g)
     w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16, generator=g) * 0.05
@@ -362,13 +202,13 @@ def test_w4_persistent_matches_fp32(hipk, epi, M, N, K):
     res = torch.randn(M, nout, device="cuda", dtype=torch.bfloat16, generator=g) if epi == "residual" else None
     ref = _ref(x, w, epi, res)
     if epi == "residual":
-        out = G.mfma_gemm(x, w, epi, residual=res, out=res, variant=15)
+        out = G.mfma_gemm(x, w, epi, residual=res, out=res, variant=variant)
         assert out.data_ptr() == res.data_ptr()
     else:
-        out = G.mfma_gemm(x, w, epi, variant=15)
+        out = G.mfma_gemm(x, w, epi, variant=variant)
     _check(out, ref)
     # the same call on the per-tile form agrees bit for bit (same MFMA order per tile)
-    if epi != "residual":
+    if epi != "residual" and variant == 15:
         _check(out, G.mfma_gemm(x, w, epi, variant=7).float(), tol=1e-6)
 
 
@@ -381,3 +221,54 @@ def test_w4_persistent_rejects_single_k_tile_and_splitk(hipk):
     w = torch.randn(256, 512, device="cuda", dtype=torch.bfloat16)
     with pytest.raises(RuntimeError):
         G.mfma_gemm(x, w, variant=15, splitk=2)
+    with pytest.raises(RuntimeError):
+        G.mfma_gemm(x, w, variant=31)  # 2 x 1 tiles: fewer than one per XCD label
+
+
+# ------------------------------------------------------------------ projection router
+def test_router_covers_every_served_decode_shape(hipk):
+    """Every projection ops.linear serves for the TP = 1 models, at every hipGraph bucket up
+    to the LLM server's default batch, the default batch itself and off-bucket batches,
+    resolves to a hand kernel, a tuned library solution, or - at a bucket the tuner measured
+    it fastest - the library's heuristic pick; an off-bucket M takes its bucket-above route
+    (never an unmeasured path), and prefill-sized M never falls to torch."""
+    from drtc_amd.llm.server import default_max_batch
+    from drtc_amd.models import get_config
+
+    G.reset()
+    for name in ("llama-3-8b", "gemma-2b", "mixtral-8x7b", "llama-3-70b"):
+        cfg = get_config(name)
+        H, D = cfg.hidden_size, cfg.head_dim
+        shapes = {"qkv": ((cfg.num_heads + 2 * cfg.num_kv_heads) * D, H),
+                  "o": (H, cfg.num_heads * D), "lm_head": (cfg.vocab_size, H)}
+        if not cfg.is_moe:
+            shapes["down"] = (H, cfg.intermediate_size)
+            shapes["gate_up"] = (2 * cfg.intermediate_size, H)
+        top = default_max_batch(name)
+        ms = sorted({b for b in G.DECODE_BUCKETS if b <= top} | {top, 208, 1000, 16384})
+        for proj, (N, K) in shapes.items():
+            for M in ms:
+                if proj == "gate_up" and M >= G.W4_GLU_MIN_M:
+                    continue  # the fused-GLU hand GEMM (norm_glu), not linear
+                kind, arg = G.route(M, N, K, K)
+                assert kind in ("w4", "lt", "skinny", "midm", "torch"), (name, proj, M, kind)
+                if M > G.DECODE_MAX_M:
+                    assert kind in ("w4", "lt"), (name, proj, M, kind)
+                elif M not in G.DECODE_BUCKETS:
+                    Mb = next(b for b in G.DECODE_BUCKETS if b >= M)
+                    kb = G.route(Mb, N, K, K)
+                    assert kind == kb[0] or (kb[0] == "skinny" and kind == "torch"), \
+                        (name, proj, M, kind, Mb, kb)
+                ent = G._activate().get((M, N, K, K))
+                if ent is not None:
+                    assert kind != "torch", (name, proj, M, ent)
+
+
+def test_linear_off_bucket_matches_fp32(hipk):
+    """An off-bucket decode batch (M = 208, Llama-3-70B down shape scaled down to the
+    8B's) runs its bucket-above route and matches fp32."""
+    g = torch.Generator(device="cuda").manual_seed(9)
+    for M, N, K in ((208, 4096, 14336), (1000, 6144, 4096), (200, 4096, 4096)):
+        x = torch.randn(M, K, device="cuda", generator=g).to(torch.bfloat16)
+        w = (torch.randn(N, K, device="cuda", generator=g) * 0.02).to(torch.bfloat16)
+        assert _rel(G.linear(x, w), x.float() @ w.float().t()) < 1e-2, (M, N, K)

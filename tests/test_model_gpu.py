@@ -138,8 +138,8 @@ def test_prefill_residual_in_gemm_epilogue(hipk, cfg, monkeypatch):
     monkeypatch.setattr(gemm, "RESIDUAL_FUSE_MIN_M", 1 << 30)
     unfused = m.forward_reference(seqs)
     calls = []
-    real = ops.linear_residual_rinv  # (the model's entry: the residual GEMM + norm statistic)
-    monkeypatch.setattr(ops, "linear_residual_rinv", lambda *a: calls.append(1) or real(*a))
+    real = ops.linear_residual
+    monkeypatch.setattr(ops, "linear_residual", lambda *a: calls.append(1) or real(*a))
     monkeypatch.setattr(gemm, "RESIDUAL_FUSE_MIN_M", 16)
     fused = m.forward_reference(seqs)
     assert len(calls) == 2 * cfg.num_layers * len(seqs)
