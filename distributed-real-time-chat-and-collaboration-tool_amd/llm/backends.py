@@ -96,14 +96,17 @@ class EngineBackend:
 
 
 # ------------------------------------------------------------- DP workers
-def _worker_main(rank: int, device: str, model_name: str, engine_kw: dict, inq, outq, seed: int,
-                 hb_interval: float = 0.5):
+def _worker_main(rank: int, device: str, model_name: str, engine_kw: dict, inq, outqs, ctlq,
+                 seed: int, hb_interval: float = 0.5):
     """One engine replica per GPU (separate process: one process per GPU).
 
-    Besides results, the worker sends a heartbeat with its engine counters
-    every ``hb_interval`` s; the parent's health monitor evicts a replica
-    whose process died or whose heartbeats stopped (SURVEY §5 failure
-    detection: per-GPU replica eviction)."""
+    Requests arrive on ``inq`` as (front-end, request id, prompt ids or text, params); the
+    completions of each engine step go back to the front-end that sent them, one message
+    per front-end (``outqs[fe]``: several gRPC front-end processes can share one replica,
+    llm/frontends.py).  Besides results, the worker sends a heartbeat with its engine
+    counters every ``hb_interval`` s on ``ctlq``; the owner's health monitor evicts a replica
+    whose process died or whose heartbeats stopped (SURVEY §5 failure detection: per-GPU
+    replica eviction)."""
     import torch
 
     from ..engine.engine import EngineLoop, LLMEngine, freeze_gc
@@ -122,9 +125,9 @@ def _worker_main(rank: int, device: str, model_name: str, engine_kw: dict, inq, 
         eng.warmup(capture=True)
         freeze_gc()  # this process only serves the engine from here on
         loop = EngineLoop(eng).start()
-        outq.put(("ready", rank, None))
+        ctlq.put(("ready", rank, None))
     except BaseException as e:  # report start-up failures to the parent
-        outq.put(("fatal", rank, repr(e)))
+        ctlq.put(("fatal", rank, repr(e)))
         return
     pending = {}
     parent = os.getppid()
@@ -134,6 +137,7 @@ def _worker_main(rank: int, device: str, model_name: str, engine_kw: dict, inq, 
     # host work), and ships each burst of completions as ONE queue message
     done_q: queue.SimpleQueue = queue.SimpleQueue()
     text_rids: set = set()  # requests submitted as prompt text: reply with text as well
+    fe_requests: dict[int, int] = {}  # requests received per front-end (heartbeat stats)
 
     def watcher():
         last_hb = 0.0
@@ -151,14 +155,16 @@ def _worker_main(rank: int, device: str, model_name: str, engine_kw: dict, inq, 
             except queue.Empty:
                 pass
             if batch:
-                out = []
+                out: dict[int, list] = {}
                 for r in batch:
-                    if pending.pop(r.request_id, None) is not None:
+                    ent = pending.pop(r.request_id, None)
+                    if ent is not None:
                         text = tok.decode(r.output_ids) if r.request_id in text_rids else None
                         text_rids.discard(r.request_id)
-                        out.append((r.request_id, (r.output_ids, r.finish_reason, text)))
-                if out:
-                    outq.put(("done_batch", rank, out))
+                        out.setdefault(ent[0], []).append(
+                            (r.request_id, (r.output_ids, r.finish_reason, text)))
+                for fe, items in out.items():
+                    outqs[fe].put(("done_batch", rank, items))
             if not loop.alive():  # engine fault: exit so the parent evicts/respawns us
                 log.error("engine loop of replica %d died: %r", rank, loop.error)
                 os._exit(3)
@@ -167,8 +173,9 @@ def _worker_main(rank: int, device: str, model_name: str, engine_kw: dict, inq, 
                 last_hb = now
                 st = dict(eng.stats)
                 st.update(running=len(eng.running), waiting=len(eng.waiting),
-                          pending=len(pending), alive=loop.alive())
-                outq.put(("hb", rank, st))
+                          pending=len(pending), alive=loop.alive(),
+                          fe_requests=dict(fe_requests))
+                ctlq.put(("hb", rank, st))
 
     threading.Thread(target=watcher, daemon=True).start()
     while True:
@@ -176,21 +183,22 @@ def _worker_main(rank: int, device: str, model_name: str, engine_kw: dict, inq, 
         if msg is None:
             break
         if msg[0] == "abort":  # the caller gave up: free the slot / KV blocks
-            r = pending.get(msg[1])
-            if r is not None:
-                eng.abort(r)
+            ent = pending.get(msg[2])
+            if ent is not None:
+                eng.abort(ent[1])
             continue
-        rid, ids, prm = msg
+        fe, rid, ids, prm = msg
+        fe_requests[fe] = fe_requests.get(fe, 0) + 1
         if isinstance(ids, str):  # prompt text: fit + tokenize here (ReplicaRouter)
             ids = fit_prompt(tok, ids, eng.max_model_len - prm.max_new_tokens - 1)
             text_rids.add(rid)
         r = Request(ids, prm, request_id=rid, on_done=done_q.put)
-        pending[rid] = r
+        pending[rid] = (fe, r)
         try:
             loop.submit(r)
         except Exception as e:
             pending.pop(rid, None)
-            outq.put(("done", rid, ([], f"error: {e}")))
+            outqs[fe].put(("done", rid, ([], f"error: {e}")))
     loop.stop()
 
 
@@ -244,8 +252,8 @@ class WorkerPool:
         self.inqs[w] = self._ctx.Queue()
         self.procs[w] = self._ctx.Process(
             target=_worker_main, daemon=True,
-            args=(w, self.devices[w], self.model_name, self.engine_kw, self.inqs[w], self.outq,
-                  self.seed, self.hb_interval))
+            args=(w, self.devices[w], self.model_name, self.engine_kw, self.inqs[w], [self.outq],
+                  self.outq, self.seed, self.hb_interval))
         self.procs[w].start()
 
     def _collect(self):
@@ -347,7 +355,7 @@ class WorkerPool:
                 ev.set()
                 self.load[worker] -= 1
                 return rid, ev, slot
-        self.inqs[worker].put((rid, ids, params))
+        self.inqs[worker].put((0, rid, ids, params))
         return rid, ev, slot
 
     def release(self, rid):
@@ -363,7 +371,7 @@ class WorkerPool:
             w = f[2] if f is not None and not f[1] else None
         if w is not None and self.inqs[w] is not None:
             try:
-                self.inqs[w].put(("abort", rid))
+                self.inqs[w].put(("abort", 0, rid))
             except (OSError, ValueError):
                 pass
         self.release(rid)

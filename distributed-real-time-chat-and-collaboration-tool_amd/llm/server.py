@@ -157,8 +157,13 @@ def build_feature_backends(args, specs: list[str]):
     return FeatureRouter(by_feature, default)
 
 
-def serve(backend, port: int = 50055, workers: int = 64, bind: str = "[::]", params=None):
-    server = grpc.server(futures.ThreadPoolExecutor(max_workers=workers))
+def serve(backend, port: int = 50055, workers: int = 64, bind: str = "[::]", params=None,
+          reuse_port: bool = False):
+    """Thread-pool gRPC server of the four RPCs over ``backend``.  ``reuse_port``: several
+    front-end processes bind the same port (SO_REUSEPORT, llm/frontends.py); off by default
+    so that a second server on a taken port fails instead of silently sharing it."""
+    server = grpc.server(futures.ThreadPoolExecutor(max_workers=workers),
+                         options=[("grpc.so_reuseport", 1 if reuse_port else 0)])
     add_servicer(server, LLM_SERVICE, LLMServicer(backend, params))
     if server.add_insecure_port(f"{bind}:{port}") == 0:
         raise RuntimeError(f"cannot bind port {port}")
@@ -246,12 +251,41 @@ def main(argv=None):
     ap.add_argument("--frontend", choices=("threads", "aio"), default="threads",
                     help="gRPC front-end: a handler thread per in-flight RPC, or grpc.aio "
                          "coroutines on one event-loop thread")
+    ap.add_argument("--frontends", type=int, default=1,
+                    help="gRPC front-end processes sharing the port (SO_REUSEPORT) over the "
+                         "engine replicas (llm/frontends.py); 1 = this process")
     ap.add_argument("--serve", action="append", default=[], metavar="FEATURE=MODEL[@GPUS][:tpN]",
                     help="host FEATURE (smart | summary | answer | suggest) on its own engine "
                          "group (repeatable; see the module docstring)")
     ap.add_argument("--log-level", default="INFO")
     args = parse_with_config(ap, argv)
     setup_logging(args.log_level)
+    if args.frontends > 1 and not args.serve and args.backend == "engine" and args.tp == 1:
+        import torch
+
+        from ..models import get_config
+        from .frontends import serve_fleet
+
+        if not args.max_batch:
+            args.max_batch = default_max_batch(args.model, args.tp)
+        cfg = get_config(args.model)
+        n = max(1, args.gpus)
+        devices = [f"cuda:{i}" for i in range(n)] if torch.cuda.is_available() else ["cpu"] * n
+        group = serve_fleet(args.model, devices,
+                            dict(max_batch=args.max_batch, max_model_len=args.max_model_len,
+                                 use_graphs=not args.no_graphs),
+                            args.frontends, args.port,
+                            (cfg.vocab_size, cfg.bos_token_id, cfg.eos_token_id),
+                            args.max_model_len,
+                            workers=args.workers or args.max_batch * n // args.frontends + 64)
+        log.info("LLM server on port %d: %d front-end processes over %d engine replicas (%s)",
+                 args.port, args.frontends, n, args.model)
+        stop = threading.Event()
+        signal.signal(signal.SIGINT, lambda *a: stop.set())
+        signal.signal(signal.SIGTERM, lambda *a: stop.set())
+        stop.wait()
+        group.stop()
+        return
     if args.serve:
         backend = build_feature_backends(args, args.serve)
         # a handler thread per request any of the engine groups can hold at once

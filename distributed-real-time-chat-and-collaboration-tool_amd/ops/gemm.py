@@ -164,7 +164,13 @@ def _prefill_algo(M: int, N: int, K: int, ldx: int, beta: int) -> int:
 
 
 def _resolve(M: int, N: int, K: int, ldx: int) -> tuple[str, int]:
-    _activate()
+    tab = _activate()
+    ent = tab.get((M, N, K, ldx))
+    if M > DECODE_MAX_M and ent is not None and ent[0] >= 0:
+        # a decode batch above the 1024 buckets that was tuned as such (Gemma-2B's 2048)
+        with _lock:
+            if hipk().lt_set_algo(M, N, K, ldx, N, ent[0]) == 0:
+                return ("lt", ent[0])
     if M > DECODE_MAX_M:
         if w4_shape_ok(M, N, K):
             return ("w4", 0)

@@ -68,6 +68,11 @@ def build_backend(args):
                                             cfg.eos_token_id)), eng
 
 
+# one HTTP/2 connection per stub (no shared subchannel): a service with several front-end
+# processes on one port (SO_REUSEPORT) balances per connection
+_OPTS = [("grpc.use_local_subchannel_pool", 1)]
+
+
 def run_load(target, n_requests: int, threads: int, seed: int):
     """``threads`` client threads issue ``n_requests`` GetSmartReply RPCs in
     total; returns (latencies s, errors, wall start, wall end, finish wall times)."""
@@ -78,7 +83,7 @@ def run_load(target, n_requests: int, threads: int, seed: int):
             r = stub.GetSmartReply(raft_pb.SmartReplyRequest(token=token, channel_id="general"),
                                    timeout=120)
             assert r.success and len(r.suggestions) == 3
-        stubs = [make_stub(grpc.insecure_channel(address), RAFT_SERVICE) for _ in range(8)]
+        stubs = [make_stub(grpc.insecure_channel(address, options=_OPTS), RAFT_SERVICE) for _ in range(8)]
     else:
         histories = [[llm_pb.Message(sender=m.sender, content=m.content)
                       for m in channel_history(rng, 5)] for _ in range(64)]
@@ -87,7 +92,7 @@ def run_load(target, n_requests: int, threads: int, seed: int):
             r = stub.GetSmartReply(llm_pb.SmartReplyRequest(
                 recent_messages=histories[rng.randrange(len(histories))]), timeout=120)
             assert len(r.suggestions) == 3
-        stubs = [make_stub(grpc.insecure_channel(address), LLM_SERVICE) for _ in range(8)]
+        stubs = [make_stub(grpc.insecure_channel(address, options=_OPTS), LLM_SERVICE) for _ in range(8)]
     lat, errors, lock, it = [], [], threading.Lock(), iter(range(n_requests))
     fin = []
 
@@ -122,7 +127,7 @@ def run_open_loop(target, n_requests: int, rate: float, seed: int):
     mode, address, token = target
     rng = random.Random(seed)
     if mode == "raft":
-        stubs = [make_stub(grpc.insecure_channel(address), RAFT_SERVICE) for _ in range(8)]
+        stubs = [make_stub(grpc.insecure_channel(address, options=_OPTS), RAFT_SERVICE) for _ in range(8)]
 
         def req(stub):
             return stub.GetSmartReply.future(
@@ -130,7 +135,7 @@ def run_open_loop(target, n_requests: int, rate: float, seed: int):
     else:
         histories = [[llm_pb.Message(sender=m.sender, content=m.content)
                       for m in channel_history(rng, 5)] for _ in range(64)]
-        stubs = [make_stub(grpc.insecure_channel(address), LLM_SERVICE) for _ in range(8)]
+        stubs = [make_stub(grpc.insecure_channel(address, options=_OPTS), LLM_SERVICE) for _ in range(8)]
 
         def req(stub):
             return stub.GetSmartReply.future(llm_pb.SmartReplyRequest(
@@ -190,6 +195,9 @@ def main():
     ap.add_argument("--mode", choices=("direct", "raft"), default="direct")
     ap.add_argument("--frontend", choices=("threads", "aio"), default="threads",
                     help="LLM service front-end (llm/server.py --frontend)")
+    ap.add_argument("--frontends", type=int, default=1,
+                    help="--backend pool: gRPC front-end processes sharing the port over the "
+                         "engine replica (llm/frontends.py)")
     ap.add_argument("--requests", type=int, default=1024)
     ap.add_argument("--concurrency", type=int, default=256)
     ap.add_argument("--max-batch", type=int, default=512)
@@ -198,10 +206,27 @@ def main():
                          "closed-loop clients); reports p50/p99 latency and engine TPOT")
     args = ap.parse_args()
 
-    backend, eng = build_backend(args)
     fp = FeatureParams(ignore_eos=True)  # full 48-token budget per reply (random weights)
     port = free_port()
-    if args.frontend == "aio":
+    group = None
+    if args.frontends > 1:
+        assert args.backend == "pool", "--frontends needs --backend pool"
+        from drtc_amd.llm.frontends import serve_fleet
+        from drtc_amd.models import get_config
+
+        cfg = get_config(args.model)
+        group = serve_fleet(args.model, ["cuda:0"], dict(max_batch=args.max_batch,
+                                                        max_model_len=2048),
+                            args.frontends, port,
+                            (cfg.vocab_size, cfg.bos_token_id, cfg.eos_token_id), 2048,
+                            workers=args.concurrency // args.frontends + 64, bind="127.0.0.1",
+                            params=fp)
+        backend, eng, llm_srv = None, None, group
+    else:
+        backend, eng = build_backend(args)
+    if group is not None:
+        pass
+    elif args.frontend == "aio":
         llm_srv = serve_aio(backend, port=port, bind="127.0.0.1", params=fp)
     else:
         llm_srv = serve_llm(backend, port=port, bind="127.0.0.1", params=fp,
@@ -228,7 +253,7 @@ def main():
         if eng is not None:
             eng.stats.clear()
         METRICS.reset()
-        pool = getattr(backend, "pool", None)
+        pool = getattr(backend, "pool", None) if group is None else group.fleet
         if pool is not None:  # replica counters arrive with the heartbeats
             time.sleep(2 * pool.hb_interval)
         rs0 = pool.health() if pool is not None else None

@@ -257,6 +257,13 @@ def test_paged_decode_fused_rope(hipk, monkeypatch, D, Hq, Hkv, ctx_lens, bpp):
     _close(kc2, kc1, 1e-2, 1e-2, "k cache")
     assert torch.equal(vc2, vc1)
     assert torch.equal(qkv2, qkv)  # the QKV rows are read, never rotated in place
+    # and directly against the plain-PyTorch fp32 references of the two ops it fuses
+    kc3, vc3, qkv3 = kc.clone(), vc.clone(), qkv.clone()
+    ops.rope_kv_ref(qkv3, pos, slots, cs, Hq, Hkv, D, kc3, vc3, ops.KV_BLOCK)
+    ref32 = ops.paged_decode_ref(qkv3[:, :Hq * D].reshape(B, Hq, D), kc3, vc3, bt, cl, scale)
+    _close(out, ref32, 2e-2, 2e-2, "fused rope attention vs fp32 reference")
+    _close(kc2, kc3, 1e-2, 1e-2, "k cache vs fp32 reference")
+    assert torch.equal(vc2, vc3)
     for b, c in enumerate(ctx_lens):
         if c == 0:
             assert out[b].abs().max().item() == 0.0

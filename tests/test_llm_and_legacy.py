@@ -477,3 +477,45 @@ def test_llm_server_serves_features_from_separate_backends():
                 router.default.calls) == (1, 2, 1)
     finally:
         srv.stop(0)
+
+
+def test_frontend_processes_share_engine_replicas():
+    """llm.server --frontends: two gRPC front-end processes on ONE port (SO_REUSEPORT) over
+    one CPU engine replica; clients on separate connections are spread over both front-ends
+    (the replica counts requests per front-end) and every reply honours the contract."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from drtc_amd.llm.frontends import serve_fleet
+    from drtc_amd.models import TINY_LLAMA
+    from drtc_amd.protos import LLM_SERVICE, llm_pb, make_stub
+    from drtc_amd.utils.cluster import free_port
+
+    port = free_port()
+    cfg = TINY_LLAMA
+    group = serve_fleet("tiny-llama", ["cpu"], dict(max_batch=8, max_model_len=512,
+                                                    use_graphs=False),
+                        2, port, (cfg.vocab_size, cfg.bos_token_id, cfg.eos_token_id), 512,
+                        workers=32, bind="127.0.0.1")
+    try:
+        # one connection per channel (no shared subchannel), so the kernel can balance them
+        stubs = [make_stub(grpc.insecure_channel(
+            f"127.0.0.1:{port}", options=[("grpc.use_local_subchannel_pool", 1)]), LLM_SERVICE)
+            for _ in range(16)]
+        msgs = [llm_pb.Message(sender="a", content="lunch tomorrow?")]
+
+        def one(i):
+            r = stubs[i % len(stubs)].GetSmartReply(
+                llm_pb.SmartReplyRequest(request_id=str(i), recent_messages=msgs), timeout=120)
+            return len(r.suggestions)
+
+        with ThreadPoolExecutor(16) as ex:
+            assert list(ex.map(one, range(48))) == [3] * 48
+        deadline = time.time() + 10
+        while time.time() < deadline:
+            per_fe = group.fleet.health()[0].get("fe_requests", {})
+            if sum(per_fe.values()) >= 48:
+                break
+            time.sleep(0.2)
+        assert sum(per_fe.values()) == 48 and len(per_fe) == 2, per_fe
+    finally:
+        group.stop()
