@@ -363,6 +363,116 @@ DRTC_DEVICE bool w4_splitk(const W4Params& p, f32x4 (&acc)[8][8], int tile, int 
   return true;
 }
 
+// Split-K, parallel combine (pcomb; every workgroup of the grid resident at once - the
+// launcher checks grid <= CUs, one workgroup per CU by its LDS): each slice writes its fp32
+// partial tile ROW-MAJOR [256][256] to its slab with write-through (sc1) stores, every
+// storing wave drains (vmcnt(0)), a workgroup barrier, then ONE lane's agent-scope add to the
+// tile's arrival counter and a bounded sc1 poll until all splitk slices arrived (the
+// MI355X hand-off table's counter row: sc1 stores + drained waves + agent atomic, sc1 loads).
+// Then slice s finishes rows [s 256/splitk, (s+1) 256/splitk) of the tile: 8 consecutive
+// columns per thread, summed over the slabs in slice order (deterministic), and the epilogue
+// (store / residual / gated activation).  The last slice to leave re-arms both counters.
+// Per workgroup 256 KiB written and (splitk x 256/splitk rows) = 256 KiB read, in parallel
+// on every CU - instead of one last arriver reading (splitk - 1) x 256 KiB alone.
+template <int EPI, int V>
+DRTC_DEVICE void w4_splitk_par(const W4Params& p, f32x4 (&acc)[8][8], int tile, int slice,
+                               int tm, int tn, int wm, int wn, int l16, int g) {
+  constexpr int kSc1 = 16;
+  constexpr int kSlab = 256 * 256 * 4;  // one slice's row-major fp32 tile
+  const int sk = p.splitk;
+  const __amdgpu_buffer_rsrc_t slab = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(reinterpret_cast<char*>(p.slab) + (int64_t)tile * sk * kSlab), (short)0,
+      sk * kSlab, 0x00020000);
+  // my partial: row 128 wm + 16 i + 4 g + r, columns 128 wn + 8 l16 + j (j = 0..7)
+  const int mine = slice * kSlab;
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = 128 * wm + 16 * i + 4 * g + r;
+      const int off = mine + (row * 256 + 128 * wn + 8 * l16) * 4;
+      f32x4 lo, hi;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        lo[j] = acc[i][j][r];
+        hi[j] = acc[i][j + 4][r];
+      }
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, lo), slab, off, 0, kSc1);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, hi), slab, off + 16, 0,
+                                             kSc1);
+    }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  int* arrive = p.counters + 2 * tile;
+  int* depart = arrive + 1;
+  if (threadIdx.x == 0) {
+    __hip_atomic_fetch_add(arrive, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int spins = 0;
+    while (__hip_atomic_load(arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < sk) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > (1 << 24)) {  // a slice never arrived: give up (never hang the GPU)
+        __hip_atomic_store(p.counters + 2 * p.tiles_m * p.tiles_n, 1, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+  // my row band: thread t takes column chunk t & 31 (8 columns) of rows band0 + t / 32 + 8 k
+  const int band = 256 / sk, band0 = slice * band;
+  const int t = threadIdx.x, cc = t & 31;
+#pragma unroll 1
+  for (int rr = t >> 5; rr < band; rr += 8) {
+    const int row = band0 + rr;
+    f32x4 lo = (f32x4){0.f, 0.f, 0.f, 0.f}, hi = lo;
+#pragma unroll 1
+    for (int s2 = 0; s2 < sk; ++s2) {
+      const int off = s2 * kSlab + (row * 256 + 8 * cc) * 4;
+      lo += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(slab, off, 0, kSc1));
+      hi += __builtin_bit_cast(f32x4,
+                               __builtin_amdgcn_raw_buffer_load_b128(slab, off + 16, 0, kSc1));
+    }
+    const int m = 256 * tm + row;
+    if (m >= p.M) continue;
+    if constexpr (w4_glu<EPI>()) {
+      // slab columns [8 c, 8 c + 8) of wave column half h = c / 16, lane l = c % 16: gate
+      // columns 64 h + 4 l + (0..3), then the matching up columns
+      const int n = 128 * tn + 64 * (cc >> 4) + 4 * (cc & 15);
+      bf16x4 o;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = f2bf(act_value<w4_act<EPI>()>(lo[j]) * hi[j]);
+      w4_st8<V>(p.c + (int64_t)m * p.ldc + n, o);
+    } else {
+      const int n = 256 * tn + 8 * cc;
+      bf16x8 o;
+      if constexpr (w4_res<EPI>()) {
+        const bf16x8 rv = *reinterpret_cast<const bf16x8*>(p.r + (int64_t)m * p.ldr + n);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          o[j] = f2bf(lo[j] + bf2f(rv[j]));
+          o[j + 4] = f2bf(hi[j] + bf2f(rv[j + 4]));
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          o[j] = f2bf(lo[j]);
+          o[j + 4] = f2bf(hi[j]);
+        }
+      }
+      w4_st16<V>(p.c + (int64_t)m * p.ldc + n, o);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int d = __hip_atomic_fetch_add(depart, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (d == sk - 1) {  // every slice of the tile has read the slabs: re-arm
+      __hip_atomic_store(arrive, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(depart, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
 // Tile coordinates of tile-order index tt (row-grouped: group_m row tiles sweep the columns).
 DRTC_DEVICE void w4_tile_of(const W4Params& p, int tt, int& tm, int& tn) {
   const int gsize = p.group_m * p.tiles_n;
@@ -575,7 +685,10 @@ __global__ __launch_bounds__(kW4Threads, 1) void gemm_w4_kernel(W4Params p) {
   }
   w4_vmcnt<0>();  // no LDS-DMA may still be landing when the workgroup leaves
 
-  if (p.splitk > 1) {
+  if constexpr ((V & 4) != 0) {  // the launcher guarantees splitk > 1: one epilogue site
+    w4_splitk_par<EPI, V>(p, acc, tm * p.tiles_n + tn, slice, tm, tn, wm, wn, l16, g);
+    return;
+  } else if (p.splitk > 1) {
     __syncthreads();
     if (!w4_splitk(p, acc, tm * p.tiles_n + tn, slice, w4_lds)) return;
   }
@@ -591,13 +704,16 @@ int w4_launch_v(const W4Params& p, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
-// schedule variants built: 0 per-tile (split-K capable), 2 the same with temporal stores,
-// 8 persistent, 24 persistent with the per-XCD K rotation
+// schedule variants built: 0 per-tile (split-K capable: last-arriver combine), 2 the same
+// with temporal stores, 4 / 6 per-tile with the parallel split-K combine, 8 persistent, 24
+// persistent with the per-XCD K rotation
 template <int EPI>
 int w4_launch(const W4Params& p, int v, hipStream_t st) {
   switch (v) {
     case 0: return w4_launch_v<EPI, 0>(p, st);
     case 2: return w4_launch_v<EPI, 2>(p, st);
+    case 4: return w4_launch_v<EPI, 4>(p, st);
+    case 6: return w4_launch_v<EPI, 6>(p, st);
     case 8: return w4_launch_v<EPI, 8>(p, st);
     case 24: return w4_launch_v<EPI, 24>(p, st);
     default: return -1;
@@ -611,8 +727,8 @@ int w4_cfg_one() {
 }
 template <int EPI>
 int w4_cfg() {
-  return w4_cfg_one<EPI, 0>() | w4_cfg_one<EPI, 2>() | w4_cfg_one<EPI, 8>() |
-         w4_cfg_one<EPI, 24>();
+  return w4_cfg_one<EPI, 0>() | w4_cfg_one<EPI, 2>() | w4_cfg_one<EPI, 4>() |
+         w4_cfg_one<EPI, 6>() | w4_cfg_one<EPI, 8>() | w4_cfg_one<EPI, 24>();
 }
 
 }  // namespace
@@ -640,6 +756,7 @@ int launch_gemm_w4(void* c, const void* a, const void* b, const void* r, int M, 
   if (glu ? (N % 128 || up_off != N) : (N % 256)) return -1;
   // persistent form (v & 8): one slice, and two K tiles per tile for the cross-tile prefetch
   if ((v & 8) && ((v != 8 && v != 24) || splitk != 1 || K / 64 < 2)) return -1;
+  if ((v & 4) && splitk < 2) return -1;  // the parallel combine is a split-K form
   if (v == 24 && (int64_t)((M + 255) / 256) * (glu ? N / 128 : N / 256) < 8) return -1;
   if (lda % 8 || ldb % 8 || (glu ? ldc % 4 : ldc % 8)) return -1;
   if (res && (ldr % 8 || r == nullptr || (uintptr_t)r % 16)) return -1;
@@ -671,9 +788,12 @@ int launch_gemm_w4(void* c, const void* a, const void* b, const void* r, int M, 
   }
   if (splitk > 1) {
     const int64_t tiles = (int64_t)p.tiles_m * p.tiles_n;
-    if (slab == nullptr || counters == nullptr || n_counters < tiles ||
+    if (slab == nullptr || counters == nullptr || n_counters < 2 * tiles + 1 ||
         slab_bytes < tiles * splitk * 64ll * kW4Threads * 16)
       return -2;
+    // parallel combine: slices wait for each other, so every workgroup must be resident at
+    // once (one per CU: the LDS ring) and a row band per slice (splitk | 256)
+    if ((v & 4) && (256 % splitk || tiles * splitk > w4_num_cus())) return -1;
     p.slab = (float*)slab;
     p.counters = counters;
   }

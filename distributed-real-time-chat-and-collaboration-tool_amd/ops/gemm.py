@@ -407,9 +407,11 @@ def new_gemm_workspace(dev: torch.device) -> tuple[torch.Tensor, torch.Tensor]:
 
 
 def gemm_w4_variant(variant: int) -> bool:
-    """mfma_gemm variants: 7 per-tile (split-K capable), 9 the same with temporal epilogue
-    stores, 15 persistent, 31 persistent with the per-XCD K rotation."""
-    return variant in (7, 9, 15, 31)
+    """mfma_gemm variants: 7 per-tile (split-K with the last-arriver combine), 9 the same
+    with temporal epilogue stores, 11 / 13 per-tile with the parallel split-K combine (every
+    slice finishes a row band of its tile; the grid must fit the CUs), 15 persistent, 31
+    persistent with the per-XCD K rotation."""
+    return variant in (7, 9, 11, 13, 15, 31)
 
 
 def mfma_gemm(x: torch.Tensor, w: torch.Tensor, epi: str = "store",

@@ -185,6 +185,48 @@ def test_w4_splitk_xcd_slice_order(hipk, epi, M, N, K, splitk, gm):
         _check(out, ref)
 
 
+@pytest.mark.parametrize("epi", ["store", "residual", "silu", "gelu_tanh"])
+@pytest.mark.parametrize("M,N,K,splitk,gm", [(256, 8192, 8192, 8, -1), (192, 8192, 4096, 8, 1),
+                                             (1024, 4096, 4096, 4, -4), (300, 1024, 2048, 2, 4),
+                                             (1000, 2048, 1024, 4, -2)])
+def test_w4_splitk_parallel_combine(hipk, epi, M, N, K, splitk, gm):
+    """Split-K with the parallel combine (variants 11 / 13): every slice publishes its fp32
+    tile write-through, waits for the others and finishes a row band of the tile (row tails
+    past M, gated tiles, in-place residual); counters re-arm, so repeated calls and a
+    hipGraph replay stay exact."""
+    g = torch.Generator(device="cuda").manual_seed(M + N + K + splitk)
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16, generator=g)
+    w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16, generator=g) * 0.05
+    nout = N // 2 if epi in ("silu", "gelu_tanh") else N
+    res = torch.randn(M, nout, device="cuda", dtype=torch.bfloat16, generator=g) if epi == "residual" else None
+    ref = _ref(x, w, epi, res)
+    for v in (11, 13):
+        r_in = res.clone() if res is not None else None
+        out = G.mfma_gemm(x, w, epi, residual=r_in, out=r_in, variant=v, splitk=splitk,
+                          group_m=gm)
+        torch.cuda.synchronize()
+        _check(out, ref)
+    if epi == "store":
+        out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+        gr = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(gr):
+            G.mfma_gemm(x, w, out=out, variant=11, splitk=splitk, group_m=gm)
+        for _ in range(3):
+            out.zero_()
+            gr.replay()
+            torch.cuda.synchronize()
+            _check(out, ref)
+
+
+def test_w4_splitk_parallel_combine_rejects(hipk):
+    x = torch.randn(1024, 4096, device="cuda", dtype=torch.bfloat16)
+    w = torch.randn(8192, 4096, device="cuda", dtype=torch.bfloat16)
+    with pytest.raises(RuntimeError):
+        G.mfma_gemm(x, w, variant=11, splitk=1)  # a split-K form
+    with pytest.raises(RuntimeError):
+        G.mfma_gemm(x, w, variant=11, splitk=8)  # 128 tiles x 8 > the CUs: not co-resident
+
+
 # ------------------------------------------------------ gemm_w4 persistent forms (15 / 31)
 @pytest.mark.parametrize("variant", [15, 31])
 @pytest.mark.parametrize("epi", ["store", "residual", "silu", "gelu_tanh"])
@@ -231,7 +273,7 @@ def test_router_covers_every_served_decode_shape(hipk):
     to the LLM server's default batch, the default batch itself and off-bucket batches,
     resolves to a hand kernel, a tuned library solution, or - at a bucket the tuner measured
     it fastest - the library's heuristic pick; an off-bucket M takes its bucket-above route
-    (never an unmeasured path), and prefill-sized M (>= W4_MIN_M) never falls to torch."""
+    (never an unmeasured path), and every prefill shape the hand GEMM covers takes it."""
     from drtc_amd.llm.server import default_max_batch
     from drtc_amd.models import get_config
 
@@ -252,12 +294,13 @@ def test_router_covers_every_served_decode_shape(hipk):
                     continue  # the fused-GLU hand GEMM (norm_glu), not linear
                 kind, arg = G.route(M, N, K, K)
                 assert kind in ("w4", "lt", "skinny", "midm", "torch"), (name, proj, M, kind)
-                if M >= G.W4_MIN_M:
-                    assert kind in ("w4", "lt"), (name, proj, M, kind)
-                elif M not in G.DECODE_BUCKETS:
+                if G.w4_shape_ok(M, N, K):
+                    assert kind == "w4", (name, proj, M, kind)
+                elif M <= G.DECODE_MAX_M and M not in G.DECODE_BUCKETS:
                     Mb = next(b for b in G.DECODE_BUCKETS if b >= M)
                     kb = G.route(Mb, N, K, K)
-                    assert kind == kb[0] or (kb[0] == "skinny" and kind == "torch"), \
+                    # the bucket's kernel, or the heuristic where its solution rejects this M
+                    assert kind == kb[0] or (kind == "torch" and kb[0] in ("lt", "skinny")), \
                         (name, proj, M, kind, Mb, kb)
                 ent = G._activate().get((M, N, K, K))
                 if ent is not None and (ent[0] >= 0 or ent[1] or ent[2]):
