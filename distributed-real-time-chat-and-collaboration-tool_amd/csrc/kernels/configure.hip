@@ -9,6 +9,8 @@ int configure_kernels() {
   if (e) return e;
   e = configure_moe();
   if (e) return e;
-  return configure_gemm_w4();
+  e = configure_gemm_w4();
+  if (e) return e;
+  return configure_gemm_xd();
 }
 }  // namespace drtc

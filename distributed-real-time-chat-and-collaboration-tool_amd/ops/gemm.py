@@ -9,6 +9,8 @@ shape (M, N, K, row stride of x) ONCE to a route, cached per shape (``route``):
   "skinny"  gemv.hip weight-streaming kernels (M <= 16)     decode buckets where the table (or
                                                             ``skinny_variant`` untuned) says so
   "midm"    gemm_midm.hip medium-M kernel (M <= 256)        decode buckets where the table says so
+  "xd"      gemm_xd.hip: 128-row tiles, full K, tile order  decode buckets where the table says so
+            partitioned by XCD (``xd_gemm``)                (full-batch qkv / o / down)
   "lt"      hipBLASLt with the per-shape measured solution  the other decode buckets, and
             (``csrc/kernels/gemm_lt.cpp``)                  prefill shapes the hand GEMM does not
                                                             take (tuned at the nearest M)
@@ -42,8 +44,9 @@ from ._ext import check, hipk, on_gpu, ptr, stream_ptr
 TUNED_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuned")
 _lock = threading.Lock()
 # (M, N, K, ldx) -> (hipBLASLt solution index or -1, skinny-kernel variant or 0,
-#                   medium-M kernel K splits or 0): the decode buckets of the tuning table
-_table: dict[tuple[int, int, int, int], tuple[int, int, int]] | None = None
+#                   medium-M kernel K splits or 0, gemm_xd tile width nf or 0): the decode
+#                   buckets of the tuning table
+_table: dict[tuple[int, int, int, int], tuple[int, int, int, int]] | None = None
 # (N, K, ldx) -> sorted [(tuned M, algo, beats F.linear, beats addmm_)]: prefill entries
 _prefill: dict[tuple[int, int, int], list[tuple[int, int, bool, bool]]] = {}
 # (M, N, K, ldx, beta) -> algo chosen for a prefill-sized call (-1: torch's path)
@@ -57,6 +60,7 @@ DECODE_BUCKETS = (1, 2, 4, 8, 16, 24, 32, 48, 64, 96, 128, 160, 192, 224, 256, 3
 _enabled = os.environ.get("DRTC_TUNED_GEMM", "1") != "0"
 _prefill_enabled = os.environ.get("DRTC_PREFILL_TUNED", "1") != "0"
 _midm_enabled = os.environ.get("DRTC_MIDM_GEMM", "1") != "0"
+_xd_enabled = os.environ.get("DRTC_XD_GEMM", "1") != "0"
 # decode batches up to this many rows may take the skinny kernel: the table's choice where
 # the shape was measured, skinny_variant()'s default otherwise; 0 disables it
 SKINNY_MAX_M = int(os.environ.get("DRTC_SKINNY_MAX_M", "16"))
@@ -85,7 +89,7 @@ def _activate() -> dict:
     with _lock:
         if _table is not None:
             return _table
-        tab: dict[tuple[int, int, int, int], tuple[int, int, int]] = {}
+        tab: dict[tuple[int, int, int, int], tuple[int, int, int, int]] = {}
         pre: dict[tuple[int, int, int], list[tuple[int, int, bool, bool]]] = {}
         if _enabled and torch.cuda.is_available():
             ver = str(hipk().lt_version())
@@ -97,7 +101,8 @@ def _activate() -> dict:
                             (M, int(e["algo"]), bool(e.get("beta0")), bool(e.get("beta1"))))
                     continue
                 tab[(M, N, K, ldx)] = (int(e.get("algo", -1)), int(e.get("skinny", 0)),
-                                       int(e.get("midm", 0)) if _midm_enabled else 0)
+                                       int(e.get("midm", 0)) if _midm_enabled else 0,
+                                       int(e.get("xd", 0)) if _xd_enabled else 0)
         for v in pre.values():
             v.sort()
         _prefill.clear()
@@ -123,7 +128,8 @@ def set_enabled(on: bool) -> None:
 
 
 # ------------------------------------------------------------------ routing
-def _decode_entry(M: int, N: int, K: int, ldx: int) -> tuple[int, tuple[int, int, int]] | None:
+def _decode_entry(M: int, N: int, K: int,
+                  ldx: int) -> tuple[int, tuple[int, int, int, int]] | None:
     """(tuned bucket, entry) for a decode-sized shape, None for torch's (hipBLASLt heuristic)
     path.  The tuner measured every (model shape, DECODE_BUCKETS M) and kept an entry only
     where something beat the heuristic pick, so a bucket without an entry means "the
@@ -180,9 +186,11 @@ def _resolve(M: int, N: int, K: int, ldx: int) -> tuple[str, int]:
     if found is None:
         v = skinny_variant(M, N, K, ldx)
         return ("skinny", v) if v else ("torch", 0)
-    _, (algo, sk, midm) = found
+    _, (algo, sk, midm, xd) = found
     if sk and M <= SKINNY_MAX_M and skinny_supports(sk, M, N, K, ldx):
         return ("skinny", sk)
+    if xd and xd_supported(M, N, K, xd):
+        return ("xd", xd)
     if midm and midm_supported(M, N, K):
         return ("midm", midm)
     if algo >= 0:
@@ -231,6 +239,8 @@ def linear(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
         return skinny_linear(x, w, arg)
     if kind == "midm":
         return midm_gemm(x, w, "store", splits=arg)
+    if kind == "xd" and _aligned(x, w):
+        return xd_gemm(x, w, nf=arg)
     return F.linear(x, w)
 
 
@@ -560,6 +570,62 @@ def norm_glu(p, w: torch.Tensor, act: str = "silu") -> torch.Tensor:
     return act_glu(norm_linear(p, w), act)
 
 
+# ------------------------------------------------------------------ XCD-partitioned decode GEMM
+XD_EPI = {"store": 0, "residual": 1}
+XD_NF = (2, 4, 6)
+
+
+XD_FORMS = {2: (4, 6), 4: (4, 5), 6: (3, 4)}  # nf -> LDS ring depths built (first = default)
+
+
+def xd_stages(nf: int) -> int:
+    return XD_FORMS[nf][0]
+
+
+def xd_supported(M: int, N: int, K: int, nf: int, stages: int = 0) -> bool:
+    """Shapes gemm_xd.hip takes with 128 x 32 nf tiles (full K, one workgroup per tile)."""
+    if nf not in XD_FORMS or (stages and stages not in XD_FORMS[nf]):
+        return False
+    return (M >= 1 and N % (32 * nf) == 0 and K % 64 == 0
+            and K // 64 > (stages or xd_stages(nf)))
+
+
+def xd_nf(M: int, N: int, K: int) -> int:
+    """Tile width of an untuned shape: the widest nf whose tile count fills whole rounds of
+    the 256 CUs best (o / down at M = 1024: nf 4 -> 256 tiles; qkv N = 6144: nf 6 -> 256)."""
+    best, best_eff = 0, 0.0
+    tm = -(-M // 128)
+    for nf in (6, 4, 2):
+        if not xd_supported(M, N, K, nf):
+            continue
+        t = tm * (N // (32 * nf))
+        eff = t / (-(-t // 256) * 256)
+        if eff > best_eff + 1e-9:
+            best, best_eff = nf, eff
+    return best
+
+
+def xd_gemm(x: torch.Tensor, w: torch.Tensor, epi: str = "store",
+            residual: torch.Tensor | None = None, out: torch.Tensor | None = None,
+            nf: int = 0, stages: int = 0) -> torch.Tensor:
+    """Decode-shaped hand GEMM, csrc/kernels/gemm_xd.hip: y = x @ w.T (+ residual; ``out``
+    may be ``residual``) on 128 x 32 nf tiles, full K, with the tile order partitioned by XCD
+    (each XCD streams its own weight column panels through its L2 for every row tile)."""
+    M, K = x.shape
+    N = w.shape[0]
+    nf = nf or xd_nf(M, N, K)
+    assert xd_supported(M, N, K, nf, stages), (M, N, K, nf, stages)
+    assert x.dtype == w.dtype == torch.bfloat16 and x.stride(1) == 1 and w.is_contiguous()
+    if out is None:
+        out = residual if (epi == "residual" and residual is not None) else \
+            torch.empty((M, N), dtype=x.dtype, device=x.device)
+    check(hipk().gemm_xd(out.data_ptr(), x.data_ptr(), w.data_ptr(), ptr(residual), M, N, K,
+                         x.stride(0), w.stride(0), out.stride(0),
+                         residual.stride(0) if residual is not None else 0, XD_EPI[epi], nf,
+                         stages, stream_ptr(x)), "gemm_xd")
+    return out
+
+
 # ------------------------------------------------------------------ medium-M decode GEMM
 MIDM_EPI = {"store": 0, "residual": 1, "silu": 2, "gelu_tanh": 3}  # gemm_midm.hip accepts 0-3
 MIDM_MAX_M = 256
@@ -626,4 +692,4 @@ __all__ = ["linear", "route", "norm_linear", "glu_linear", "norm_glu", "linear_r
            "residual_fusable", "w4_glu_ok", "w4_ok", "w4_shape_ok", "w4_group_m", "mfma_gemm",
            "gemm_workspace", "new_gemm_workspace", "skinny_linear", "skinny_ok",
            "skinny_variant", "skinny_supports", "midm_gemm", "midm_supported", "midm_splits",
-           "tune", "save_entries", "load_table", "reset", "set_enabled", "table_path"]
+           "xd_gemm", "xd_supported", "xd_nf", "tune", "save_entries", "load_table", "reset", "set_enabled", "table_path"]

@@ -293,7 +293,7 @@ def test_router_covers_every_served_decode_shape(hipk):
                 if proj == "gate_up" and M >= G.W4_GLU_MIN_M:
                     continue  # the fused-GLU hand GEMM (norm_glu), not linear
                 kind, arg = G.route(M, N, K, K)
-                assert kind in ("w4", "lt", "skinny", "midm", "torch"), (name, proj, M, kind)
+                assert kind in ("w4", "lt", "skinny", "midm", "xd", "torch"), (name, proj, M, kind)
                 if G.w4_shape_ok(M, N, K):
                     assert kind == "w4", (name, proj, M, kind)
                 elif M <= G.DECODE_MAX_M and M not in G.DECODE_BUCKETS:
@@ -303,7 +303,7 @@ def test_router_covers_every_served_decode_shape(hipk):
                     assert kind == kb[0] or (kind == "torch" and kb[0] in ("lt", "skinny")), \
                         (name, proj, M, kind, Mb, kb)
                 ent = G._activate().get((M, N, K, K))
-                if ent is not None and (ent[0] >= 0 or ent[1] or ent[2]):
+                if ent is not None and (ent[0] >= 0 or ent[1] or ent[2] or ent[3]):
                     assert kind != "torch", (name, proj, M, ent)  # a measured winner is used
 
 
@@ -315,3 +315,71 @@ def test_linear_off_bucket_matches_fp32(hipk):
         x = torch.randn(M, K, device="cuda", generator=g).to(torch.bfloat16)
         w = (torch.randn(N, K, device="cuda", generator=g) * 0.02).to(torch.bfloat16)
         assert _rel(G.linear(x, w), x.float() @ w.float().t()) < 1e-2, (M, N, K)
+
+
+# ---------------------------------------------------------------- gemm_xd.hip (decode tiles)
+@pytest.mark.parametrize("epi", ["store", "residual"])
+@pytest.mark.parametrize("nf,stages", [(2, 4), (2, 6), (4, 4), (4, 5), (6, 3), (6, 4)])
+@pytest.mark.parametrize("M,N,K", [(1024, 768, 4096), (1000, 1536, 448), (77, 384, 1024),
+                                   (512, 3072, 1472), (129, 1152, 2048)])
+def test_xd_gemm_matches_fp32(hipk, epi, nf, stages, M, N, K):
+    if not G.xd_supported(M, N, K, nf, stages):
+        pytest.skip("shape outside the nf tile grid")
+    g = torch.Generator(device="cuda").manual_seed(M * 7 + N + K + nf)
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16, generator=g)
+    w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16, generator=g) * 0.05
+    res = torch.randn(M, N, device="cuda", dtype=torch.bfloat16, generator=g) \
+        if epi == "residual" else None
+    ref = _ref(x, w, epi, res)
+    out = G.xd_gemm(x, w, epi, residual=res, nf=nf, stages=stages)
+    torch.cuda.synchronize()
+    _check(out, ref)
+
+
+def test_xd_gemm_strided_input_in_place_residual_and_graph(hipk):
+    M, N, K = 640, 4096, 2048
+    g = torch.Generator(device="cuda").manual_seed(5)
+    big = torch.randn(M, K + 192, device="cuda", dtype=torch.bfloat16, generator=g)
+    x = big[:, 64:64 + K]  # row stride K + 192
+    w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16, generator=g) * 0.05
+    res = torch.randn(M, N, device="cuda", dtype=torch.bfloat16, generator=g)
+    ref = _ref(x, w, "residual", res)
+    r = res.clone()
+    G.xd_gemm(x, w, "residual", residual=r, out=r)  # in place into the residual stream
+    torch.cuda.synchronize()
+    _check(r, ref)
+    out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        G.xd_gemm(x, w, out=out)
+        gr = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(gr, stream=s):
+            G.xd_gemm(x, w, out=out)
+    for _ in range(3):
+        out.zero_()
+        gr.replay()
+    torch.cuda.synchronize()
+    _check(out, _ref(x, w, "store", None))
+
+
+def test_xd_gemm_rejects_bad_shapes(hipk):
+    x = torch.randn(64, 512, device="cuda", dtype=torch.bfloat16)
+    w = torch.randn(200, 512, device="cuda", dtype=torch.bfloat16)  # N % 64 != 0
+    y = torch.empty(64, 200, device="cuda", dtype=torch.bfloat16)
+    for nf in (2, 4, 6, 3):
+        assert hipk.gemm_xd(y.data_ptr(), x.data_ptr(), w.data_ptr(), 0, 64, 200, 512, 512, 512,
+                            200, 0, 0, nf, 0, 0) == -1
+    # a ring depth that is not built
+    assert hipk.gemm_xd(y.data_ptr(), x.data_ptr(), w.data_ptr(), 0, 64, 256, 512, 512, 512,
+                        256, 0, 0, 4, 7, 0) == -1
+    w2 = torch.randn(256, 256, device="cuda", dtype=torch.bfloat16)
+    x2 = torch.randn(64, 256, device="cuda", dtype=torch.bfloat16)
+    y2 = torch.empty(64, 256, device="cuda", dtype=torch.bfloat16)
+    # K / 64 must exceed the stage count (4 at nf 4)
+    assert hipk.gemm_xd(y2.data_ptr(), x2.data_ptr(), w2.data_ptr(), 0, 64, 256, 256, 256, 256,
+                        256, 0, 0, 4, 0, 0) == -1
+    # residual epilogue without a residual
+    x3 = torch.randn(64, 512, device="cuda", dtype=torch.bfloat16)
+    w3 = torch.randn(256, 512, device="cuda", dtype=torch.bfloat16)
+    assert hipk.gemm_xd(y2.data_ptr(), x3.data_ptr(), w3.data_ptr(), 0, 64, 256, 512, 512, 512,
+                        256, 0, 1, 2, 0, 0) == -1
