@@ -757,7 +757,8 @@ int launch_gemm_w4(void* c, const void* a, const void* b, const void* r, int M, 
   // persistent form (v & 8): one slice, and two K tiles per tile for the cross-tile prefetch
   if ((v & 8) && ((v != 8 && v != 24) || splitk != 1 || K / 64 < 2)) return -1;
   if ((v & 4) && splitk < 2) return -1;  // the parallel combine is a split-K form
-  if (v == 24 && (int64_t)((M + 255) / 256) * (glu ? N / 128 : N / 256) < 8) return -1;
+  // the per-XCD K rotation needs whole XCD rounds of workgroups: below 8 tiles, plain persistent
+  if (v == 24 && (int64_t)((M + 255) / 256) * (glu ? N / 128 : N / 256) < 8) v = 8;
   if (lda % 8 || ldb % 8 || (glu ? ldc % 4 : ldc % 8)) return -1;
   if (res && (ldr % 8 || r == nullptr || (uintptr_t)r % 16)) return -1;
   if ((uintptr_t)a % 16 || (uintptr_t)b % 16 || (uintptr_t)c % (glu ? 8 : 16)) return -1;

@@ -738,9 +738,16 @@ class EngineLoop:
     """Background thread that drives an engine; used by the LLM gRPC service
     so concurrent RPCs are batched together (continuous batching)."""
 
-    def __init__(self, engine: LLMEngine, idle_sleep: float = 0.0005):
+    def __init__(self, engine: LLMEngine, idle_sleep: float = 0.0005,
+                 burst_gap_s: float | None = None, burst_max_s: float = 0.05):
         self.engine = engine
         self.idle_sleep = idle_sleep
+        # burst gathering (off unless burst_gap_s > 0; DRTC_BURST_GAP_MS): see _hold
+        if burst_gap_s is None:
+            burst_gap_s = float(os.environ.get("DRTC_BURST_GAP_MS", "0")) / 1000.0
+        self.burst_gap_s, self.burst_max_s = burst_gap_s, burst_max_s
+        self._last_submit = 0.0
+        self._hold_start: float | None = None
         self._stop = threading.Event()
         self._wake = threading.Event()
         self.thread = threading.Thread(target=self._loop, name="llm-engine", daemon=True)
@@ -752,8 +759,27 @@ class EngineLoop:
 
     def submit(self, req: Request) -> Request:
         self.engine.add_request(req)
+        self._last_submit = time.perf_counter()
         self._wake.set()
         return req
+
+    def _hold(self) -> bool:
+        """Burst gathering for closed-loop clients: while requests are still streaming in (the
+        last one arrived less than ``burst_gap_s`` ago), the queue holds less than one prefill
+        chunk and no large batch is decoding, let the burst gather instead of running a small
+        prefill and then small decode steps for its first requests - at most ``burst_max_s``
+        per burst.  A lone request waits at most ``burst_gap_s``."""
+        if self.burst_gap_s <= 0:
+            return False
+        e = self.engine
+        now = time.perf_counter()
+        if (not e.waiting or e._waiting_tokens >= e.prefill_chunk_tokens
+                or len(e.running) > e.max_batch // 4 or now - self._last_submit >= self.burst_gap_s):
+            self._hold_start = None
+            return False
+        if self._hold_start is None:
+            self._hold_start = now
+        return now - self._hold_start < self.burst_max_s
 
     def alive(self) -> bool:
         return self.thread.is_alive() and self.error is None
@@ -762,6 +788,12 @@ class EngineLoop:
         try:
             while not self._stop.is_set():
                 if self.engine.has_work():
+                    if self._hold():
+                        t0 = time.perf_counter()
+                        self._wake.wait(self.burst_gap_s)
+                        self._wake.clear()
+                        self.engine.stats["burst_hold_us"] += int(1e6 * (time.perf_counter() - t0))
+                        continue
                     self.engine.step()
                 else:
                     # idle time (no request anywhere in the engine), reported in the

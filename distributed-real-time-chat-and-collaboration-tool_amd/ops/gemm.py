@@ -44,8 +44,8 @@ from ._ext import check, hipk, on_gpu, ptr, stream_ptr
 TUNED_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuned")
 _lock = threading.Lock()
 # (M, N, K, ldx) -> (hipBLASLt solution index or -1, skinny-kernel variant or 0,
-#                   medium-M kernel K splits or 0, gemm_xd tile width nf or 0): the decode
-#                   buckets of the tuning table
+#                   medium-M kernel K splits or 0, gemm_xd form or 0): the decode buckets of
+#                   the tuning table
 _table: dict[tuple[int, int, int, int], tuple[int, int, int, int]] | None = None
 # (N, K, ldx) -> sorted [(tuned M, algo, beats F.linear, beats addmm_)]: prefill entries
 _prefill: dict[tuple[int, int, int], list[tuple[int, int, bool, bool]]] = {}
@@ -240,7 +240,7 @@ def linear(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     if kind == "midm":
         return midm_gemm(x, w, "store", splits=arg)
     if kind == "xd" and _aligned(x, w):
-        return xd_gemm(x, w, nf=arg)
+        return xd_gemm(x, w, form=arg)
     return F.linear(x, w)
 
 
@@ -493,8 +493,13 @@ def save_entries(entries: dict[str, dict], path: str | None = None) -> str:
 # per-tile form in one process (profiles/r3r/probe.log): prefill qkv +0.5 %, o +2.0 %,
 # gate_up+GLU +0.9 %, a 4400-row chunk's gate_up+GLU +2.3 %, decode gate_up+GLU at M = 1024
 # +4.0 %.  DRTC_W4_PERSIST=0 restores the per-tile form (variant 7).
+# Variant 31 (the default since round 4) adds the per-XCD K rotation: each XCD label starts its
+# K loop at its own eighth of K, so the eight XCDs' epilogue store bursts do not coincide.
+# Same box, interleaved (profiles/r4d/seam.log): decode gate_up + GLU at M = 1024 207.4 vs
+# 231.1 us (v15), prefill shapes within +-1 % (K = 14336 1.2 % faster).  Fewer than 8 tiles
+# run the plain persistent form.
 W4_PERSIST = os.environ.get("DRTC_W4_PERSIST", "1") == "1"
-W4_PERSIST_VARIANT = int(os.environ.get("DRTC_W4_VARIANT", "15"))
+W4_PERSIST_VARIANT = int(os.environ.get("DRTC_W4_VARIANT", "31"))
 
 
 def _w4v(K: int) -> int:
@@ -572,57 +577,65 @@ def norm_glu(p, w: torch.Tensor, act: str = "silu") -> torch.Tensor:
 
 # ------------------------------------------------------------------ XCD-partitioned decode GEMM
 XD_EPI = {"store": 0, "residual": 1}
-XD_NF = (2, 4, 6)
+# forms built in gemm_xd.hip, as mt * 100 + nf * 10 + splitk (128 mt x 32 nf tiles, K split
+# over splitk slices) -> LDS ring depth
+XD_FORMS = {121: 4, 141: 4, 161: 3, 241: 3, 261: 2, 242: 3, 262: 2}
 
 
-XD_FORMS = {2: (4, 6), 4: (4, 5), 6: (3, 4)}  # nf -> LDS ring depths built (first = default)
+def xd_form(form: int) -> tuple[int, int, int]:
+    return form // 100, form // 10 % 10, form % 10
 
 
-def xd_stages(nf: int) -> int:
-    return XD_FORMS[nf][0]
-
-
-def xd_supported(M: int, N: int, K: int, nf: int, stages: int = 0) -> bool:
-    """Shapes gemm_xd.hip takes with 128 x 32 nf tiles (full K, one workgroup per tile)."""
-    if nf not in XD_FORMS or (stages and stages not in XD_FORMS[nf]):
+def xd_supported(M: int, N: int, K: int, form: int) -> bool:
+    """Shapes gemm_xd.hip takes in ``form`` (mt * 100 + nf * 10 + splitk)."""
+    if form not in XD_FORMS:
         return False
-    return (M >= 1 and N % (32 * nf) == 0 and K % 64 == 0
-            and K // 64 > (stages or xd_stages(nf)))
+    mt, nf, sk = xd_form(form)
+    return (M >= 1 and N % (32 * nf) == 0 and K % (64 * sk) == 0
+            and K // 64 // sk > XD_FORMS[form])
 
 
-def xd_nf(M: int, N: int, K: int) -> int:
-    """Tile width of an untuned shape: the widest nf whose tile count fills whole rounds of
-    the 256 CUs best (o / down at M = 1024: nf 4 -> 256 tiles; qkv N = 6144: nf 6 -> 256)."""
-    best, best_eff = 0, 0.0
-    tm = -(-M // 128)
-    for nf in (6, 4, 2):
-        if not xd_supported(M, N, K, nf):
+def xd_default_form(M: int, N: int, K: int) -> int:
+    """Form of an untuned shape: the fewest operand bytes per CU among the forms whose work
+    items fill whole rounds of the 256 CUs best (o / down at M = 1024: 256-row tiles with
+    split-K 2; qkv N = 6144: 256 x 192 with split-K 2)."""
+    best, key = 0, None
+    for form in XD_FORMS:
+        if not xd_supported(M, N, K, form):
             continue
-        t = tm * (N // (32 * nf))
-        eff = t / (-(-t // 256) * 256)
-        if eff > best_eff + 1e-9:
-            best, best_eff = nf, eff
+        mt, nf, sk = xd_form(form)
+        items = -(-M // (128 * mt)) * (N // (32 * nf)) * sk
+        fill = items / (-(-items // 256) * 256)
+        rounds = -(-items // 256)
+        per_cu = rounds * (128 * mt + 32 * nf) * (K // sk)  # operand elements per CU
+        k = (round(fill, 3), -per_cu)
+        if key is None or k > key:
+            best, key = form, k
     return best
 
 
 def xd_gemm(x: torch.Tensor, w: torch.Tensor, epi: str = "store",
             residual: torch.Tensor | None = None, out: torch.Tensor | None = None,
-            nf: int = 0, stages: int = 0) -> torch.Tensor:
+            form: int = 0, ws: tuple[torch.Tensor, torch.Tensor] | None = None) -> torch.Tensor:
     """Decode-shaped hand GEMM, csrc/kernels/gemm_xd.hip: y = x @ w.T (+ residual; ``out``
-    may be ``residual``) on 128 x 32 nf tiles, full K, with the tile order partitioned by XCD
-    (each XCD streams its own weight column panels through its L2 for every row tile)."""
+    may be ``residual``) on 128 mt x 32 nf tiles, K split over 1 or 2 slices, with the tile
+    order partitioned by XCD (each XCD streams its own weight column panels through its L2
+    for every row tile).  ``form`` = mt * 100 + nf * 10 + splitk (0: ``xd_default_form``)."""
     M, K = x.shape
     N = w.shape[0]
-    nf = nf or xd_nf(M, N, K)
-    assert xd_supported(M, N, K, nf, stages), (M, N, K, nf, stages)
+    form = form or xd_default_form(M, N, K)
+    assert xd_supported(M, N, K, form), (M, N, K, form)
     assert x.dtype == w.dtype == torch.bfloat16 and x.stride(1) == 1 and w.is_contiguous()
+    mt, nf, sk = xd_form(form)
     if out is None:
         out = residual if (epi == "residual" and residual is not None) else \
             torch.empty((M, N), dtype=x.dtype, device=x.device)
+    slab, cnt = ((ws or gemm_workspace(x.device)) if sk > 1 else (None, None))
     check(hipk().gemm_xd(out.data_ptr(), x.data_ptr(), w.data_ptr(), ptr(residual), M, N, K,
                          x.stride(0), w.stride(0), out.stride(0),
-                         residual.stride(0) if residual is not None else 0, XD_EPI[epi], nf,
-                         stages, stream_ptr(x)), "gemm_xd")
+                         residual.stride(0) if residual is not None else 0, XD_EPI[epi], mt, nf,
+                         sk, ptr(slab), slab.numel() * 4 if slab is not None else 0, ptr(cnt),
+                         cnt.numel() if cnt is not None else 0, stream_ptr(x)), "gemm_xd")
     return out
 
 
@@ -692,4 +705,4 @@ __all__ = ["linear", "route", "norm_linear", "glu_linear", "norm_glu", "linear_r
            "residual_fusable", "w4_glu_ok", "w4_ok", "w4_shape_ok", "w4_group_m", "mfma_gemm",
            "gemm_workspace", "new_gemm_workspace", "skinny_linear", "skinny_ok",
            "skinny_variant", "skinny_supports", "midm_gemm", "midm_supported", "midm_splits",
-           "xd_gemm", "xd_supported", "xd_nf", "tune", "save_entries", "load_table", "reset", "set_enabled", "table_path"]
+           "xd_gemm", "xd_supported", "xd_default_form", "tune", "save_entries", "load_table", "reset", "set_enabled", "table_path"]

@@ -1,33 +1,16 @@
-#!/usr/bin/env python3
-"""Average rocprofv3 PMC counters per kernel (short names) over every pass directory given."""
-import csv
-import glob
-import sys
-from collections import defaultdict
-
-
+import csv, sys, collections, re
 def short(n):
-    if "gemm_w4" in n:
-        return "w4"
-    if "gemm256" in n:
-        return "gemm256"
-    if n.startswith("Custom_Cijk") or n.startswith("Cijk"):
-        return "hipblaslt:" + ("MT" + n.split("_MT")[1].split("_")[0] if "_MT" in n else n[:30])
-    return n[:40]
-
-
-def main():
-    acc = defaultdict(lambda: defaultdict(list))
-    for d in sys.argv[1:]:
-        for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
-            for r in csv.DictReader(open(f)):
-                k = short(r.get("Kernel_Name", ""))
-                acc[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
-    for k, cs in acc.items():
-        print(f"== {k}")
-        for c, vs in sorted(cs.items()):
-            print(f"   {c:28s} {sum(vs) / len(vs):16.4g}  (n={len(vs)})")
-
-
-if __name__ == "__main__":
-    main()
+    if 'gemm_xd' in n:
+        m=re.search(r'XdCfg<(\d), (\d), (\d), (\d)>', n); return 'xd%s%s%s'%(m.group(1),m.group(2),m.group(4))
+    if 'gemm_w4' in n: return 'w4'
+    if 'Cijk' in n: return 'lib:'+n[:40]
+    return n[:30]
+agg=collections.defaultdict(lambda: collections.defaultdict(float)); cnt=collections.Counter()
+for d in sys.argv[1:]:
+    for r in csv.DictReader(open(d)):
+        k=short(r['Kernel_Name'])
+        agg[k][r['Counter_Name']]+=float(r['Counter_Value'])
+        cnt[(k,r['Counter_Name'])]+=1
+for k,v in agg.items():
+    n=max(c for (kk,_),c in cnt.items() if kk==k)
+    print(k, 'dispatches', n, {c: round(x/cnt[(k,c)],1) for c,x in v.items()})

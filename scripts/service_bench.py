@@ -175,7 +175,7 @@ def _delta(before, pool):
     time.sleep(2 * pool.hb_interval)
     out = []
     for b, a in zip(before, pool.health()):
-        out.append({k: a[k] - b.get(k, 0) for k in ("idle_ms", "prefill_steps", "prefill_tokens",
+        out.append({k: a[k] - b.get(k, 0) for k in ("idle_ms", "burst_hold_us", "prefill_steps", "prefill_tokens",
                                                    "decode_steps", "mixed_steps", "decode_tokens")
                     if isinstance(a.get(k), int)})
     return out

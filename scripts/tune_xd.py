@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Measure the XCD-partitioned decode GEMM (csrc/kernels/gemm_xd.hip) against the engine's
 path without it (ops.linear: tuned hipBLASLt / midm / F.linear) for every decode projection
-of a model at the larger decode buckets, and write a tuning entry {"xd": nf} where the hand
+of a model at the larger decode buckets, and write a tuning entry {"xd": form} where the hand
 kernel wins by at least --min-gain.
 
 W is rotated over copies (>= 512 MB in all) so it streams from HBM, as in a decode step;
@@ -54,28 +54,28 @@ def main() -> None:
             ws = [(torch.randn(N, K, device=dev, generator=g) * 0.02).to(torch.bfloat16)
                   for _ in range(ncopy)]
             for M in (int(m) for m in a.ms.split(",")):
-                nfs = [nf for nf in G.XD_FORMS if G.xd_supported(M, N, K, nf)]
-                if not nfs:
+                forms = [f for f in G.XD_FORMS if G.xd_supported(M, N, K, f)]
+                if not forms:
                     continue
                 x = torch.randn(M, K, device=dev, generator=g).to(torch.bfloat16)
                 base = time_arm(lambda w: G.linear(x, w), ws)
                 kind = G.route(M, N, K, K)[0]
                 ref = x.float() @ ws[0].float().t()
                 best = None
-                for nf in nfs:
-                    y = G.xd_gemm(x, ws[0], nf=nf)
+                for nf in forms:
+                    y = G.xd_gemm(x, ws[0], form=nf)
                     err = ((y.float() - ref).abs().max() / ref.abs().max()).item()
                     if err > 2e-2:
                         print(json.dumps({"model": model, "tp": tp, "gemm": name, "M": M,
-                                          "nf": nf, "err": err, "FAILED": True}), flush=True)
+                                          "form": nf, "err": err, "FAILED": True}), flush=True)
                         continue
-                    us = time_arm(lambda w, nf=nf: G.xd_gemm(x, w, nf=nf), ws)
+                    us = time_arm(lambda w, nf=nf: G.xd_gemm(x, w, form=nf), ws)
                     if best is None or us < best[1]:
                         best = (nf, us)
                 rec = {"model": model, "tp": int(tp), "gemm": name, "M": M, "N": N, "K": K,
                        "base": kind, "base_us": round(base, 1)}
                 if best is not None:
-                    rec.update(xd_nf=best[0], xd_us=round(best[1], 1),
+                    rec.update(xd_form=best[0], xd_us=round(best[1], 1),
                                gain=round(base / best[1] - 1, 3))
                     if best[1] < base * (1 - a.min_gain):
                         out[ver][f"{M},{N},{K},{K}"] = {

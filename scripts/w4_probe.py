@@ -57,14 +57,13 @@ def main():
                 fns[arm] = lambda: ops.act_glu(ops.linear(x, nxt()), a.epi)
             else:
                 fns[arm] = lambda: ops.linear(x, nxt())
-        elif arm[0] == "x":  # "xNF[:S]": gemm_xd, 128 x 32 NF tiles, S-deep LDS ring
-            f = arm[1:].split(":")
-            nf, st = int(f[0] or 0), int(f[1]) if len(f) > 1 else 0
+        elif arm[0] == "x":  # "xFORM": gemm_xd form mt*100 + nf*10 + splitk (x0: by shape)
+            form = int(arm[1:] or 0)
             if a.epi == "residual":
-                fns[arm] = lambda nf=nf, st=st: G.xd_gemm(x, nxt(), "residual", residual=res,
-                                                          out=res, nf=nf, stages=st)
+                fns[arm] = lambda form=form: G.xd_gemm(x, nxt(), "residual", residual=res,
+                                                       out=res, form=form)
             else:
-                fns[arm] = lambda nf=nf, st=st: G.xd_gemm(x, nxt(), out=out, nf=nf, stages=st)
+                fns[arm] = lambda form=form: G.xd_gemm(x, nxt(), out=out, form=form)
         else:
             # "vV" or "vV:splitk:group_m" (group_m < 0: K-slice-by-XCD tile order)
             f = arm[1:].split(":")

@@ -468,3 +468,50 @@ def test_request_wait_races_finish():
         assert res == [True] and r.finish_reason == "stop"
     r = Request([1])
     assert r.wait(0.01) is False  # not finished: times out
+
+
+def test_engine_loop_burst_gathering():
+    """EngineLoop burst gathering (DRTC_BURST_GAP_MS): while requests keep arriving less than
+    the gap apart, the loop lets them gather (bounded by burst_max_s) instead of stepping on
+    the first one; off by default; a lone request waits at most the gap."""
+    import collections
+    import time
+
+    from drtc_amd.engine.engine import EngineLoop
+
+    class Stub:
+        def __init__(self):
+            self.waiting, self.running, self._inflight, self._aborts = [], [], None, []
+            self._waiting_tokens, self.prefill_chunk_tokens, self.max_batch = 0, 16384, 1024
+            self.stats, self.steps, self.batches = collections.Counter(), 0, []
+
+        def add_request(self, r):
+            self.waiting.append(r)
+            self._waiting_tokens += 100
+
+        def has_work(self):
+            return bool(self.waiting)
+
+        def step(self):
+            self.steps += 1
+            self.batches.append(len(self.waiting))
+            self.waiting.clear()
+            self._waiting_tokens = 0
+
+    assert EngineLoop(Stub()).burst_gap_s == 0.0  # off unless configured
+    e = Stub()
+    loop = EngineLoop(e, burst_gap_s=0.02, burst_max_s=0.5).start()
+    try:
+        for _ in range(20):  # a burst: 20 arrivals 1 ms apart -> gathered into few steps
+            loop.submit(object())
+            time.sleep(0.001)
+        time.sleep(0.15)
+        assert sum(e.batches) == 20 and e.steps <= 3, e.batches
+        assert e.stats["burst_hold_us"] > 0
+        t0 = time.perf_counter()
+        loop.submit(object())  # a lone request: stepped once the gap has passed
+        while e.waiting:
+            time.sleep(0.001)
+        assert time.perf_counter() - t0 < 0.2
+    finally:
+        loop.stop()

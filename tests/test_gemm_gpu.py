@@ -263,8 +263,10 @@ def test_w4_persistent_rejects_single_k_tile_and_splitk(hipk):
     w = torch.randn(256, 512, device="cuda", dtype=torch.bfloat16)
     with pytest.raises(RuntimeError):
         G.mfma_gemm(x, w, variant=15, splitk=2)
-    with pytest.raises(RuntimeError):
-        G.mfma_gemm(x, w, variant=31)  # 2 x 1 tiles: fewer than one per XCD label
+    # 2 x 1 tiles, fewer than one per XCD label: the plain persistent form runs
+    y = G.mfma_gemm(x, w, variant=31)
+    torch.cuda.synchronize()
+    _check(y, _ref(x, w, "store", None))
 
 
 # ------------------------------------------------------------------ projection router
@@ -319,24 +321,30 @@ def test_linear_off_bucket_matches_fp32(hipk):
 
 # ---------------------------------------------------------------- gemm_xd.hip (decode tiles)
 @pytest.mark.parametrize("epi", ["store", "residual"])
-@pytest.mark.parametrize("nf,stages", [(2, 4), (2, 6), (4, 4), (4, 5), (6, 3), (6, 4)])
-@pytest.mark.parametrize("M,N,K", [(1024, 768, 4096), (1000, 1536, 448), (77, 384, 1024),
-                                   (512, 3072, 1472), (129, 1152, 2048)])
-def test_xd_gemm_matches_fp32(hipk, epi, nf, stages, M, N, K):
-    if not G.xd_supported(M, N, K, nf, stages):
-        pytest.skip("shape outside the nf tile grid")
-    g = torch.Generator(device="cuda").manual_seed(M * 7 + N + K + nf)
+@pytest.mark.parametrize("form", sorted(G.XD_FORMS))
+@pytest.mark.parametrize("M,N,K", [(1024, 768, 4096), (1000, 1536, 896), (77, 384, 1024),
+                                   (512, 3072, 1408), (129, 1152, 2048), (300, 768, 640)])
+def test_xd_gemm_matches_fp32(hipk, epi, form, M, N, K):
+    if not G.xd_supported(M, N, K, form):
+        pytest.skip("shape outside the form's tile grid")
+    g = torch.Generator(device="cuda").manual_seed(M * 7 + N + K + form)
     x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16, generator=g)
     w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16, generator=g) * 0.05
     res = torch.randn(M, N, device="cuda", dtype=torch.bfloat16, generator=g) \
         if epi == "residual" else None
     ref = _ref(x, w, epi, res)
-    out = G.xd_gemm(x, w, epi, residual=res, nf=nf, stages=stages)
+    out = G.xd_gemm(x, w, epi, residual=res, form=form)
     torch.cuda.synchronize()
     _check(out, ref)
+    if form % 10 == 2:  # split-K: counters re-armed, a second call gives the same bits
+        out2 = G.xd_gemm(x, w, epi, residual=res, form=form)
+        torch.cuda.synchronize()
+        assert torch.equal(out, out2)
+        assert int(G.gemm_workspace(x.device)[1][:2 * 64 + 1].abs().sum()) == 0
 
 
-def test_xd_gemm_strided_input_in_place_residual_and_graph(hipk):
+@pytest.mark.parametrize("form", [141, 242])
+def test_xd_gemm_strided_input_in_place_residual_and_graph(hipk, form):
     M, N, K = 640, 4096, 2048
     g = torch.Generator(device="cuda").manual_seed(5)
     big = torch.randn(M, K + 192, device="cuda", dtype=torch.bfloat16, generator=g)
@@ -345,16 +353,16 @@ def test_xd_gemm_strided_input_in_place_residual_and_graph(hipk):
     res = torch.randn(M, N, device="cuda", dtype=torch.bfloat16, generator=g)
     ref = _ref(x, w, "residual", res)
     r = res.clone()
-    G.xd_gemm(x, w, "residual", residual=r, out=r)  # in place into the residual stream
+    G.xd_gemm(x, w, "residual", residual=r, out=r, form=form)  # in place into the residual
     torch.cuda.synchronize()
     _check(r, ref)
     out = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
     s = torch.cuda.Stream()
     with torch.cuda.stream(s):
-        G.xd_gemm(x, w, out=out)
+        G.xd_gemm(x, w, out=out, form=form)
         gr = torch.cuda.CUDAGraph()
         with torch.cuda.graph(gr, stream=s):
-            G.xd_gemm(x, w, out=out)
+            G.xd_gemm(x, w, out=out, form=form)
     for _ in range(3):
         out.zero_()
         gr.replay()
@@ -363,23 +371,19 @@ def test_xd_gemm_strided_input_in_place_residual_and_graph(hipk):
 
 
 def test_xd_gemm_rejects_bad_shapes(hipk):
-    x = torch.randn(64, 512, device="cuda", dtype=torch.bfloat16)
-    w = torch.randn(200, 512, device="cuda", dtype=torch.bfloat16)  # N % 64 != 0
-    y = torch.empty(64, 200, device="cuda", dtype=torch.bfloat16)
-    for nf in (2, 4, 6, 3):
-        assert hipk.gemm_xd(y.data_ptr(), x.data_ptr(), w.data_ptr(), 0, 64, 200, 512, 512, 512,
-                            200, 0, 0, nf, 0, 0) == -1
-    # a ring depth that is not built
-    assert hipk.gemm_xd(y.data_ptr(), x.data_ptr(), w.data_ptr(), 0, 64, 256, 512, 512, 512,
-                        256, 0, 0, 4, 7, 0) == -1
-    w2 = torch.randn(256, 256, device="cuda", dtype=torch.bfloat16)
-    x2 = torch.randn(64, 256, device="cuda", dtype=torch.bfloat16)
-    y2 = torch.empty(64, 256, device="cuda", dtype=torch.bfloat16)
-    # K / 64 must exceed the stage count (4 at nf 4)
-    assert hipk.gemm_xd(y2.data_ptr(), x2.data_ptr(), w2.data_ptr(), 0, 64, 256, 256, 256, 256,
-                        256, 0, 0, 4, 0, 0) == -1
-    # residual epilogue without a residual
-    x3 = torch.randn(64, 512, device="cuda", dtype=torch.bfloat16)
-    w3 = torch.randn(256, 512, device="cuda", dtype=torch.bfloat16)
-    assert hipk.gemm_xd(y2.data_ptr(), x3.data_ptr(), w3.data_ptr(), 0, 64, 256, 512, 512, 512,
-                        256, 0, 1, 2, 0, 0) == -1
+    def call(M, N, K, epi=0, mt=1, nf=4, sk=1, ws=None):
+        x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
+        w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16)
+        y = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+        slab, cnt = ws or (None, None)
+        return hipk.gemm_xd(y.data_ptr(), x.data_ptr(), w.data_ptr(), 0, M, N, K, K, K, N, 0,
+                            epi, mt, nf, sk, slab.data_ptr() if slab is not None else 0,
+                            slab.numel() * 4 if slab is not None else 0,
+                            cnt.data_ptr() if cnt is not None else 0,
+                            cnt.numel() if cnt is not None else 0, 0)
+    assert call(64, 200, 512, nf=2) == -1        # N not a multiple of the tile width
+    assert call(64, 256, 512, nf=3) == -1        # no such form
+    assert call(64, 256, 512, mt=1, sk=2) == -1  # split-K is a 256-row form
+    assert call(64, 256, 256, nf=4) == -1        # K / 64 must exceed the ring depth (4)
+    assert call(64, 256, 512, epi=1, nf=2) == -1  # residual epilogue without a residual
+    assert call(256, 256, 1024, mt=2, nf=4, sk=2) == -2  # split-K without a workspace
