@@ -98,7 +98,7 @@ PYBIND11_MODULE(_hipk, m) {
                                 P<void>(slab), slab_bytes, P<int>(counters), n_counters,
                                 variant - 7, S(st));
   });
-  // gemm_xd (ops.gemm.xd_gemm): decode-shaped tiles, XCD-partitioned order, split-K 1 / 2
+  // gemm_xd (ops.gemm.xd_gemm): decode-shaped tiles, XCD-partitioned order, split-K 1..8
   m.def("gemm_xd", [](u64 c, u64 a, u64 b, u64 r, int M, int N, int K, int lda, int ldb, int ldc,
                       int ldr, int epi, int mt, int nf, int splitk, u64 slab, int64_t slab_bytes,
                       u64 counters, int n_counters, u64 st) {

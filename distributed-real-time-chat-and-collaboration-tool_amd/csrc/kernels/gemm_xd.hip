@@ -7,9 +7,10 @@
 // set by the operand bytes each CU must read: (rows + columns of its tile) x K x 2.  This
 // kernel picks the tile per shape:
 //
-//   * 128 MT x 32 NF output tiles (MT 1 / 2, NF 2 / 4 / 6), K split over SK = 1 / 2 slices,
-//     one workgroup per (tile, slice) and per CU (o / down at M = 1024: 8 x 32 tiles of
-//     128 x 128, or 4 x 32 x 2 slices of 256 x 128; qkv N = 6144: 8 x 32 of 128 x 192).
+//   * 128 MT x 32 NF output tiles (MT 1 / 2, NF 2 / 4 / 6), K split over splitk = 1..8 slices
+//     (whole K tiles, as even as they divide), one workgroup per (tile, slice) and per CU
+//     (o / down at M = 1024: 8 x 32 tiles of 128 x 128, or 4 x 32 x 2 slices of 256 x 128;
+//     qkv N = 6144: 8 x 32 of 128 x 192; Llama-3-70B at M = 256: 256 x 128 x 3-4 slices).
 //   * Tile order partitioned by XCD (workgroup b runs on XCD b % 8 under round-robin dispatch -
 //     used for speed only, the map below is a bijection of blockIdx): XCD x owns one K slice of
 //     a contiguous range of the column-major tile order, i.e. a contiguous set of weight column
@@ -28,13 +29,16 @@
 //     [vmcnt: own DMA of tile t + 1 landed, lgkmcnt(0), ONE barrier: everyone's tile t + 1
 //     landed and every read of stage t done]; half 1 MFMAs | LDS-DMA of tile t + S into stage
 //     t + ds_read of tile t + 1 half 0.  The first K tile accumulates onto a zero C operand.
-//   * Split-K 2 with a ticket-first combine: each slice draws a ticket when its K loop ends;
-//     the first writes its fp32 tile to the slab (write-through sc1 stores, drained, barrier)
-//     and raises the tile's ready flag; the second (already resident and finished: no wait on
-//     an unscheduled workgroup) polls the flag (bounded), adds the partial (sc1 loads), stores,
-//     and re-arms both counters.  cdna_hip_programming.md §6 G16 hand-off recipe.
+//   * Split-K with a ticket-first combine: each slice draws a ticket when its K loop ends;
+//     tickets 0 .. splitk - 2 write their fp32 tile to their slab slot (write-through sc1
+//     stores, drained, barrier) and count themselves ready; the last ticket (resident, and
+//     waiting only for slices that already hold a ticket: no wait on an unscheduled
+//     workgroup) polls the ready count (bounded), adds the partials (sc1 loads) inside its
+//     epilogue and re-arms both counters.  cdna_hip_programming.md §6 G16 hand-off recipe.
 //   * Epilogue through LDS (the wave's tile as bf16, then 16-B row-contiguous global stores):
-//     store, or + residual (may alias c).
+//     store, + residual (may alias c), or SiLU / tanh-GELU gating of a [gate; up] weight:
+//     each wave's B rows hold the gate rows (fragments j < NF / 2) and the up rows (j >= NF /
+//     2) of the SAME 8 NF output columns, so the gate value meets its up value in a lane.
 #include "common.h"
 #include "launchers.h"
 
@@ -46,11 +50,14 @@ namespace {
 typedef __attribute__((address_space(3))) void* xd_lds_ptr;
 
 constexpr int kXdThreads = 256;
-enum { XD_STORE = 0, XD_RESIDUAL = 1 };
+enum { XD_STORE = 0, XD_RESIDUAL = 1, XD_SILU = 2, XD_GELU = 3 };
+template <int EPI>
+DRTC_DEVICE constexpr bool xd_glu() { return EPI == XD_SILU || EPI == XD_GELU; }
 
-template <int MT_, int NF_, int S_, int SK_>
+template <int MT_, int NF_, int S_, bool SPLIT_>
 struct XdCfg {
-  static constexpr int MT = MT_, NF = NF_, S = S_, SK = SK_;
+  static constexpr int MT = MT_, NF = NF_, S = S_;
+  static constexpr bool SPLIT = SPLIT_;            // split-K combine compiled in
   static constexpr int TM = 128 * MT;              // tile rows
   static constexpr int TN = 32 * NF;               // tile columns
   static constexpr int FA = 4 * MT;                // A fragments per wave (16 rows each)
@@ -73,9 +80,10 @@ struct XdParams {
   const bf16_t* r;
   float* slab;
   int* counters;
-  int M, N, K;
+  int M, N, K;  // N = columns of c (gated: N = up_off, b has 2 N rows)
   int lda, ldb, ldc, ldr;
   int tiles_m, tiles_n, per_xcd;
+  int splitk, up_off;
 };
 
 template <class C>
@@ -230,19 +238,23 @@ DRTC_DEVICE void xd_tail(f32x4 (&acc)[C::FA][C::NF], bf16x8 (&fa0)[C::FA], bf16x
   }
 }
 
-// Split-K 2, ticket-first combine (see the file comment).  Counters of tile t: [2 t] ticket,
-// [2 t + 1] ready flag; [2 tiles] the error word (a partial that never arrived).  Returns false
-// for the first arriver (which published its partial and is done), true for the second, which
-// adds the partial inside the epilogue (xd_partial: one fragment at a time, so the
-// accumulators stay in place) and re-arms the counters.
+// Split-K, ticket-first combine (see the file comment).  Counters of tile t: [2 t] ticket,
+// [2 t + 1] ready count; [2 tiles] the error word (a partial that never arrived).  The slab
+// holds splitk - 1 partial slots per tile.  Returns false for a slice that published its
+// partial (it is done), true for the last ticket, which adds the partials inside the
+// epilogue (xd_partial: one fragment at a time, so the accumulators stay in place) and
+// re-arms the counters.
+template <class C>
+constexpr int xd_tile_bytes() { return C::FA * C::NF * kXdThreads * 16; }
+constexpr int kXdSc1 = 16;  // cache-policy bits of the buffer op: sc1 (write-through)
+
 template <class C>
 DRTC_DEVICE __amdgpu_buffer_rsrc_t xd_slab(const XdParams& p, int tile) {
-  constexpr int kTileBytes = C::FA * C::NF * kXdThreads * 16;
+  const int64_t slot = (int64_t)xd_tile_bytes<C>();
   return __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(reinterpret_cast<char*>(p.slab) + (int64_t)tile * kTileBytes), (short)0,
-      kTileBytes, 0x00020000);
+      (void*)(reinterpret_cast<char*>(p.slab) + (int64_t)tile * (p.splitk - 1) * slot), (short)0,
+      (int)((p.splitk - 1) * slot), 0x00020000);
 }
-constexpr int kXdSc1 = 16;  // cache-policy bits of the buffer op: sc1 (write-through)
 
 template <class C>
 DRTC_DEVICE bool xd_combine(const XdParams& p, f32x4 (&acc)[C::FA][C::NF], int tile, char* lds) {
@@ -255,24 +267,26 @@ DRTC_DEVICE bool xd_combine(const XdParams& p, f32x4 (&acc)[C::FA][C::NF], int t
   if (tid == 0)
     *flag = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
-  if (*flag == 0) {
-    // first: publish the partial in fragment order (16 B per lane, coalesced), then the flag
+  const int t = *flag;
+  if (t < p.splitk - 1) {
+    // publish the partial in slot t, fragment order (16 B per lane, coalesced), then count
+    const int base = t * xd_tile_bytes<C>();
 #pragma unroll
     for (int i = 0; i < C::FA; ++i)
 #pragma unroll
       for (int j = 0; j < C::NF; ++j)
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), slab,
-                                               ((i * C::NF + j) * kXdThreads + tid) * 16, 0,
-                                               kXdSc1);
+                                               base + ((i * C::NF + j) * kXdThreads + tid) * 16,
+                                               0, kXdSc1);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (tid == 0) __hip_atomic_store(ready, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid == 0) __hip_atomic_fetch_add(ready, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return false;
   }
-  // second: the first arriver is resident and past its K loop - its flag comes
+  // the last ticket: every other slice holds a ticket (resident, past its K loop)
   if (tid == 0) {
     int spins = 0;
-    while (__hip_atomic_load(ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
+    while (__hip_atomic_load(ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < p.splitk - 1) {
       __builtin_amdgcn_s_sleep(1);
       if (++spins > (1 << 24)) {  // never hang the GPU: record the fault and go on
         __hip_atomic_store(p.counters + 2 * p.tiles_m * p.tiles_n, 1, __ATOMIC_RELAXED,
@@ -285,33 +299,40 @@ DRTC_DEVICE bool xd_combine(const XdParams& p, f32x4 (&acc)[C::FA][C::NF], int t
   return true;
 }
 
+// Fragment (i, j) of every published partial of the tile, summed in slot order.
 template <class C>
-DRTC_DEVICE f32x4 xd_partial(const __amdgpu_buffer_rsrc_t& slab, int i, int j) {
-  return __builtin_bit_cast(
-      f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                 slab, ((i * C::NF + j) * kXdThreads + (int)threadIdx.x) * 16, 0, kXdSc1));
+DRTC_DEVICE f32x4 xd_partial(const XdParams& p, const __amdgpu_buffer_rsrc_t& slab, int i, int j) {
+  const int off = ((i * C::NF + j) * kXdThreads + (int)threadIdx.x) * 16;
+  f32x4 v = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(slab, off, 0, kXdSc1));
+  for (int t = 1; t < p.splitk - 1; ++t)
+    v += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                       slab, off + t * xd_tile_bytes<C>(), 0, kXdSc1));
+  return v;
 }
 
 template <class C, int EPI>
 __global__ __launch_bounds__(kXdThreads, 1) void gemm_xd_kernel(XdParams p) {
   constexpr int MT = C::MT, NF = C::NF, FA = C::FA;
   extern __shared__ __attribute__((aligned(16))) char xd_lds[];
-  // ---- work item: XCD label x = b % 8 takes K slice x % SK of the tiles
-  // [(x / SK) per_xcd, (x / SK + 1) per_xcd) of the column-major order (all row tiles of a
-  // weight panel consecutive)
+  // ---- work item: XCD label x = b % 8 takes the items [x per_xcd, (x + 1) per_xcd) of the
+  // slice-major, column-major order (item = slice * tiles + tile; all row tiles of a weight
+  // panel consecutive): an XCD streams one K slice of a contiguous block of column panels
   const int b = blockIdx.x;
-  const int x = b & 7;
-  const int slice = C::SK == 1 ? 0 : x % C::SK;
-  const int tile = (x / C::SK) * p.per_xcd + (b >> 3);
-  if (tile >= p.tiles_m * p.tiles_n) return;
+  const int ntiles = p.tiles_m * p.tiles_n;
+  const int item = (b & 7) * p.per_xcd + (b >> 3);
+  if (item >= ntiles * p.splitk) return;
+  const int slice = item / ntiles, tile = item - slice * ntiles;
   const int tn = tile / p.tiles_m, tm = tile - tn * p.tiles_m;
-  const int m0 = C::TM * tm, n0 = C::TN * tn;
+  constexpr int TNO = xd_glu<EPI>() ? C::TN / 2 : C::TN;  // output columns per tile
+  const int m0 = C::TM * tm, n0 = TNO * tn;
 
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wv >> 1, wn = wv & 1, l16 = lane & 15, g = lane >> 4;
-  const int nk = (p.K >> 6) / C::SK;  // K tiles of this slice
-  const int64_t k0 = (int64_t)slice * nk * 64;
+  const int nkt = p.K >> 6;  // slice s: K tiles [s nkt / splitk, (s + 1) nkt / splitk)
+  const int kt0 = slice * nkt / p.splitk;
+  const int nk = (slice + 1) * nkt / p.splitk - kt0;
+  const int64_t k0 = (int64_t)kt0 * 64;
 
   // ---- DMA plan: instruction i of wave wv fills stage rows 32 MT wv + 8 i + (lane >> 3)
   // (A) / 8 NF wv + 8 i + (lane >> 3) (B), lane's LDS chunk lane & 7 <- source chunk ^
@@ -334,7 +355,15 @@ __global__ __launch_bounds__(kXdThreads, 1) void gemm_xd_kernel(XdParams p) {
     for (int i = 0; i < C::DB; ++i) {
       const int R = 8 * NF * wv + 8 * i + (lane >> 3);
       const int c = (lane & 7) ^ ((R >> 1) & 7);
-      d.vb[i] = (unsigned)(R * p.ldb * 2 + c * 16);
+      int src = R;  // weight row (relative to n0) of stage row R
+      if constexpr (xd_glu<EPI>()) {
+        // wave half w = R / 16 NF, fragment jb = (R % 16 NF) / 16: gate rows of output
+        // columns w 8 NF + (jb % (NF / 2)) 16 + (R % 16), then the up rows of the same columns
+        const int w = R / (16 * NF), jb = (R % (16 * NF)) / 16;
+        const int col = w * 8 * NF + (jb % (NF / 2)) * 16 + (R & 15);
+        src = jb < NF / 2 ? col : p.up_off + col;
+      }
+      d.vb[i] = (unsigned)(src * p.ldb * 2 + c * 16);
     }
     d.lds_a = __builtin_amdgcn_readfirstlane(lds0 + 32 * MT * wv * 128);
     d.lds_b = __builtin_amdgcn_readfirstlane(lds0 + C::BOFF + 8 * NF * wv * 128);
@@ -379,43 +408,62 @@ __global__ __launch_bounds__(kXdThreads, 1) void gemm_xd_kernel(XdParams p) {
   xd_tail<C, C::S - 2>(acc, fa0, fb0, fa1, fb1, lds, cur, f, d);
   xd_vmcnt<0>();
 
-  bool part = false;  // split-K: this workgroup adds the other slice's partial
-  if constexpr (C::SK == 2) {
+  bool part = false;  // split-K: this workgroup adds the other slices' partials
+  if constexpr (C::SPLIT) {
     if (!xd_combine<C>(p, acc, tile, xd_lds)) return;
     part = true;
   }
 
-  // ---- epilogue: the wave's 64 MT x 16 NF tile as bf16 into LDS, then 16-B global stores of
-  // whole row segments (acc[i][j][r] = C[64 MT wm + 16 i + 4 g + r][16 NF wn + 16 j + l16])
+  // ---- epilogue: the wave's tile as bf16 into LDS, then 16-B global stores of whole row
+  // segments (acc[i][j][r] = C[64 MT wm + 16 i + 4 g + r][16 NF wn + 16 j + l16]; gated:
+  // output column 8 NF wn + 16 j + l16 = act(acc[i][j]) * acc[i][j + NF / 2], j < NF / 2)
   __syncthreads();  // every wave is done reading the stages
-  char* ep = xd_lds + wv * 64 * MT * C::PITCH;
-  const __amdgpu_buffer_rsrc_t slab = xd_slab<C>(p, C::SK == 2 ? tile : 0);
+  constexpr int OC = xd_glu<EPI>() ? 8 * NF : 16 * NF;  // output columns per wave
+  constexpr int PITCH = 2 * OC + 16;
+  char* ep = xd_lds + wv * 64 * MT * PITCH;
+  const __amdgpu_buffer_rsrc_t slab = xd_slab<C>(p, C::SPLIT ? tile : 0);
 #pragma unroll
-  for (int i = 0; i < FA; ++i)
+  for (int i = 0; i < FA; ++i) {
+    if constexpr (xd_glu<EPI>()) {
 #pragma unroll
-    for (int j = 0; j < NF; ++j) {
-      f32x4 v = acc[i][j];
-      if (C::SK == 2 && part) v += xd_partial<C>(slab, i, j);
+      for (int j = 0; j < NF / 2; ++j) {
+        f32x4 gv = acc[i][j], uv = acc[i][j + NF / 2];
+        if (C::SPLIT && part) {
+          gv += xd_partial<C>(p, slab, i, j);
+          uv += xd_partial<C>(p, slab, i, j + NF / 2);
+        }
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
-        *reinterpret_cast<bf16_t*>(ep + (16 * i + 4 * g + r) * C::PITCH + (16 * j + l16) * 2) =
-            f2bf(v[r]);
+        for (int r = 0; r < 4; ++r)
+          *reinterpret_cast<bf16_t*>(ep + (16 * i + 4 * g + r) * PITCH + (16 * j + l16) * 2) =
+              f2bf(act_value<EPI == XD_SILU ? 0 : 1>(gv[r]) * uv[r]);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < NF; ++j) {
+        f32x4 v = acc[i][j];
+        if (C::SPLIT && part) v += xd_partial<C>(p, slab, i, j);
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          *reinterpret_cast<bf16_t*>(ep + (16 * i + 4 * g + r) * PITCH + (16 * j + l16) * 2) =
+              f2bf(v[r]);
+      }
     }
-  if (C::SK == 2 && part && threadIdx.x == 0) {
+  }
+  if (C::SPLIT && part && threadIdx.x == 0) {
     // re-arm (the next launch on this stream starts after this one ends)
     __hip_atomic_store(p.counters + 2 * tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(p.counters + 2 * tile + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __syncthreads();
-  constexpr int CPR = 2 * NF;  // 16-B chunks per wave-tile row
+  constexpr int CPR = OC / 8;  // 16-B chunks per wave-tile row
 #pragma unroll
   for (int s = 0; s < CPR * MT; ++s) {
     const int q = lane + 64 * s;
     const int row = q / CPR, ch = q - row * CPR;
     const int m = m0 + 64 * MT * wm + row;
     if (m >= p.M) continue;
-    const int n = n0 + 16 * NF * wn + 8 * ch;
-    bf16x8 v = *reinterpret_cast<const bf16x8*>(ep + row * C::PITCH + ch * 16);
+    const int n = n0 + OC * wn + 8 * ch;
+    bf16x8 v = *reinterpret_cast<const bf16x8*>(ep + row * PITCH + ch * 16);
     if constexpr (EPI == XD_RESIDUAL) {
       const bf16x8 rv = *reinterpret_cast<const bf16x8*>(p.r + (int64_t)m * p.ldr + n);
 #pragma unroll
@@ -425,34 +473,46 @@ __global__ __launch_bounds__(kXdThreads, 1) void gemm_xd_kernel(XdParams p) {
   }
 }
 
-template <class C>
-int xd_launch(const XdParams& p, bool res, hipStream_t st) {
-  if (res)
-    hipLaunchKernelGGL((gemm_xd_kernel<C, XD_RESIDUAL>), dim3(8 * p.per_xcd), dim3(kXdThreads),
-                       (C::LDS), st, p);
-  else
-    hipLaunchKernelGGL((gemm_xd_kernel<C, XD_STORE>), dim3(8 * p.per_xcd), dim3(kXdThreads),
-                       (C::LDS), st, p);
+template <class C, int EPI>
+int xd_launch_e(const XdParams& p, hipStream_t st) {
+  hipLaunchKernelGGL((gemm_xd_kernel<C, EPI>), dim3(8 * p.per_xcd), dim3(kXdThreads), (C::LDS),
+                     st, p);
   return (int)hipGetLastError();
 }
 
 template <class C>
+int xd_launch(const XdParams& p, int epi, hipStream_t st) {
+  switch (epi) {
+    case XD_STORE: return xd_launch_e<C, XD_STORE>(p, st);
+    case XD_RESIDUAL: return xd_launch_e<C, XD_RESIDUAL>(p, st);
+    case XD_SILU: return xd_launch_e<C, XD_SILU>(p, st);
+    default: return xd_launch_e<C, XD_GELU>(p, st);
+  }
+}
+
+template <class C>
 int xd_cfg() {
-  return (int)hipFuncSetAttribute((const void*)gemm_xd_kernel<C, XD_STORE>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS) |
-         (int)hipFuncSetAttribute((const void*)gemm_xd_kernel<C, XD_RESIDUAL>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
+  int e = 0;
+  for (const void* f : {(const void*)gemm_xd_kernel<C, XD_STORE>,
+                        (const void*)gemm_xd_kernel<C, XD_RESIDUAL>,
+                        (const void*)gemm_xd_kernel<C, XD_SILU>,
+                        (const void*)gemm_xd_kernel<C, XD_GELU>})
+    e |= (int)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
+  return e;
 }
 
 // Forms built (mt, nf) -> ring depth: 128-row tiles nf 2 / 4 / 6 (4 / 4 / 3 stages), 256-row
-// tiles nf 4 / 6 (3 / 2 stages); the 256-row forms with split-K 1 or 2.
-using Xd1x2 = XdCfg<1, 2, 4, 1>;
-using Xd1x4 = XdCfg<1, 4, 4, 1>;
-using Xd1x6 = XdCfg<1, 6, 3, 1>;
-using Xd2x4 = XdCfg<2, 4, 3, 1>;
-using Xd2x6 = XdCfg<2, 6, 2, 1>;
-using Xd2x4k2 = XdCfg<2, 4, 3, 2>;
-using Xd2x6k2 = XdCfg<2, 6, 2, 2>;
+// tiles nf 4 / 6 (3 / 2 stages); each with and without the split-K combine.
+template <bool SP>
+using Xd1x2 = XdCfg<1, 2, 4, SP>;
+template <bool SP>
+using Xd1x4 = XdCfg<1, 4, 4, SP>;
+template <bool SP>
+using Xd1x6 = XdCfg<1, 6, 3, SP>;
+template <bool SP>
+using Xd2x4 = XdCfg<2, 4, 3, SP>;
+template <bool SP>
+using Xd2x6 = XdCfg<2, 6, 2, SP>;
 
 int xd_stages(int mt, int nf) {
   if (mt == 1) return nf == 6 ? 3 : (nf == 2 || nf == 4 ? 4 : 0);
@@ -460,29 +520,44 @@ int xd_stages(int mt, int nf) {
   return 0;
 }
 
+template <bool SP>
+int xd_dispatch(const XdParams& p, int mt, int nf, int epi, hipStream_t st) {
+  switch (mt * 10 + nf) {
+    case 12: return xd_launch<Xd1x2<SP>>(p, epi, st);
+    case 14: return xd_launch<Xd1x4<SP>>(p, epi, st);
+    case 16: return xd_launch<Xd1x6<SP>>(p, epi, st);
+    case 24: return xd_launch<Xd2x4<SP>>(p, epi, st);
+    case 26: return xd_launch<Xd2x6<SP>>(p, epi, st);
+    default: return -1;
+  }
+}
+
 }  // namespace
 
-int64_t gemm_xd_workspace_bytes(int M, int N, int mt, int nf, int splitk) {
+int64_t gemm_xd_workspace_bytes(int M, int N, int mt, int nf, int splitk, int glu) {
   if (splitk < 2 || mt < 1 || nf < 1) return 0;
-  const int64_t tiles = (int64_t)((M + 128 * mt - 1) / (128 * mt)) * (N / (32 * nf));
-  return tiles * (128 * mt) * (32 * nf) * 4;
+  const int tno = glu ? 16 * nf : 32 * nf;
+  const int64_t tiles = (int64_t)((M + 128 * mt - 1) / (128 * mt)) * (N / tno);
+  return tiles * (splitk - 1) * (128 * mt) * (32 * nf) * 4;
 }
 
 int launch_gemm_xd(void* c, const void* a, const void* b, const void* r, int M, int N, int K,
                    int lda, int ldb, int ldc, int ldr, int epi, int mt, int nf, int splitk,
                    void* slab, int64_t slab_bytes, int* counters, int n_counters,
                    hipStream_t st) {
-  if (epi != XD_STORE && epi != XD_RESIDUAL) return -1;
+  if (epi < XD_STORE || epi > XD_GELU) return -1;
+  const bool glu = epi == XD_SILU || epi == XD_GELU;
   const int stages = xd_stages(mt, nf);
-  if (stages == 0 || (splitk != 1 && splitk != 2) || (splitk == 2 && mt != 2)) return -1;
+  if (stages == 0 || splitk < 1 || splitk > 8 || (glu && nf % 2)) return -1;
   if (lda % 8 || ldb % 8 || ldc % 8) return -1;
   if ((uintptr_t)a % 16 || (uintptr_t)b % 16 || (uintptr_t)c % 16) return -1;
   if (epi == XD_RESIDUAL && (r == nullptr || ldr % 8 || (uintptr_t)r % 16)) return -1;
-  const int tm_rows = 128 * mt, tn = 32 * nf;
-  // shape contract: whole column tiles, whole K tiles per slice, more K tiles per slice than
-  // the ring holds (the first K tile is peeled), 32-bit buffer offsets from the tile bases
-  if (M <= 0 || N <= 0 || N % tn || K % (64 * splitk) || K / 64 / splitk <= stages) return -1;
-  if ((int64_t)tm_rows * lda * 2 >= (1ll << 31) || (int64_t)tn * ldb * 2 >= (1ll << 31))
+  const int tm_rows = 128 * mt, tno = glu ? 16 * nf : 32 * nf;
+  // shape contract: whole column tiles, every slice more K tiles than the ring holds (the
+  // first K tile is peeled), 32-bit buffer offsets from the tile bases
+  if (M <= 0 || N <= 0 || N % tno || K % 64 || K / 64 / splitk <= stages) return -1;
+  if ((int64_t)tm_rows * lda * 2 >= (1ll << 31) ||
+      (int64_t)(glu ? N + tno : 32 * nf) * ldb * 2 >= (1ll << 31))
     return -1;
   XdParams p{};
   p.c = (bf16_t*)c;
@@ -492,34 +567,28 @@ int launch_gemm_xd(void* c, const void* a, const void* b, const void* r, int M, 
   p.M = M; p.N = N; p.K = K;
   p.lda = lda; p.ldb = ldb; p.ldc = ldc; p.ldr = ldr;
   p.tiles_m = (M + tm_rows - 1) / tm_rows;
-  p.tiles_n = N / tn;
+  p.tiles_n = N / tno;
+  p.splitk = splitk;
+  p.up_off = glu ? N : 0;
   const int64_t tiles = (int64_t)p.tiles_m * p.tiles_n;
   if (tiles * splitk * 8 >= (1ll << 31)) return -1;
-  // XCD labels per slice: 8 / splitk; each takes per_xcd consecutive tiles
   p.per_xcd = (int)((tiles * splitk + 7) / 8);
-  if (splitk == 2) {
+  if (splitk > 1) {
     if (slab == nullptr || counters == nullptr || n_counters < 2 * tiles + 1 ||
-        slab_bytes < gemm_xd_workspace_bytes(M, N, mt, nf, splitk))
+        slab_bytes < gemm_xd_workspace_bytes(M, N, mt, nf, splitk, glu))
       return -2;
     p.slab = (float*)slab;
     p.counters = counters;
+    return xd_dispatch<true>(p, mt, nf, epi, st);
   }
-  const bool res = epi == XD_RESIDUAL;
-  switch (mt * 100 + nf * 10 + splitk) {
-    case 121: return xd_launch<Xd1x2>(p, res, st);
-    case 141: return xd_launch<Xd1x4>(p, res, st);
-    case 161: return xd_launch<Xd1x6>(p, res, st);
-    case 241: return xd_launch<Xd2x4>(p, res, st);
-    case 261: return xd_launch<Xd2x6>(p, res, st);
-    case 242: return xd_launch<Xd2x4k2>(p, res, st);
-    case 262: return xd_launch<Xd2x6k2>(p, res, st);
-    default: return -1;
-  }
+  return xd_dispatch<false>(p, mt, nf, epi, st);
 }
 
 int configure_gemm_xd() {
-  return xd_cfg<Xd1x2>() | xd_cfg<Xd1x4>() | xd_cfg<Xd1x6>() | xd_cfg<Xd2x4>() |
-         xd_cfg<Xd2x6>() | xd_cfg<Xd2x4k2>() | xd_cfg<Xd2x6k2>();
+  return xd_cfg<Xd1x2<false>>() | xd_cfg<Xd1x4<false>>() | xd_cfg<Xd1x6<false>>() |
+         xd_cfg<Xd2x4<false>>() | xd_cfg<Xd2x6<false>>() | xd_cfg<Xd1x2<true>>() |
+         xd_cfg<Xd1x4<true>>() | xd_cfg<Xd1x6<true>>() | xd_cfg<Xd2x4<true>>() |
+         xd_cfg<Xd2x6<true>>();
 }
 
 }  // namespace drtc

@@ -119,15 +119,16 @@ int launch_gemm_w4(void* c, const void* a, const void* b, const void* r, int M, 
 int64_t gemm_w4_workspace_bytes(int64_t M, int64_t N, int splitk);
 int configure_gemm_w4();
 
-// XCD-partitioned decode GEMM (gemm_xd.hip): c[M,N] = a[M,K] . b[N,K]^T (+ r when epi == 1, may
-// alias c); 128 mt x 32 nf tiles ((mt, nf) in (1, 2/4/6), (2, 4/6)), K split over splitk = 1 / 2
-// slices (mt 2 only; slab + counters zeroed once, see gemm_xd_workspace_bytes), one workgroup
-// per tile and slice; N % (32 nf) == 0, K % (64 splitk) == 0, K / 64 / splitk > ring depth.
+// XCD-partitioned decode GEMM (gemm_xd.hip): c[M,N] = epi(a[M,K] . b[N,K]^T); epi 0 store, 1 + r
+// (residual, may alias c), 2 / 3 SiLU / GELU gating of b = [gate; up] (2 N rows); 128 mt x 32 nf
+// tiles ((mt, nf) in (1, 2/4/6), (2, 4/6); gated: 16 nf output columns, nf even), K split over
+// splitk = 1..8 slices (splitk > 1: slab + counters zeroed once, gemm_xd_workspace_bytes), one
+// workgroup per tile and slice; N % tile columns == 0, K % 64 == 0, K / 64 / splitk > ring.
 int launch_gemm_xd(void* c, const void* a, const void* b, const void* r, int M, int N, int K,
                    int lda, int ldb, int ldc, int ldr, int epi, int mt, int nf, int splitk,
                    void* slab, int64_t slab_bytes, int* counters, int n_counters,
                    hipStream_t st);
-int64_t gemm_xd_workspace_bytes(int M, int N, int mt, int nf, int splitk);
+int64_t gemm_xd_workspace_bytes(int M, int N, int mt, int nf, int splitk, int glu);
 int configure_gemm_xd();
 
 // Raise the dynamic-LDS ceiling of the kernels that need > 64 KiB (head_dim

@@ -44,9 +44,9 @@ from ._ext import check, hipk, on_gpu, ptr, stream_ptr
 TUNED_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tuned")
 _lock = threading.Lock()
 # (M, N, K, ldx) -> (hipBLASLt solution index or -1, skinny-kernel variant or 0,
-#                   medium-M kernel K splits or 0, gemm_xd form or 0): the decode buckets of
-#                   the tuning table
-_table: dict[tuple[int, int, int, int], tuple[int, int, int, int]] | None = None
+#                   medium-M kernel K splits or 0, gemm_xd form or 0, gemm_xd gated form for
+#                   a [gate; up] weight or 0): the decode buckets of the tuning table
+_table: dict[tuple[int, int, int, int], tuple[int, int, int, int, int]] | None = None
 # (N, K, ldx) -> sorted [(tuned M, algo, beats F.linear, beats addmm_)]: prefill entries
 _prefill: dict[tuple[int, int, int], list[tuple[int, int, bool, bool]]] = {}
 # (M, N, K, ldx, beta) -> algo chosen for a prefill-sized call (-1: torch's path)
@@ -89,7 +89,7 @@ def _activate() -> dict:
     with _lock:
         if _table is not None:
             return _table
-        tab: dict[tuple[int, int, int, int], tuple[int, int, int, int]] = {}
+        tab: dict[tuple[int, int, int, int], tuple[int, int, int, int, int]] = {}
         pre: dict[tuple[int, int, int], list[tuple[int, int, bool, bool]]] = {}
         if _enabled and torch.cuda.is_available():
             ver = str(hipk().lt_version())
@@ -102,7 +102,8 @@ def _activate() -> dict:
                     continue
                 tab[(M, N, K, ldx)] = (int(e.get("algo", -1)), int(e.get("skinny", 0)),
                                        int(e.get("midm", 0)) if _midm_enabled else 0,
-                                       int(e.get("xd", 0)) if _xd_enabled else 0)
+                                       int(e.get("xd", 0)) if _xd_enabled else 0,
+                                       int(e.get("xd_glu", 0)) if _xd_enabled else 0)
         for v in pre.values():
             v.sort()
         _prefill.clear()
@@ -129,7 +130,7 @@ def set_enabled(on: bool) -> None:
 
 # ------------------------------------------------------------------ routing
 def _decode_entry(M: int, N: int, K: int,
-                  ldx: int) -> tuple[int, tuple[int, int, int, int]] | None:
+                  ldx: int) -> tuple[int, tuple[int, int, int, int, int]] | None:
     """(tuned bucket, entry) for a decode-sized shape, None for torch's (hipBLASLt heuristic)
     path.  The tuner measured every (model shape, DECODE_BUCKETS M) and kept an entry only
     where something beat the heuristic pick, so a bucket without an entry means "the
@@ -186,7 +187,7 @@ def _resolve(M: int, N: int, K: int, ldx: int) -> tuple[str, int]:
     if found is None:
         v = skinny_variant(M, N, K, ldx)
         return ("skinny", v) if v else ("torch", 0)
-    _, (algo, sk, midm, xd) = found
+    _, (algo, sk, midm, xd, _) = found
     if sk and M <= SKINNY_MAX_M and skinny_supports(sk, M, N, K, ldx):
         return ("skinny", sk)
     if xd and xd_supported(M, N, K, xd):
@@ -561,10 +562,22 @@ def w4_glu_ok(x: torch.Tensor, w: torch.Tensor, act: str) -> bool:
             and _aligned(x, w))
 
 
+def glu_form(M: int, N2: int, K: int, ldx: int) -> int:
+    """gemm_xd gated form the tuning table measured fastest for a decode batch M through the
+    [gate; up] weight [N2, K] (bucket-above for an off-bucket M), 0 if none."""
+    if not (_xd_enabled and _enabled) or M > DECODE_MAX_M:
+        return 0
+    found = _decode_entry(M, N2, K, ldx)
+    form = found[1][4] if found is not None else 0
+    return form if form and xd_supported(M, N2 // 2, K, form, glu=True) else 0
+
+
 def norm_glu(p, w: torch.Tensor, act: str = "silu") -> torch.Tensor:
     """h = act(norm(x) @ gate^T) * (norm(x) @ up^T) for an ``ops.PendingNorm`` p and the fused
     [gate; up] weight: on the 4-wave hand GEMM with the GLU in its epilogue when
-    ``w4_glu_ok`` (one launch, no [M, 2I] intermediate), else norm_linear + act_glu."""
+    ``w4_glu_ok`` (one launch, no [M, 2I] intermediate); at the decode batches where the
+    tuner measured it faster, gemm_xd with the GLU in its epilogue; else norm_linear +
+    act_glu."""
     from .activation import act_glu
 
     if w4_glu_ok(p.x, w, act):
@@ -572,59 +585,79 @@ def norm_glu(p, w: torch.Tensor, act: str = "silu") -> torch.Tensor:
         M, K = x.shape
         return mfma_gemm(x, w, act, variant=_w4v(K),
                          group_m=w4_group_m(M, w.shape[0] // 2, K, glu=True))
+    x = p.x
+    if (act in ("silu", "gelu_tanh") and isinstance(x, torch.Tensor) and _gpu_bf16(x, w)
+            and w.shape[1] == x.shape[1] and _aligned(x, w)):
+        form = glu_form(x.shape[0], w.shape[0], x.shape[1], x.shape[1])  # normed x: dense
+        if form:
+            xm = p.materialize()
+            return xd_gemm(xm, w, act, form=form)
     return act_glu(norm_linear(p, w), act)
 
 
 # ------------------------------------------------------------------ XCD-partitioned decode GEMM
-XD_EPI = {"store": 0, "residual": 1}
-# forms built in gemm_xd.hip, as mt * 100 + nf * 10 + splitk (128 mt x 32 nf tiles, K split
-# over splitk slices) -> LDS ring depth
-XD_FORMS = {121: 4, 141: 4, 161: 3, 241: 3, 261: 2, 242: 3, 262: 2}
+XD_EPI = {"store": 0, "residual": 1, "silu": 2, "gelu_tanh": 3}
+# tile shapes built in gemm_xd.hip, (mt, nf) -> LDS ring depth (128 mt x 32 nf tiles); a form
+# is mt * 100 + nf * 10 + splitk (K split over 1..8 slices)
+XD_TILES = {(1, 2): 4, (1, 4): 4, (1, 6): 3, (2, 4): 3, (2, 6): 2}
+XD_MAX_SPLITK = 8
+# the forms the tuner (scripts/tune_xd.py) measures
+XD_FORMS = tuple(sorted([mt * 100 + nf * 10 + 1 for mt, nf in XD_TILES] +
+                        [200 + nf * 10 + sk for nf in (4, 6) for sk in (2, 3, 4)]))
 
 
 def xd_form(form: int) -> tuple[int, int, int]:
     return form // 100, form // 10 % 10, form % 10
 
 
-def xd_supported(M: int, N: int, K: int, form: int) -> bool:
-    """Shapes gemm_xd.hip takes in ``form`` (mt * 100 + nf * 10 + splitk)."""
-    if form not in XD_FORMS:
-        return False
+def xd_supported(M: int, N: int, K: int, form: int, glu: bool = False) -> bool:
+    """Shapes gemm_xd.hip takes in ``form`` (mt * 100 + nf * 10 + splitk); N = output
+    columns (gated: half the rows of the [gate; up] weight)."""
     mt, nf, sk = xd_form(form)
-    return (M >= 1 and N % (32 * nf) == 0 and K % (64 * sk) == 0
-            and K // 64 // sk > XD_FORMS[form])
+    if (mt, nf) not in XD_TILES or not 1 <= sk <= XD_MAX_SPLITK or (glu and nf % 2):
+        return False
+    tno = 16 * nf if glu else 32 * nf
+    if not (M >= 1 and N % tno == 0 and K % 64 == 0 and K // 64 // sk > XD_TILES[(mt, nf)]):
+        return False
+    # split-K: the partial slots and tile counters fit the device workspace
+    tiles = -(-M // (128 * mt)) * (N // tno)
+    return sk == 1 or (tiles * (sk - 1) * (128 * mt) * (32 * nf) * 4 <= WS_SLAB_BYTES
+                       and 2 * tiles + 1 <= WS_COUNTERS)
 
 
-def xd_default_form(M: int, N: int, K: int) -> int:
-    """Form of an untuned shape: the fewest operand bytes per CU among the forms whose work
-    items fill whole rounds of the 256 CUs best (o / down at M = 1024: 256-row tiles with
-    split-K 2; qkv N = 6144: 256 x 192 with split-K 2)."""
-    best, key = 0, None
+def xd_default_form(M: int, N: int, K: int, glu: bool = False) -> int:
+    """Form of an untuned shape, by a per-CU operand-bytes model (profiles/r4i): a CU's
+    time ~ (tile rows + columns) x (K / splitk) x 2 B per round of 256 work items, plus the
+    split-K combine (its fp32 partials, weighted 5x: measured far costlier than their bytes)."""
+    best, cost = 0, None
     for form in XD_FORMS:
-        if not xd_supported(M, N, K, form):
+        if not xd_supported(M, N, K, form, glu):
             continue
         mt, nf, sk = xd_form(form)
-        items = -(-M // (128 * mt)) * (N // (32 * nf)) * sk
-        fill = items / (-(-items // 256) * 256)
+        tno = 16 * nf if glu else 32 * nf
+        items = -(-M // (128 * mt)) * (N // tno) * sk
         rounds = -(-items // 256)
-        per_cu = rounds * (128 * mt + 32 * nf) * (K // sk)  # operand elements per CU
-        k = (round(fill, 3), -per_cu)
-        if key is None or k > key:
-            best, key = form, k
+        c = rounds * ((128 * mt + 32 * nf) * (K // sk) * 2 + 100_000
+                      + 5 * (sk - 1) * (128 * mt) * (32 * nf) * 4)
+        if cost is None or c < cost:
+            best, cost = form, c
     return best
 
 
 def xd_gemm(x: torch.Tensor, w: torch.Tensor, epi: str = "store",
             residual: torch.Tensor | None = None, out: torch.Tensor | None = None,
             form: int = 0, ws: tuple[torch.Tensor, torch.Tensor] | None = None) -> torch.Tensor:
-    """Decode-shaped hand GEMM, csrc/kernels/gemm_xd.hip: y = x @ w.T (+ residual; ``out``
-    may be ``residual``) on 128 mt x 32 nf tiles, K split over 1 or 2 slices, with the tile
-    order partitioned by XCD (each XCD streams its own weight column panels through its L2
-    for every row tile).  ``form`` = mt * 100 + nf * 10 + splitk (0: ``xd_default_form``)."""
+    """Decode-shaped hand GEMM, csrc/kernels/gemm_xd.hip: y = epi(x @ w.T) on 128 mt x 32 nf
+    tiles, K split over 1..8 slices, with the tile order partitioned by XCD (each XCD streams
+    its own weight column panels through its L2 for every row tile).  epi "store";
+    "residual" (``out`` may be ``residual``); "silu" / "gelu_tanh": w is the fused [gate; up]
+    weight [2I, K] and y[:, n] = act(x . gate_n) * (x . up_n).  ``form`` = mt * 100 +
+    nf * 10 + splitk (0: ``xd_default_form``)."""
     M, K = x.shape
-    N = w.shape[0]
-    form = form or xd_default_form(M, N, K)
-    assert xd_supported(M, N, K, form), (M, N, K, form)
+    glu = epi in ("silu", "gelu_tanh")
+    N = w.shape[0] // 2 if glu else w.shape[0]
+    form = form or xd_default_form(M, N, K, glu)
+    assert xd_supported(M, N, K, form, glu), (M, N, K, form, epi)
     assert x.dtype == w.dtype == torch.bfloat16 and x.stride(1) == 1 and w.is_contiguous()
     mt, nf, sk = xd_form(form)
     if out is None:

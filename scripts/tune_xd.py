@@ -2,7 +2,8 @@
 """Measure the XCD-partitioned decode GEMM (csrc/kernels/gemm_xd.hip) against the engine's
 path without it (ops.linear: tuned hipBLASLt / midm / F.linear) for every decode projection
 of a model at the larger decode buckets, and write a tuning entry {"xd": form} where the hand
-kernel wins by at least --min-gain.
+kernel wins by at least --min-gain; for gate_up below the fused-GLU gemm_w4 batches also the
+GLU epilogue form against the route + act_glu ({"xd_glu": form}).
 
 W is rotated over copies (>= 512 MB in all) so it streams from HBM, as in a decode step;
 arms are interleaved (time_arm of tune_midm.py).
@@ -27,6 +28,37 @@ from tune_midm import time_arm  # noqa: E402
 BUCKETS = (128, 160, 192, 224, 256, 320, 384, 448, 512, 640, 768, 896, 1024)
 
 
+def measure(G, x, ws, N, K, epi, base_fn, name, model, tp, M):
+    """Time the engine's current route (base_fn) and every gemm_xd form for one shape
+    (epi "store" or a GLU: N = output columns); print and return the record."""
+    glu = epi != "store"
+    forms = [f for f in G.XD_FORMS if G.xd_supported(M, N, K, f, glu)]
+    if not forms:
+        return None
+    base = time_arm(base_fn, ws)
+    y = x.float() @ ws[0].float().t()
+    if glu:
+        y = torch.nn.functional.silu(y[:, :N]) * y[:, N:]
+    best = None
+    for f in forms:
+        got = G.xd_gemm(x, ws[0], epi, form=f)
+        err = ((got.float() - y).abs().max() / y.abs().max()).item()
+        if err > 2e-2:
+            print(json.dumps({"model": model, "tp": tp, "gemm": name, "epi": epi, "M": M,
+                              "form": f, "err": err, "FAILED": True}), flush=True)
+            continue
+        us = time_arm(lambda w, f=f: G.xd_gemm(x, w, epi, form=f), ws)
+        if best is None or us < best[1]:
+            best = (f, us)
+    del y
+    rec = {"model": model, "tp": int(tp), "gemm": name, "epi": epi, "M": M, "N": N, "K": K,
+           "base": G.route(M, N * (2 if glu else 1), K, K)[0], "base_us": round(base, 1)}
+    if best is not None:
+        rec.update(xd_form=best[0], xd_us=round(best[1], 1), gain=round(base / best[1] - 1, 3))
+    print(json.dumps(rec), flush=True)
+    return rec if best is not None else None
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--configs", default="llama-3-8b:1,gemma-2b:1,llama-3-70b:1,llama-3-70b:8")
@@ -34,6 +66,7 @@ def main() -> None:
     ap.add_argument("--min-gain", type=float, default=0.03)
     ap.add_argument("--out", default="gpurun_out/xd_tuned.json")
     a = ap.parse_args()
+    from drtc_amd import ops
     from drtc_amd.ops import gemm as G
     from drtc_amd.ops._ext import hipk
 
@@ -54,36 +87,24 @@ def main() -> None:
             ws = [(torch.randn(N, K, device=dev, generator=g) * 0.02).to(torch.bfloat16)
                   for _ in range(ncopy)]
             for M in (int(m) for m in a.ms.split(",")):
-                forms = [f for f in G.XD_FORMS if G.xd_supported(M, N, K, f)]
-                if not forms:
-                    continue
                 x = torch.randn(M, K, device=dev, generator=g).to(torch.bfloat16)
-                base = time_arm(lambda w: G.linear(x, w), ws)
-                kind = G.route(M, N, K, K)[0]
-                ref = x.float() @ ws[0].float().t()
-                best = None
-                for nf in forms:
-                    y = G.xd_gemm(x, ws[0], form=nf)
-                    err = ((y.float() - ref).abs().max() / ref.abs().max()).item()
-                    if err > 2e-2:
-                        print(json.dumps({"model": model, "tp": tp, "gemm": name, "M": M,
-                                          "form": nf, "err": err, "FAILED": True}), flush=True)
-                        continue
-                    us = time_arm(lambda w, nf=nf: G.xd_gemm(x, w, form=nf), ws)
-                    if best is None or us < best[1]:
-                        best = (nf, us)
-                rec = {"model": model, "tp": int(tp), "gemm": name, "M": M, "N": N, "K": K,
-                       "base": kind, "base_us": round(base, 1)}
-                if best is not None:
-                    rec.update(xd_form=best[0], xd_us=round(best[1], 1),
-                               gain=round(base / best[1] - 1, 3))
-                    if best[1] < base * (1 - a.min_gain):
-                        out[ver][f"{M},{N},{K},{K}"] = {
-                            "xd": best[0], "xd_us": round(best[1], 1),
-                            "xd_base_us": round(base, 1), "gemm": name, "model": model,
-                            "tp": int(tp)}
-                print(json.dumps(rec), flush=True)
-                del ref
+                key = f"{M},{N},{K},{K}"
+                ent = {}
+                # plain projection (ops.linear) against the engine's route without gemm_xd
+                rec = measure(G, x, ws, N, K, "store", lambda w: G.linear(x, w), name, model, tp, M)
+                if rec and rec["xd_us"] < rec["base_us"] * (1 - a.min_gain):
+                    ent.update(xd=rec["xd_form"], xd_us=rec["xd_us"], xd_base_us=rec["base_us"])
+                # gate_up with the GLU in the epilogue, below the fused-GLU gemm_w4 batches:
+                # against norm_linear's route + act_glu
+                if name == "gate_up" and M < G.W4_GLU_MIN_M:
+                    act = "silu"
+                    rec = measure(G, x, ws, N // 2, K, act,
+                                  lambda w: ops.act_glu(G.linear(x, w), act), name, model, tp, M)
+                    if rec and rec["xd_us"] < rec["base_us"] * (1 - a.min_gain):
+                        ent.update(xd_glu=rec["xd_form"], xd_glu_us=rec["xd_us"],
+                                   xd_glu_base_us=rec["base_us"])
+                if ent:
+                    out[ver][key] = {**ent, "gemm": name, "model": model, "tp": int(tp)}
             del ws
             torch.cuda.empty_cache()
     os.makedirs(os.path.dirname(a.out), exist_ok=True)

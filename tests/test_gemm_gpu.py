@@ -336,11 +336,37 @@ def test_xd_gemm_matches_fp32(hipk, epi, form, M, N, K):
     out = G.xd_gemm(x, w, epi, residual=res, form=form)
     torch.cuda.synchronize()
     _check(out, ref)
-    if form % 10 == 2:  # split-K: counters re-armed, a second call gives the same bits
+    if form % 10 > 1:  # split-K: counters re-armed, a second call gives the same bits
         out2 = G.xd_gemm(x, w, epi, residual=res, form=form)
         torch.cuda.synchronize()
         assert torch.equal(out, out2)
-        assert int(G.gemm_workspace(x.device)[1][:2 * 64 + 1].abs().sum()) == 0
+        assert int(G.gemm_workspace(x.device)[1][:2 * 256 + 1].abs().sum()) == 0
+
+
+@pytest.mark.parametrize("act", ["silu", "gelu_tanh"])
+@pytest.mark.parametrize("form", [121, 141, 161, 241, 242, 243, 261, 264])
+@pytest.mark.parametrize("M,I,K", [(256, 1536, 1024), (200, 768, 1600), (1024, 384, 832)])
+def test_xd_gemm_glu_matches_fp32(hipk, act, form, M, I, K):
+    if not G.xd_supported(M, I, K, form, glu=True):
+        pytest.skip("shape outside the form's tile grid")
+    g = torch.Generator(device="cuda").manual_seed(M + I + K + form)
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16, generator=g)
+    w = torch.randn(2 * I, K, device="cuda", dtype=torch.bfloat16, generator=g) * 0.05
+    out = G.xd_gemm(x, w, act, form=form)
+    torch.cuda.synchronize()
+    _check(out, _ref(x, w, act, None))
+
+
+@pytest.mark.parametrize("form", [143, 145, 247, 268])
+def test_xd_gemm_uneven_splitk(hipk, form):
+    """K tiles that the slices do not divide evenly (K / 64 = 61 over 3, 5, 7, 8 slices)."""
+    M, N, K = 384, 768, 61 * 64
+    g = torch.Generator(device="cuda").manual_seed(form)
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16, generator=g)
+    w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16, generator=g) * 0.05
+    out = G.xd_gemm(x, w, form=form)
+    torch.cuda.synchronize()
+    _check(out, _ref(x, w, "store", None))
 
 
 @pytest.mark.parametrize("form", [141, 242])
@@ -383,7 +409,33 @@ def test_xd_gemm_rejects_bad_shapes(hipk):
                             cnt.numel() if cnt is not None else 0, 0)
     assert call(64, 200, 512, nf=2) == -1        # N not a multiple of the tile width
     assert call(64, 256, 512, nf=3) == -1        # no such form
-    assert call(64, 256, 512, mt=1, sk=2) == -1  # split-K is a 256-row form
+    assert call(64, 256, 512, sk=9) == -1        # at most 8 slices
+    assert call(64, 40, 512, epi=2, nf=2) == -1  # gated: N not a multiple of 16 nf
     assert call(64, 256, 256, nf=4) == -1        # K / 64 must exceed the ring depth (4)
     assert call(64, 256, 512, epi=1, nf=2) == -1  # residual epilogue without a residual
     assert call(256, 256, 1024, mt=2, nf=4, sk=2) == -2  # split-K without a workspace
+
+
+def test_norm_glu_takes_tuned_xd_form(hipk, monkeypatch):
+    """A decode batch whose table entry carries a gated gemm_xd form runs it through
+    ops.norm_glu (no act_glu pass) and matches the fp32 reference of norm + GLU."""
+    from drtc_amd import ops
+
+    M, I, K = 256, 1536, 1024
+    g = torch.Generator(device="cuda").manual_seed(3)
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16, generator=g)
+    nw = (1 + 0.1 * torch.randn(K, device="cuda", generator=g)).to(torch.bfloat16)
+    w = torch.randn(2 * I, K, device="cuda", dtype=torch.bfloat16, generator=g) * 0.05
+    G.reset()
+    tab = dict(G._activate())
+    tab[(M, 2 * I, K, K)] = (-1, 0, 0, 0, 242)
+    monkeypatch.setattr(G, "_table", tab)
+    calls = []
+    real = G.xd_gemm
+    monkeypatch.setattr(G, "xd_gemm", lambda *a, **k: calls.append(k.get("form")) or real(*a, **k))
+    out = ops.norm_glu(ops.PendingNorm(x, None, nw, 1e-5, False), w, "silu")
+    torch.cuda.synchronize()
+    assert calls == [242]
+    xn = ops.rmsnorm_ref(x, nw, 1e-5).to(torch.bfloat16)
+    _check(out, _ref(xn, w, "silu", None))
+    G.reset()
