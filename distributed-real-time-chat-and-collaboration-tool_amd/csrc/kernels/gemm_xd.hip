@@ -30,11 +30,13 @@
 //     landed and every read of stage t done]; half 1 MFMAs | LDS-DMA of tile t + S into stage
 //     t + ds_read of tile t + 1 half 0.  The first K tile accumulates onto a zero C operand.
 //   * Split-K with a ticket-first combine: each slice draws a ticket when its K loop ends;
-//     tickets 0 .. splitk - 2 write their fp32 tile to their slab slot (write-through sc1
-//     stores, drained, barrier) and count themselves ready; the last ticket (resident, and
+//     tickets 0 .. splitk - 2 write their fp32 tile to their slice's slab slot (write-through
+//     sc1 stores, drained, barrier) and count themselves ready; the last ticket (resident, and
 //     waiting only for slices that already hold a ticket: no wait on an unscheduled
-//     workgroup) polls the ready count (bounded), adds the partials (sc1 loads) inside its
-//     epilogue and re-arms both counters.  cdna_hip_programming.md §6 G16 hand-off recipe.
+//     workgroup) polls the ready count (bounded), sums the slices in slice order (its own
+//     accumulators at its own position: bitwise deterministic whatever the arrival order;
+//     sc1 loads) inside its epilogue and re-arms both counters.  cdna_hip_programming.md §6
+//     G16 hand-off recipe.
 //   * Epilogue through LDS (the wave's tile as bf16, then 16-B row-contiguous global stores):
 //     store, + residual (may alias c), or SiLU / tanh-GELU gating of a [gate; up] weight:
 //     each wave's B rows hold the gate rows (fragments j < NF / 2) and the up rows (j >= NF /
@@ -240,10 +242,10 @@ DRTC_DEVICE void xd_tail(f32x4 (&acc)[C::FA][C::NF], bf16x8 (&fa0)[C::FA], bf16x
 
 // Split-K, ticket-first combine (see the file comment).  Counters of tile t: [2 t] ticket,
 // [2 t + 1] ready count; [2 tiles] the error word (a partial that never arrived).  The slab
-// holds splitk - 1 partial slots per tile.  Returns false for a slice that published its
-// partial (it is done), true for the last ticket, which adds the partials inside the
-// epilogue (xd_partial: one fragment at a time, so the accumulators stay in place) and
-// re-arms the counters.
+// holds one partial slot per slice and tile.  Returns false for a slice that published its
+// partial (it is done), true for the last ticket, which sums the slices inside the epilogue
+// (xd_sum: one fragment at a time, so the accumulators stay in place) and re-arms the
+// counters.
 template <class C>
 constexpr int xd_tile_bytes() { return C::FA * C::NF * kXdThreads * 16; }
 constexpr int kXdSc1 = 16;  // cache-policy bits of the buffer op: sc1 (write-through)
@@ -252,12 +254,13 @@ template <class C>
 DRTC_DEVICE __amdgpu_buffer_rsrc_t xd_slab(const XdParams& p, int tile) {
   const int64_t slot = (int64_t)xd_tile_bytes<C>();
   return __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(reinterpret_cast<char*>(p.slab) + (int64_t)tile * (p.splitk - 1) * slot), (short)0,
-      (int)((p.splitk - 1) * slot), 0x00020000);
+      (void*)(reinterpret_cast<char*>(p.slab) + (int64_t)tile * p.splitk * slot), (short)0,
+      (int)(p.splitk * slot), 0x00020000);
 }
 
 template <class C>
-DRTC_DEVICE bool xd_combine(const XdParams& p, f32x4 (&acc)[C::FA][C::NF], int tile, char* lds) {
+DRTC_DEVICE bool xd_combine(const XdParams& p, f32x4 (&acc)[C::FA][C::NF], int tile, int slice,
+                            char* lds) {
   const __amdgpu_buffer_rsrc_t slab = xd_slab<C>(p, tile);
   int* ticket = p.counters + 2 * tile;
   int* ready = ticket + 1;
@@ -269,8 +272,9 @@ DRTC_DEVICE bool xd_combine(const XdParams& p, f32x4 (&acc)[C::FA][C::NF], int t
   __syncthreads();
   const int t = *flag;
   if (t < p.splitk - 1) {
-    // publish the partial in slot t, fragment order (16 B per lane, coalesced), then count
-    const int base = t * xd_tile_bytes<C>();
+    // publish the partial in this slice's slot, fragment order (16 B per lane, coalesced),
+    // then count it ready
+    const int base = slice * xd_tile_bytes<C>();
 #pragma unroll
     for (int i = 0; i < C::FA; ++i)
 #pragma unroll
@@ -299,14 +303,19 @@ DRTC_DEVICE bool xd_combine(const XdParams& p, f32x4 (&acc)[C::FA][C::NF], int t
   return true;
 }
 
-// Fragment (i, j) of every published partial of the tile, summed in slot order.
+// Fragment (i, j) of the tile summed over the slices in slice order; `own` (this workgroup's
+// accumulators) stands in for its own slice.
 template <class C>
-DRTC_DEVICE f32x4 xd_partial(const XdParams& p, const __amdgpu_buffer_rsrc_t& slab, int i, int j) {
+DRTC_DEVICE f32x4 xd_sum(const XdParams& p, const __amdgpu_buffer_rsrc_t& slab, int i, int j,
+                         int slice, f32x4 own) {
   const int off = ((i * C::NF + j) * kXdThreads + (int)threadIdx.x) * 16;
-  f32x4 v = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(slab, off, 0, kXdSc1));
-  for (int t = 1; t < p.splitk - 1; ++t)
-    v += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                       slab, off + t * xd_tile_bytes<C>(), 0, kXdSc1));
+  f32x4 v = own;
+  if (slice != 0)
+    v = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(slab, off, 0, kXdSc1));
+  for (int s = 1; s < p.splitk; ++s)
+    v += s == slice ? own
+                    : __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                    slab, off + s * xd_tile_bytes<C>(), 0, kXdSc1));
   return v;
 }
 
@@ -410,7 +419,7 @@ __global__ __launch_bounds__(kXdThreads, 1) void gemm_xd_kernel(XdParams p) {
 
   bool part = false;  // split-K: this workgroup adds the other slices' partials
   if constexpr (C::SPLIT) {
-    if (!xd_combine<C>(p, acc, tile, xd_lds)) return;
+    if (!xd_combine<C>(p, acc, tile, slice, xd_lds)) return;
     part = true;
   }
 
@@ -429,8 +438,8 @@ __global__ __launch_bounds__(kXdThreads, 1) void gemm_xd_kernel(XdParams p) {
       for (int j = 0; j < NF / 2; ++j) {
         f32x4 gv = acc[i][j], uv = acc[i][j + NF / 2];
         if (C::SPLIT && part) {
-          gv += xd_partial<C>(p, slab, i, j);
-          uv += xd_partial<C>(p, slab, i, j + NF / 2);
+          gv = xd_sum<C>(p, slab, i, j, slice, gv);
+          uv = xd_sum<C>(p, slab, i, j + NF / 2, slice, uv);
         }
 #pragma unroll
         for (int r = 0; r < 4; ++r)
@@ -441,7 +450,7 @@ __global__ __launch_bounds__(kXdThreads, 1) void gemm_xd_kernel(XdParams p) {
 #pragma unroll
       for (int j = 0; j < NF; ++j) {
         f32x4 v = acc[i][j];
-        if (C::SPLIT && part) v += xd_partial<C>(p, slab, i, j);
+        if (C::SPLIT && part) v = xd_sum<C>(p, slab, i, j, slice, v);
 #pragma unroll
         for (int r = 0; r < 4; ++r)
           *reinterpret_cast<bf16_t*>(ep + (16 * i + 4 * g + r) * PITCH + (16 * j + l16) * 2) =
@@ -538,7 +547,7 @@ int64_t gemm_xd_workspace_bytes(int M, int N, int mt, int nf, int splitk, int gl
   if (splitk < 2 || mt < 1 || nf < 1) return 0;
   const int tno = glu ? 16 * nf : 32 * nf;
   const int64_t tiles = (int64_t)((M + 128 * mt - 1) / (128 * mt)) * (N / tno);
-  return tiles * (splitk - 1) * (128 * mt) * (32 * nf) * 4;
+  return tiles * splitk * (128 * mt) * (32 * nf) * 4;
 }
 
 int launch_gemm_xd(void* c, const void* a, const void* b, const void* r, int M, int N, int K,

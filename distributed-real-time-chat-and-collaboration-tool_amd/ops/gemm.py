@@ -621,7 +621,7 @@ def xd_supported(M: int, N: int, K: int, form: int, glu: bool = False) -> bool:
         return False
     # split-K: the partial slots and tile counters fit the device workspace
     tiles = -(-M // (128 * mt)) * (N // tno)
-    return sk == 1 or (tiles * (sk - 1) * (128 * mt) * (32 * nf) * 4 <= WS_SLAB_BYTES
+    return sk == 1 or (tiles * sk * (128 * mt) * (32 * nf) * 4 <= WS_SLAB_BYTES
                        and 2 * tiles + 1 <= WS_COUNTERS)
 
 
