@@ -614,7 +614,7 @@ def test_tuned_linear(hipk, M, N, K):
     ref = x.float() @ w.float().t()
     saved = gemm._table
     try:
-        gemm._table = {(M, N, K, K): (r["algo"], 0, 0)}
+        gemm._table = {(M, N, K, K): (r["algo"], 0, 0, 0, 0)}
         y = ops.linear(x, w)
         _close(y, ref, 2e-2, 2e-2, "tuned linear")
         g = torch.cuda.CUDAGraph()
@@ -716,7 +716,7 @@ def test_skinny_norm_gemm(hipk, M, K, resid, gemma):
     saved, saved_max = gemm._table, gemm.NORM_FUSE_MAX_M
     try:
         gemm.NORM_FUSE_MAX_M = 4  # the kernel covers M <= 4; the engine fuses at M = 1
-        gemm._table = {(M, N, K, K): (-1, 1, 0)}  # measured pick: dot2 kernel
+        gemm._table = {(M, N, K, K): (-1, 1, 0, 0, 0)}  # measured pick: dot2 kernel
         p = ops.PendingNorm(x, res.clone() if resid else None, nw, 1e-5, gemma)
         y = ops.norm_linear(p, w)
         torch.cuda.synchronize()
@@ -724,7 +724,7 @@ def test_skinny_norm_gemm(hipk, M, K, resid, gemma):
         assert torch.equal(p.stream(), h_ref)
         _close(y, y_ref, 3e-2, 2e-2, "norm gemm")
         # unfused path gives the same stream and (within rounding) the same y
-        gemm._table = {(M, N, K, K): (-1, 0, 0)}
+        gemm._table = {(M, N, K, K): (-1, 0, 0, 0, 0)}
         q = ops.PendingNorm(x, res.clone() if resid else None, nw, 1e-5, gemma)
         y2 = ops.norm_linear(q, w)
         assert q._out is not None
@@ -752,7 +752,7 @@ def test_skinny_glu_gemm(hipk, M, I, act):
     saved, saved_max = gemm._table, gemm.GLU_FUSE_MAX_M
     try:
         gemm.GLU_FUSE_MAX_M = 2
-        gemm._table = {(M, N, I, I): (-1, 1, 0)}
+        gemm._table = {(M, N, I, I): (-1, 1, 0, 0, 0)}
         y = ops.glu_linear(gu, w, act)
         _close(y, y_ref, 2e-2, 2e-2, "glu gemm")
         y_unfused = gemm.skinny_linear(a, w, 1)
