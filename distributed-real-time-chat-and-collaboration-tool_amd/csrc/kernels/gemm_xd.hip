@@ -68,10 +68,11 @@ struct XdCfg {
   static constexpr int NR = FA + NF;               // fragment reads per wave per K half
   static constexpr int BOFF = TM * 128;            // B region within a stage
   static constexpr int STAGE = BOFF + TN * 128;
-  static constexpr int LDS = S * STAGE;
+  static constexpr int LDS = S * STAGE;            // the K-tile ring
   static constexpr int PITCH = 32 * NF + 16;       // epilogue bytes per wave-tile row (padded)
-  static_assert(4 * 64 * MT * PITCH <= LDS, "epilogue image must fit the stages");
-  static_assert(LDS <= 160 * 1024, "LDS ring exceeds the CU's 160 KiB");
+  static constexpr int IMAGE = 4 * 64 * MT * PITCH;  // the epilogue's bf16 tile image
+  static constexpr int ALLOC = LDS > IMAGE ? LDS : IMAGE;
+  static_assert(ALLOC <= 160 * 1024, "LDS exceeds the CU's 160 KiB");
   static_assert(NR < H, "half-0 fragment reads must fit the half");
 };
 
@@ -484,8 +485,8 @@ __global__ __launch_bounds__(kXdThreads, 1) void gemm_xd_kernel(XdParams p) {
 
 template <class C, int EPI>
 int xd_launch_e(const XdParams& p, hipStream_t st) {
-  hipLaunchKernelGGL((gemm_xd_kernel<C, EPI>), dim3(8 * p.per_xcd), dim3(kXdThreads), (C::LDS),
-                     st, p);
+  hipLaunchKernelGGL((gemm_xd_kernel<C, EPI>), dim3(8 * p.per_xcd), dim3(kXdThreads),
+                     (C::ALLOC), st, p);
   return (int)hipGetLastError();
 }
 
@@ -506,12 +507,12 @@ int xd_cfg() {
                         (const void*)gemm_xd_kernel<C, XD_RESIDUAL>,
                         (const void*)gemm_xd_kernel<C, XD_SILU>,
                         (const void*)gemm_xd_kernel<C, XD_GELU>})
-    e |= (int)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
+    e |= (int)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, C::ALLOC);
   return e;
 }
 
 // Forms built (mt, nf) -> ring depth: 128-row tiles nf 2 / 4 / 6 (4 / 4 / 3 stages), 256-row
-// tiles nf 4 / 6 (3 / 2 stages); each with and without the split-K combine.
+// tiles nf 4 / 6 / 8 (3 / 2 / 2 stages); each with and without the split-K combine.
 template <bool SP>
 using Xd1x2 = XdCfg<1, 2, 4, SP>;
 template <bool SP>
@@ -522,10 +523,12 @@ template <bool SP>
 using Xd2x4 = XdCfg<2, 4, 3, SP>;
 template <bool SP>
 using Xd2x6 = XdCfg<2, 6, 2, SP>;
+template <bool SP>
+using Xd2x8 = XdCfg<2, 8, 2, SP>;
 
 int xd_stages(int mt, int nf) {
   if (mt == 1) return nf == 6 ? 3 : (nf == 2 || nf == 4 ? 4 : 0);
-  if (mt == 2) return nf == 4 ? 3 : (nf == 6 ? 2 : 0);
+  if (mt == 2) return nf == 4 ? 3 : (nf == 6 || nf == 8 ? 2 : 0);
   return 0;
 }
 
@@ -537,6 +540,7 @@ int xd_dispatch(const XdParams& p, int mt, int nf, int epi, hipStream_t st) {
     case 16: return xd_launch<Xd1x6<SP>>(p, epi, st);
     case 24: return xd_launch<Xd2x4<SP>>(p, epi, st);
     case 26: return xd_launch<Xd2x6<SP>>(p, epi, st);
+    case 28: return xd_launch<Xd2x8<SP>>(p, epi, st);
     default: return -1;
   }
 }
@@ -597,7 +601,7 @@ int configure_gemm_xd() {
   return xd_cfg<Xd1x2<false>>() | xd_cfg<Xd1x4<false>>() | xd_cfg<Xd1x6<false>>() |
          xd_cfg<Xd2x4<false>>() | xd_cfg<Xd2x6<false>>() | xd_cfg<Xd1x2<true>>() |
          xd_cfg<Xd1x4<true>>() | xd_cfg<Xd1x6<true>>() | xd_cfg<Xd2x4<true>>() |
-         xd_cfg<Xd2x6<true>>();
+         xd_cfg<Xd2x6<true>>() | xd_cfg<Xd2x8<false>>() | xd_cfg<Xd2x8<true>>();
 }
 
 }  // namespace drtc

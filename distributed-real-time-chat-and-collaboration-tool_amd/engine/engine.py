@@ -133,6 +133,15 @@ class LLMEngine:
         # trickling the ~max_batch/48 slots freed per step into every step;
         # the steps in between are pure, graph-replayed, pipelined decodes
         self.admit_group = int(os.environ.get("DRTC_ADMIT_GROUP", str(max(1, max_batch // 16))))
+        # arrival gathering for mixed steps (off unless admit_min_tokens > 0): while requests
+        # are decoding and new prompts are still arriving (last one < admit_gap_s ago), run
+        # pure decode steps until the queue holds admit_min_tokens prompt tokens, at most
+        # admit_max_delay_s after the oldest queued arrival - one GEMM-efficient mixed step
+        # per chunk instead of a small one per step (closed-loop clients return in bursts)
+        self.admit_min_tokens = int(os.environ.get("DRTC_ADMIT_MIN_TOKENS", "0"))
+        self.admit_gap_s = float(os.environ.get("DRTC_ADMIT_GAP_MS", "3")) / 1000.0
+        self.admit_max_delay_s = float(os.environ.get("DRTC_ADMIT_MAX_MS", "100")) / 1000.0
+        self._last_arrival = 0.0
 
     # ------------------------------------------------------------ API
     def add_request(self, req: Request) -> Request:
@@ -147,7 +156,20 @@ class LLMEngine:
             req.state = RequestState.WAITING
             self.waiting.append(req)
             self._waiting_tokens += n
+            self._last_arrival = time.perf_counter()
         return req
+
+    def _admit_ready(self) -> bool:
+        """Whether a mixed step may admit now (see ``admit_min_tokens``)."""
+        if self.admit_min_tokens <= 0 or self._waiting_tokens >= self.admit_min_tokens:
+            return True
+        if len(self.waiting) >= self.max_batch - len(self.running):
+            return True  # slot-bound: the queue fills every free slot already
+        now = time.perf_counter()
+        if now - self._last_arrival >= self.admit_gap_s:
+            return True  # arrivals paused: nothing more to gather
+        oldest = self.waiting[0].arrival_time if self.waiting else now
+        return now - oldest >= self.admit_max_delay_s
 
     def has_work(self) -> bool:
         return bool(self.running or self.waiting or self._inflight or self._aborts)
@@ -210,7 +232,14 @@ class LLMEngine:
             done = self._apply_aborts()
             self._record(done)
             return done
-        if self.mixed and (self.running or self._inflight is not None) and self._could_admit():
+        busy = self.running or self._inflight is not None
+        if self.mixed and busy and self._could_admit() and not self._admit_ready():
+            # gathering arrivals for one chunk-sized mixed step: decode meanwhile
+            with tracing.span("engine.decode", batch=len(self.running)):
+                done = self._run_decode()
+            self._record(done)
+            return done
+        if self.mixed and busy and self._could_admit():
             done = self._process_inflight() if self._inflight is not None else []
             with self.lock:
                 self._ensure_blocks()
@@ -273,6 +302,8 @@ class LLMEngine:
         if len(self.waiting) > self.max_batch - len(self.running):
             # slot-bound: a whole admission group (_could_admit) in one step
             return self.prefill_chunk_tokens
+        if self.admit_min_tokens > 0:  # gathered arrivals: admit them as one chunk
+            return max(self.mixed_tokens, min(self.prefill_chunk_tokens, self._waiting_tokens))
         return max(self.mixed_tokens, min(self.prefill_chunk_tokens, self._waiting_tokens // 4))
 
     def _admit(self, budget: int | None = None) -> list[Request]:

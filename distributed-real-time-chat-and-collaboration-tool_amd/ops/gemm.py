@@ -599,11 +599,11 @@ def norm_glu(p, w: torch.Tensor, act: str = "silu") -> torch.Tensor:
 XD_EPI = {"store": 0, "residual": 1, "silu": 2, "gelu_tanh": 3}
 # tile shapes built in gemm_xd.hip, (mt, nf) -> LDS ring depth (128 mt x 32 nf tiles); a form
 # is mt * 100 + nf * 10 + splitk (K split over 1..8 slices)
-XD_TILES = {(1, 2): 4, (1, 4): 4, (1, 6): 3, (2, 4): 3, (2, 6): 2}
+XD_TILES = {(1, 2): 4, (1, 4): 4, (1, 6): 3, (2, 4): 3, (2, 6): 2, (2, 8): 2}
 XD_MAX_SPLITK = 8
 # the forms the tuner (scripts/tune_xd.py) measures
 XD_FORMS = tuple(sorted([mt * 100 + nf * 10 + 1 for mt, nf in XD_TILES] +
-                        [200 + nf * 10 + sk for nf in (4, 6) for sk in (2, 3, 4)]))
+                        [200 + nf * 10 + sk for nf in (4, 6, 8) for sk in (2, 3, 4)]))
 
 
 def xd_form(form: int) -> tuple[int, int, int]:

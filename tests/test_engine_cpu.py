@@ -515,3 +515,35 @@ def test_engine_loop_burst_gathering():
         assert time.perf_counter() - t0 < 0.2
     finally:
         loop.stop()
+
+
+def test_mixed_admission_gathers_arrivals():
+    """Arrival gathering for mixed steps (DRTC_ADMIT_MIN_TOKENS): while prompts keep arriving
+    the engine decodes and holds them until a chunk's worth is queued, then admits them in ONE
+    mixed step; the tokens equal the prefill-first engine's; off by default."""
+    from drtc_amd.engine import Request
+
+    m = TransformerLM(TINY_LLAMA, "cpu", seed=5)
+    prompts = [list(range(1, 12 + 3 * i)) for i in range(6)]
+    params = [SamplingParams.greedy(12, ignore_eos=True) for _ in prompts]
+
+    def run(min_tokens: int, mixed: bool = True):
+        eng = LLMEngine(m, max_batch=8, max_model_len=256, num_blocks=64, use_graphs=False)
+        eng.mixed = mixed
+        assert eng.admit_min_tokens == 0
+        eng.admit_min_tokens, eng.admit_gap_s, eng.admit_max_delay_s = min_tokens, 10.0, 10.0
+        reqs = [eng.add_request(Request(list(prompts[0]), params[0]))]
+        eng.step()  # prefill of the first request
+        for p, prm in zip(prompts[1:], params[1:]):  # a burst trickles in between steps
+            reqs.append(eng.add_request(Request(list(p), prm)))
+            eng.step()
+        while eng.has_work():
+            eng.step()
+        return [r.output_ids for r in reqs], eng.stats
+
+    ref, _ = run(0, mixed=False)
+    got, st = run(sum(len(p) for p in prompts[1:]))
+    assert got == ref
+    assert st["mixed_steps"] == 1, dict(st)  # the whole burst admitted together
+    _, st0 = run(0)
+    assert st0["mixed_steps"] > 1

@@ -344,7 +344,7 @@ def test_xd_gemm_matches_fp32(hipk, epi, form, M, N, K):
 
 
 @pytest.mark.parametrize("act", ["silu", "gelu_tanh"])
-@pytest.mark.parametrize("form", [121, 141, 161, 241, 242, 243, 261, 264])
+@pytest.mark.parametrize("form", [121, 141, 161, 241, 242, 243, 261, 264, 281, 283])
 @pytest.mark.parametrize("M,I,K", [(256, 1536, 1024), (200, 768, 1600), (1024, 384, 832)])
 def test_xd_gemm_glu_matches_fp32(hipk, act, form, M, I, K):
     if not G.xd_supported(M, I, K, form, glu=True):
@@ -357,7 +357,7 @@ def test_xd_gemm_glu_matches_fp32(hipk, act, form, M, I, K):
     _check(out, _ref(x, w, act, None))
 
 
-@pytest.mark.parametrize("form", [143, 145, 247, 268])
+@pytest.mark.parametrize("form", [143, 145, 247, 268, 285])
 def test_xd_gemm_uneven_splitk(hipk, form):
     """K tiles that the slices do not divide evenly (K / 64 = 61 over 3, 5, 7, 8 slices)."""
     M, N, K = 384, 768, 61 * 64
