@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 mkdir -p gpurun_out/r4o
 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread \
-  tests/test_gemm_gpu.py -k "xd or norm_glu" > gpurun_out/r4o/tests.log 2>&1 || { tail -30 gpurun_out/r4o/tests.log; exit 1; }
+  tests/test_gemm_gpu.py tests/test_service_gpu.py -k "xd or norm_glu or side_by_side" > gpurun_out/r4o/tests.log 2>&1 || { tail -30 gpurun_out/r4o/tests.log; exit 1; }
 tail -1 gpurun_out/r4o/tests.log
 P="timeout -k 10 150 python -u scripts/w4_probe.py --iters 20 --rounds 5"
 {

@@ -51,3 +51,46 @@ def test_llm_service_on_gpu_through_raft_cluster(hipk, tmp_path):
     finally:
         srv.stop(0)
         backend.close()
+
+
+def test_llm_server_serves_two_models_side_by_side_on_one_gpu(hipk):
+    """``llm.server --serve smart=tiny-llama@0 --serve summary=tiny-gemma@0``: two engine
+    groups (different model families) share one MI355X behind one service address; each RPC
+    runs on its feature's engine (its engine's step counters move, the other's do not)."""
+    import argparse
+
+    from drtc_amd.llm import server as S
+    from drtc_amd.utils.cluster import free_port
+
+    args = argparse.Namespace(backend="engine", model="tiny-llama", tp=1, gpus=1, max_batch=8,
+                              max_model_len=512, no_graphs=False, custom_allreduce=False,
+                              in_process=True)
+    router = S.build_feature_backends(args, ["smart=tiny-llama@0", "summary=tiny-gemma@0"])
+    smart, summ = router.route("smart"), router.route("summary")
+    assert smart is not summ
+    assert smart.engine.model.cfg.name == "tiny-llama"
+    assert summ.engine.model.cfg.name == "tiny-gemma"
+    fp = FeatureParams(ignore_eos=True)
+    for f in (fp.answer, fp.smart, fp.summary, fp.suggest):
+        f.max_new_tokens = 6
+    port = free_port()
+    srv = S.serve(router, port=port, bind="127.0.0.1", params=fp)
+    try:
+        stub = make_stub(grpc.insecure_channel(f"127.0.0.1:{port}"), LLM_SERVICE)
+        msgs = [llm_pb.Message(sender="a", content="lunch tomorrow?")]
+        s0 = dict(smart.engine.stats), dict(summ.engine.stats)
+        r = stub.GetSmartReply(llm_pb.SmartReplyRequest(request_id="1", recent_messages=msgs),
+                               timeout=60)
+        assert len(r.suggestions) == 3
+        s1 = dict(smart.engine.stats), dict(summ.engine.stats)
+        assert s1[0].get("prefill_steps", 0) > s0[0].get("prefill_steps", 0)
+        assert s1[1].get("prefill_steps", 0) == s0[1].get("prefill_steps", 0)
+        r = stub.SummarizeConversation(llm_pb.SummarizeRequest(request_id="2", messages=msgs,
+                                                               max_length=200), timeout=60)
+        assert r.success
+        s2 = dict(smart.engine.stats), dict(summ.engine.stats)
+        assert s2[1].get("prefill_steps", 0) > s1[1].get("prefill_steps", 0)
+        assert s2[0].get("prefill_steps", 0) == s1[0].get("prefill_steps", 0)
+    finally:
+        srv.stop(0)
+        router.close()
