@@ -1,8 +1,10 @@
-"""In-process local cluster harness (tests, demos, benchmarks).
+"""Local cluster harnesses (tests, demos, benchmarks).
 
-Starts N Raft chat nodes on ephemeral localhost ports (the reference's
-manual 3-terminal setup, automated), optionally an LLM service, and exposes
-kill/restart for failover experiments.
+``LocalCluster`` starts N Raft chat nodes in THIS process on ephemeral localhost ports (the
+reference's manual 3-terminal setup, automated) and exposes kill/restart for failover
+experiments.  ``ProcessCluster`` starts each node in its own process, as a deployment runs
+them (one interpreter per node: the leader's RPC handling does not share a GIL with the
+followers, the benchmark clients or an in-process LLM front-end).
 """
 from __future__ import annotations
 
@@ -96,3 +98,69 @@ class LocalCluster:
     def __exit__(self, *exc):
         self.stop()
         return False
+
+
+def _node_proc(cfg, ready, stop) -> None:
+    import signal as _signal
+
+    from ..server.node import serve
+
+    _signal.signal(_signal.SIGINT, _signal.SIG_IGN)  # the parent stops us through `stop`
+    node, server = serve(cfg, block=False, bind="127.0.0.1")
+    ready.set()
+    stop.wait()
+    server.stop(1.0)
+    node.stop()
+
+
+class ProcessCluster(LocalCluster):
+    """LocalCluster with every node in its own (spawned) process; leader discovery and
+    logins go over RPC."""
+
+    def start(self) -> "ProcessCluster":
+        import multiprocessing as mp
+
+        ctx = mp.get_context("spawn")
+        self._stop = ctx.Event()
+        self.procs = {}
+        readies = []
+        for i in self.peers:
+            r = ctx.Event()
+            p = ctx.Process(target=_node_proc, args=(self.cfgs[i], r, self._stop), daemon=True)
+            p.start()
+            self.procs[i] = p
+            readies.append(r)
+        for r in readies:
+            if not r.wait(120):
+                self.stop()
+                raise RuntimeError("a Raft node process did not start")
+        return self
+
+    def leader(self, timeout: float = 20.0) -> int:
+        t_end = time.time() + timeout
+        while time.time() < t_end:
+            for i in self.peers:
+                try:
+                    r = self.stub(i).GetLeaderInfo(raft_pb.GetLeaderRequest(), timeout=1.0)
+                except grpc.RpcError:
+                    continue
+                if r.is_leader:
+                    try:  # genesis (default users / channels) applied: a login succeeds
+                        self.login(i)
+                        return i
+                    except (AssertionError, grpc.RpcError):
+                        pass
+            time.sleep(0.05)
+        raise TimeoutError("no leader")
+
+    def kill(self, i: int) -> None:
+        raise NotImplementedError("ProcessCluster stops all nodes together")
+
+    def stop(self) -> None:
+        if getattr(self, "_stop", None) is not None:
+            self._stop.set()
+        for p in getattr(self, "procs", {}).values():
+            p.join(timeout=10)
+            if p.is_alive():
+                p.kill()
+        self.procs = {}

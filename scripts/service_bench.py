@@ -34,7 +34,7 @@ import grpc  # noqa: E402
 from drtc_amd.llm.server import serve as serve_llm, serve_aio  # noqa: E402
 from drtc_amd.llm.service import FeatureParams  # noqa: E402
 from drtc_amd.protos import LLM_SERVICE, RAFT_SERVICE, llm_pb, make_stub, raft_pb  # noqa: E402
-from drtc_amd.utils.cluster import LocalCluster, free_port  # noqa: E402
+from drtc_amd.utils.cluster import LocalCluster, ProcessCluster, free_port  # noqa: E402
 from drtc_amd.utils.metrics import METRICS  # noqa: E402
 from drtc_amd.utils.synthetic import channel_history  # noqa: E402
 
@@ -198,6 +198,9 @@ def main():
     ap.add_argument("--frontends", type=int, default=1,
                     help="--backend pool: gRPC front-end processes sharing the port over the "
                          "engine replica (llm/frontends.py)")
+    ap.add_argument("--in-process-nodes", action="store_true",
+                    help="--mode raft: run the 3 Raft nodes in this process (default: one "
+                         "process per node, as deployed)")
     ap.add_argument("--requests", type=int, default=1024)
     ap.add_argument("--concurrency", type=int, default=256)
     ap.add_argument("--max-batch", type=int, default=512)
@@ -236,15 +239,16 @@ def main():
     tmp = tempfile.TemporaryDirectory()
     try:
         if args.mode == "raft":
-            cluster = LocalCluster(3, data_root=tmp.name, llm_address=f"127.0.0.1:{port}",
-                                   grpc_workers=args.concurrency + 16).start()
+            cls = LocalCluster if args.in_process_nodes else ProcessCluster
+            cluster = cls(3, data_root=tmp.name, llm_address=f"127.0.0.1:{port}",
+                          grpc_workers=args.concurrency + 16).start()
             leader = cluster.leader()
             token = cluster.login(leader)
             st = cluster.stub(leader)
             for m in channel_history(rng, 5):
                 st.SendMessage(raft_pb.SendMessageRequest(token=token, channel_id="general",
                                                           content=m.content))
-            target = (args.mode, cluster.addresses()[leader], token)
+            target = (args.mode, cluster.peers[leader], token)
         else:
             target = (args.mode, f"127.0.0.1:{port}", None)
 

@@ -342,3 +342,24 @@ def test_logout_on_follower_is_forwarded_to_leader(cluster):
             break
         time.sleep(0.05)
     assert not any(ok)
+
+
+def test_process_cluster_one_interpreter_per_node(tmp_path):
+    """utils.cluster.ProcessCluster: three Raft nodes in three processes elect a leader that
+    serves logins and a replicated write over RPC, then shut down together."""
+    from drtc_amd.protos import raft_pb
+    from drtc_amd.utils.cluster import ProcessCluster
+
+    c = ProcessCluster(3, data_root=str(tmp_path)).start()
+    try:
+        L = c.leader()
+        tok = c.login(L)
+        r = c.stub(L).SendMessage(raft_pb.SendMessageRequest(token=tok, channel_id="general",
+                                                             content="from another process"))
+        assert r.success
+        got = c.stub(L).GetMessages(raft_pb.GetMessagesRequest(token=tok, channel_id="general",
+                                                               limit=50))
+        assert any(m.content == "from another process" for m in got.messages)
+    finally:
+        c.stop()
+    assert all(not p.is_alive() for p in c.procs.values())
