@@ -769,13 +769,25 @@ class EngineLoop:
     """Background thread that drives an engine; used by the LLM gRPC service
     so concurrent RPCs are batched together (continuous batching)."""
 
+    # serving defaults (closed-loop service bench, profiles/r4o: 1024 clients, 10 waves, same
+    # box: 89.9 % of the engine bench with neither, 94.9 % direct with both; via the Raft
+    # leader 92.0 -> 94.5 % with arrival gathering at 16k tokens)
+    SERVING_BURST_GAP_MS = 3.0
+    SERVING_ADMIT_MIN_TOKENS = 8192
+
     def __init__(self, engine: LLMEngine, idle_sleep: float = 0.0005,
                  burst_gap_s: float | None = None, burst_max_s: float = 0.05):
         self.engine = engine
         self.idle_sleep = idle_sleep
-        # burst gathering (off unless burst_gap_s > 0; DRTC_BURST_GAP_MS): see _hold
+        # burst gathering (DRTC_BURST_GAP_MS, 0 disables): see _hold
         if burst_gap_s is None:
-            burst_gap_s = float(os.environ.get("DRTC_BURST_GAP_MS", "0")) / 1000.0
+            burst_gap_s = float(os.environ.get("DRTC_BURST_GAP_MS",
+                                               str(self.SERVING_BURST_GAP_MS))) / 1000.0
+        # arrival gathering for the mixed steps of a served engine (LLMEngine.admit_min_tokens;
+        # DRTC_ADMIT_MIN_TOKENS=0 disables)
+        if getattr(engine, "admit_min_tokens", None) == 0 and \
+                "DRTC_ADMIT_MIN_TOKENS" not in os.environ:
+            engine.admit_min_tokens = self.SERVING_ADMIT_MIN_TOKENS
         self.burst_gap_s, self.burst_max_s = burst_gap_s, burst_max_s
         self._last_submit = 0.0
         self._hold_start: float | None = None

@@ -473,7 +473,7 @@ def test_request_wait_races_finish():
 def test_engine_loop_burst_gathering():
     """EngineLoop burst gathering (DRTC_BURST_GAP_MS): while requests keep arriving less than
     the gap apart, the loop lets them gather (bounded by burst_max_s) instead of stepping on
-    the first one; off by default; a lone request waits at most the gap."""
+    the first one; a lone request waits at most the gap."""
     import collections
     import time
 
@@ -498,7 +498,7 @@ def test_engine_loop_burst_gathering():
             self.waiting.clear()
             self._waiting_tokens = 0
 
-    assert EngineLoop(Stub()).burst_gap_s == 0.0  # off unless configured
+    assert EngineLoop(Stub(), burst_gap_s=0.0).burst_gap_s == 0.0  # 0 disables it
     e = Stub()
     loop = EngineLoop(e, burst_gap_s=0.02, burst_max_s=0.5).start()
     try:
