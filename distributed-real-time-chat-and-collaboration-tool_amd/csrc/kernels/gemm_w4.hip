@@ -151,6 +151,10 @@ struct W4Tile {
 // Schedule variants (mfma_gemm variant 7 + V):
 //   V & 2  plain (temporal) epilogue stores instead of non-temporal ones
 //   V & 8  persistent form (see gemm_w4_kernel); V & 16 its per-XCD K rotation
+//   V & 32 the next tile's half-0 fragments read one per 4 MFMAs over half 1 (barrier 3 at
+//          MFMA 63) instead of one per MFMA at 104-119: the burst ran the LDS array at its
+//          256 B/clk limit beside the landing LDS-DMA (PMC: +72 % SQ_WAIT_INST_LDS against
+//          hipBLASLt's kernel of the same tile, profiles/r4j)
 template <int V, bool DMA, bool NEXT, bool Z, int Q>
 DRTC_DEVICE void w4_step(f32x4 (&acc)[8][8], bf16x8 (&fa0)[8], bf16x8 (&fb0)[8],
                          bf16x8 (&fa1)[8], bf16x8 (&fb1)[8], const W4Tile& T, const W4Dma& d) {
@@ -195,23 +199,35 @@ DRTC_DEVICE void w4_step(f32x4 (&acc)[8][8], bf16x8 (&fa0)[8], bf16x8 (&fb0)[8],
   }
   // ---- tile t + 1: its DMA (issued during tile t - 1) landed for every wave, then its
   // half-0 fragments: fa0[0], fb0[0..7], fa0[1..7]
-  constexpr int qn = 103;
+  constexpr bool kSpread = (V & 32) != 0;
+  constexpr int qn = kSpread ? 63 : 103;
+  // this step's own DMAs (tile t + 2) issued before qn: B 8 + A (1 at qn 63, 8 at 103)
+  constexpr int kYoung = kSpread ? 9 : 16;
   if constexpr (NEXT && Q == qn) {
     if constexpr (DMA && Z) {
       // first K step of a persistent tile: the previous tile's epilogue stores sit between
       // the DMA of K step 1 (needed now) and this step's DMA - do not wait for them
       if (T.seam)
-        w4_vmcnt<48>();
+        w4_vmcnt<32 + kYoung>();
       else
-        w4_vmcnt<16>();
+        w4_vmcnt<kYoung>();
     } else if constexpr (DMA) {
-      w4_vmcnt<16>();
+      w4_vmcnt<kYoung>();
     } else {
       w4_vmcnt<0>();
     }
     w4_barrier();
   }
-  if constexpr (NEXT && Q > qn && Q <= qn + 16) {
+  if constexpr (NEXT && kSpread && Q > qn && ((Q - qn - 1) & 3) == 0 && (Q - qn - 1) / 4 < 16) {
+    constexpr int r = (Q - qn - 1) / 4;
+    if constexpr (r == 0)
+      fa0[0] = w4_rd(T.lds, T.nxt + T.ra0);
+    else if constexpr (r <= 8)
+      fb0[r - 1] = w4_rd(T.lds, T.nxt + T.rb0 + 128 * (r - 1));
+    else
+      fa0[r - 8] = w4_rd(T.lds, T.nxt + T.ra0 + 2048 * (r - 8));
+  }
+  if constexpr (NEXT && !kSpread && Q > qn && Q <= qn + 16) {
     constexpr int r = Q - qn - 1;
     if constexpr (r == 0)
       fa0[0] = w4_rd(T.lds, T.nxt + T.ra0);
@@ -716,6 +732,8 @@ int w4_launch(const W4Params& p, int v, hipStream_t st) {
     case 6: return w4_launch_v<EPI, 6>(p, st);
     case 8: return w4_launch_v<EPI, 8>(p, st);
     case 24: return w4_launch_v<EPI, 24>(p, st);
+    case 40: return w4_launch_v<EPI, 40>(p, st);
+    case 56: return w4_launch_v<EPI, 56>(p, st);
     default: return -1;
   }
 }
@@ -728,7 +746,8 @@ int w4_cfg_one() {
 template <int EPI>
 int w4_cfg() {
   return w4_cfg_one<EPI, 0>() | w4_cfg_one<EPI, 2>() | w4_cfg_one<EPI, 4>() |
-         w4_cfg_one<EPI, 6>() | w4_cfg_one<EPI, 8>() | w4_cfg_one<EPI, 24>();
+         w4_cfg_one<EPI, 6>() | w4_cfg_one<EPI, 8>() | w4_cfg_one<EPI, 24>() |
+         w4_cfg_one<EPI, 40>() | w4_cfg_one<EPI, 56>();
 }
 
 }  // namespace
@@ -755,10 +774,11 @@ int launch_gemm_w4(void* c, const void* a, const void* b, const void* r, int M, 
   if (M <= 0 || N <= 0 || K <= 0 || K % 64 || splitk < 1 || (K / 64) % splitk) return -1;
   if (glu ? (N % 128 || up_off != N) : (N % 256)) return -1;
   // persistent form (v & 8): one slice, and two K tiles per tile for the cross-tile prefetch
-  if ((v & 8) && ((v != 8 && v != 24) || splitk != 1 || K / 64 < 2)) return -1;
+  if ((v & 8) && ((v != 8 && v != 24 && v != 40 && v != 56) || splitk != 1 || K / 64 < 2))
+    return -1;
   if ((v & 4) && splitk < 2) return -1;  // the parallel combine is a split-K form
   // the per-XCD K rotation needs whole XCD rounds of workgroups: below 8 tiles, plain persistent
-  if (v == 24 && (int64_t)((M + 255) / 256) * (glu ? N / 128 : N / 256) < 8) v = 8;
+  if ((v & 16) && (int64_t)((M + 255) / 256) * (glu ? N / 128 : N / 256) < 8) v &= ~16;
   if (lda % 8 || ldb % 8 || (glu ? ldc % 4 : ldc % 8)) return -1;
   if (res && (ldr % 8 || r == nullptr || (uintptr_t)r % 16)) return -1;
   if ((uintptr_t)a % 16 || (uintptr_t)b % 16 || (uintptr_t)c % (glu ? 8 : 16)) return -1;

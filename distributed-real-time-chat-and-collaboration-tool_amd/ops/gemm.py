@@ -421,8 +421,9 @@ def gemm_w4_variant(variant: int) -> bool:
     """mfma_gemm variants: 7 per-tile (split-K with the last-arriver combine), 9 the same
     with temporal epilogue stores, 11 / 13 per-tile with the parallel split-K combine (every
     slice finishes a row band of its tile; the grid must fit the CUs), 15 persistent, 31
-    persistent with the per-XCD K rotation."""
-    return variant in (7, 9, 11, 13, 15, 31)
+    persistent with the per-XCD K rotation, 47 / 63 those two with the next tile's fragment
+    reads spread over half 1."""
+    return variant in (7, 9, 11, 13, 15, 31, 47, 63)
 
 
 def mfma_gemm(x: torch.Tensor, w: torch.Tensor, epi: str = "store",

@@ -24,12 +24,15 @@ $P --shape 16384,6144,4096 --arms lib,v31,x281 --rotate 1
 svc() {  # tag, args
   local tag=$1; shift
   env "$@" timeout -k 10 500 python scripts/service_bench.py --model llama-3-8b --backend pool --client-procs 8 \
-    --requests 10240 --concurrency 1024 --max-batch 1024 --mode direct > gpurun_out/r4o/service_$tag.json 2> gpurun_out/r4o/service_$tag.err
+    --requests 10240 --concurrency 1024 --max-batch 1024 $MODE > gpurun_out/r4o/service_$tag.json 2> gpurun_out/r4o/service_$tag.err
   local rc=$?; python -c "
 import json; d=json.load(open('gpurun_out/r4o/service_$tag.json'))
 print('$tag', {k: d.get(k) for k in ('requests','errors','seconds','gen_tokens_per_s','p50_latency_ms','p99_latency_ms')}, d.get('replica_delta'))"; return $rc
 }
 timeout -k 10 400 python -u bench.py --steps 6 --warmup 2 > gpurun_out/r4o/engine.json 2> gpurun_out/r4o/engine.err || exit 1
 cut -c1-120 gpurun_out/r4o/engine.json
+MODE="--mode direct"
 svc g3 DRTC_BURST_GAP_MS=3 && svc g3_a16k DRTC_BURST_GAP_MS=3 DRTC_ADMIT_MIN_TOKENS=16384 && \
-svc g3_a8k DRTC_BURST_GAP_MS=3 DRTC_ADMIT_MIN_TOKENS=8192
+svc g3_a8k DRTC_BURST_GAP_MS=3 DRTC_ADMIT_MIN_TOKENS=8192 || exit 1
+MODE="--mode raft"
+svc raft_g3 DRTC_BURST_GAP_MS=3 && svc raft_g3_a16k DRTC_BURST_GAP_MS=3 DRTC_ADMIT_MIN_TOKENS=16384

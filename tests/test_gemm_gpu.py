@@ -228,7 +228,7 @@ def test_w4_splitk_parallel_combine_rejects(hipk):
 
 
 # ------------------------------------------------------ gemm_w4 persistent forms (15 / 31)
-@pytest.mark.parametrize("variant", [15, 31])
+@pytest.mark.parametrize("variant", [15, 31, 47, 63])
 @pytest.mark.parametrize("epi", ["store", "residual", "silu", "gelu_tanh"])
 @pytest.mark.parametrize("M,N,K", [(8192, 8192, 128), (4500, 4096, 576), (2300, 8192, 192),
                                    (1024, 4096, 1088), (2048, 2048, 512)])
