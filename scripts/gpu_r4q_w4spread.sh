@@ -11,10 +11,10 @@ timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method threa
 tail -1 gpurun_out/r4q/tests.log
 P="timeout -k 10 150 python -u scripts/w4_probe.py --iters 10 --rounds 5"
 {
-$P --shape 16384,6144,4096 --arms lib,v31,v63,v15,v47 --group-m 4 &&
-$P --shape 16384,4096,4096 --epi residual --arms lib,v31,v63 --group-m 4 &&
-$P --shape 16384,28672,4096 --epi silu --arms lib,v31,v63 &&
-$P --shape 16384,4096,14336 --arms lib,v31,v63 --group-m 2 &&
+$P --shape 16384,6144,4096 --arms lib,v31,v63,v15,v47,x281 --group-m 4 &&
+$P --shape 16384,4096,4096 --epi residual --arms lib,v31,v63,x281 --group-m 4 &&
+$P --shape 16384,28672,4096 --epi silu --arms lib,v31,v63,x281 &&
+$P --shape 16384,4096,14336 --arms lib,v31,v63,x281 --group-m 2 &&
 $P --shape 1024,28672,4096 --epi silu --arms lib,v31,v63 --rotate 3
 } 2>&1 | grep -v amdgpu.ids | tee gpurun_out/r4q/probe.log || exit 1
 b() {  # tag, env...
