@@ -15,7 +15,10 @@ $P --shape 16384,6144,4096 --arms lib,v31,v63,v15,v47,x281 --group-m 4 &&
 $P --shape 16384,4096,4096 --epi residual --arms lib,v31,v63,x281 --group-m 4 &&
 $P --shape 16384,28672,4096 --epi silu --arms lib,v31,v63,x281 &&
 $P --shape 16384,4096,14336 --arms lib,v31,v63,x281 --group-m 2 &&
-$P --shape 1024,28672,4096 --epi silu --arms lib,v31,v63 --rotate 3
+$P --shape 1024,28672,4096 --epi silu --arms lib,v31,v63,x281,x241 --rotate 3 &&
+$P --shape 512,28672,4096 --epi silu --arms lib,v31,x281,x241 --rotate 3 &&
+$P --shape 256,57344,8192 --epi silu --arms lib,x241,x281,x242 --rotate 2 &&
+$P --shape 1024,4096,14336 --arms lib,x242 --rotate 4
 } 2>&1 | grep -v amdgpu.ids | tee gpurun_out/r4q/probe.log || exit 1
 b() {  # tag, env...
   local tag=$1; shift

@@ -48,6 +48,10 @@ def main():
     res = torch.randn(M, nout, device=dev, dtype=torch.bfloat16) if a.epi == "residual" else None
     out = torch.empty(M, nout, device=dev, dtype=torch.bfloat16)
     G.gemm_workspace(dev)
+    # "lib" is the library path the engine had before the hand decode GEMMs: route around the
+    # gemm_xd table entries (ops.linear would otherwise dispatch them)
+    G._xd_enabled = False
+    G.reset()
     fns = {}
     for arm in a.arms.split(","):
         if arm == "lib":
@@ -63,7 +67,7 @@ def main():
                 fns[arm] = lambda form=form: G.xd_gemm(x, nxt(), "residual", residual=res,
                                                        out=res, form=form)
             else:
-                fns[arm] = lambda form=form: G.xd_gemm(x, nxt(), out=out, form=form)
+                fns[arm] = lambda form=form: G.xd_gemm(x, nxt(), a.epi, out=out, form=form)
         else:
             # "vV" or "vV:splitk:group_m" (group_m < 0: K-slice-by-XCD tile order)
             f = arm[1:].split(":")
