@@ -444,6 +444,7 @@ def mfma_gemm(x: torch.Tensor, w: torch.Tensor, epi: str = "store",
     N = w.shape[0] // 2 if glu else w.shape[0]
     if out is None:
         out = torch.empty((M, N), dtype=x.dtype, device=x.device)
+    assert out.shape == (M, N) and out.stride(1) == 1, (out.shape, M, N)  # written through ldc
     slab, cnt = ((ws or gemm_workspace(x.device)) if splitk > 1 else (None, None))
     check(hipk().gemm(out.data_ptr(), x.data_ptr(), w.data_ptr(), ptr(residual), M, N, K,
                       x.stride(0), w.stride(0), out.stride(0),
@@ -664,6 +665,10 @@ def xd_gemm(x: torch.Tensor, w: torch.Tensor, epi: str = "store",
     if out is None:
         out = residual if (epi == "residual" and residual is not None) else \
             torch.empty((M, N), dtype=x.dtype, device=x.device)
+    # the kernel writes M x N through ldc: the output must hold exactly that
+    assert out.shape == (M, N) and out.stride(1) == 1 and out.dtype == x.dtype, (out.shape, M, N)
+    if epi == "residual":
+        assert residual is not None and residual.shape == (M, N) and residual.stride(1) == 1
     slab, cnt = ((ws or gemm_workspace(x.device)) if sk > 1 else (None, None))
     check(hipk().gemm_xd(out.data_ptr(), x.data_ptr(), w.data_ptr(), ptr(residual), M, N, K,
                          x.stride(0), w.stride(0), out.stride(0),
