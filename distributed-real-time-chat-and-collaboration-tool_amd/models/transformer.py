@@ -248,8 +248,9 @@ class TransformerLM:
     def _mlp(self, L: dict, x: ops.PendingNorm, decode: bool = False) -> torch.Tensor:
         if self.cfg.is_moe:
             return self._moe(L, x.materialize(), decode), False
-        if ops.w4_glu_ok(x.x, L["gate_up"], self.cfg.act):
-            # prefill / full-batch decode: gate_up GEMM with the GLU in its epilogue (gemm_w4)
+        if ops.fused_glu_ok(x.x, L["gate_up"], self.cfg.act):
+            # prefill / decode batches with a fused form: gate_up GEMM with the GLU in its
+            # epilogue (gemm_w4, or a tuned gated gemm_xd form)
             h = ops.norm_glu(x, L["gate_up"], self.cfg.act)
             res = self._fusable_residual(h, x)
             if res is not None:

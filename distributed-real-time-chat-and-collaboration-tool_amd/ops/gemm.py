@@ -502,7 +502,12 @@ def save_entries(entries: dict[str, dict], path: str | None = None) -> str:
 # 231.1 us (v15), prefill shapes within +-1 % (K = 14336 1.2 % faster).  Fewer than 8 tiles
 # run the plain persistent form.
 W4_PERSIST = os.environ.get("DRTC_W4_PERSIST", "1") == "1"
-W4_PERSIST_VARIANT = int(os.environ.get("DRTC_W4_VARIANT", "31"))
+# Variant 63 (the default since profiles/r4q) also spreads the next tile's fragment reads
+# over half 1 (one per 4 MFMAs after a barrier at MFMA 63, instead of a burst of one per MFMA
+# at 104-119): interleaved on one box, prefill gate_up+GLU 2557 vs 2597 us, o+residual 384.9
+# vs 392.9, down 1256.6 vs 1280.5, qkv 534.7 vs 531.4, decode gate_up+GLU at M = 1024 199.2
+# vs 214.1; headline 20,599 / 20,572 vs 20,338 tok/s.
+W4_PERSIST_VARIANT = int(os.environ.get("DRTC_W4_VARIANT", "63"))
 
 
 def _w4v(K: int) -> int:
@@ -574,6 +579,15 @@ def glu_form(M: int, N2: int, K: int, ldx: int) -> int:
     return form if form and xd_supported(M, N2 // 2, K, form, glu=True) else 0
 
 
+def fused_glu_ok(x: torch.Tensor, w: torch.Tensor, act: str) -> bool:
+    """Whether ``norm_glu`` computes x [M, K] @ [gate; up]^T with the GLU inside a GEMM
+    epilogue (gemm_w4 at prefill-sized / full decode batches, or a tuned gated gemm_xd form)."""
+    if w4_glu_ok(x, w, act):
+        return True
+    return (act in ("silu", "gelu_tanh") and _gpu_bf16(x, w) and w.shape[1] == x.shape[1]
+            and _aligned(x, w) and glu_form(x.shape[0], w.shape[0], x.shape[1], x.shape[1]) != 0)
+
+
 def norm_glu(p, w: torch.Tensor, act: str = "silu") -> torch.Tensor:
     """h = act(norm(x) @ gate^T) * (norm(x) @ up^T) for an ``ops.PendingNorm`` p and the fused
     [gate; up] weight: on the 4-wave hand GEMM with the GLU in its epilogue when
@@ -582,18 +596,18 @@ def norm_glu(p, w: torch.Tensor, act: str = "silu") -> torch.Tensor:
     act_glu."""
     from .activation import act_glu
 
+    x = p.x
+    if (act in ("silu", "gelu_tanh") and isinstance(x, torch.Tensor) and _gpu_bf16(x, w)
+            and w.shape[1] == x.shape[1] and _aligned(x, w)):
+        form = glu_form(x.shape[0], w.shape[0], x.shape[1], x.shape[1])  # normed x: dense
+        if form:  # a decode batch where the tuner measured the gated gemm_xd fastest
+            xm = p.materialize()
+            return xd_gemm(xm, w, act, form=form)
     if w4_glu_ok(p.x, w, act):
         x = p.materialize()
         M, K = x.shape
         return mfma_gemm(x, w, act, variant=_w4v(K),
                          group_m=w4_group_m(M, w.shape[0] // 2, K, glu=True))
-    x = p.x
-    if (act in ("silu", "gelu_tanh") and isinstance(x, torch.Tensor) and _gpu_bf16(x, w)
-            and w.shape[1] == x.shape[1] and _aligned(x, w)):
-        form = glu_form(x.shape[0], w.shape[0], x.shape[1], x.shape[1])  # normed x: dense
-        if form:
-            xm = p.materialize()
-            return xd_gemm(xm, w, act, form=form)
     return act_glu(norm_linear(p, w), act)
 
 
@@ -740,7 +754,8 @@ def midm_gemm(x: torch.Tensor, w: torch.Tensor, epi: str = "store",
     return out
 
 
-__all__ = ["linear", "route", "norm_linear", "glu_linear", "norm_glu", "linear_residual",
+__all__ = ["linear", "route", "norm_linear", "glu_linear", "norm_glu", "fused_glu_ok",
+           "linear_residual",
            "residual_fusable", "w4_glu_ok", "w4_ok", "w4_shape_ok", "w4_group_m", "mfma_gemm",
            "gemm_workspace", "new_gemm_workspace", "skinny_linear", "skinny_ok",
            "skinny_variant", "skinny_supports", "midm_gemm", "midm_supported", "midm_splits",

@@ -65,6 +65,7 @@ def main() -> None:
     ap.add_argument("--ms", default=",".join(map(str, BUCKETS)))
     ap.add_argument("--min-gain", type=float, default=0.03)
     ap.add_argument("--out", default="gpurun_out/xd_tuned.json")
+    ap.add_argument("--gemms", default="qkv,o,gate_up,down", help="projections to tune")
     a = ap.parse_args()
     from drtc_amd import ops
     from drtc_amd.ops import gemm as G
@@ -80,8 +81,8 @@ def main() -> None:
     for spec in a.configs.split(","):
         model, tp = spec.split(":")
         for name, (N, K) in projection_shapes(model, int(tp)).items():
-            if name == "lm_head":  # 256 x 256 library tiles win at vocabulary widths
-                continue
+            if name == "lm_head" or name not in a.gemms.split(","):
+                continue  # lm_head: 256 x 256 library tiles win at vocabulary widths
             wbytes = N * K * 2
             ncopy = max(2, min(10, -(-512 * 2**20 // wbytes)))
             ws = [(torch.randn(N, K, device=dev, generator=g) * 0.02).to(torch.bfloat16)
@@ -94,12 +95,18 @@ def main() -> None:
                 rec = measure(G, x, ws, N, K, "store", lambda w: G.linear(x, w), name, model, tp, M)
                 if rec and rec["xd_us"] < rec["base_us"] * (1 - a.min_gain):
                     ent.update(xd=rec["xd_form"], xd_us=rec["xd_us"], xd_base_us=rec["base_us"])
-                # gate_up with the GLU in the epilogue, below the fused-GLU gemm_w4 batches:
-                # against norm_linear's route + act_glu
-                if name == "gate_up" and M < G.W4_GLU_MIN_M:
+                # gate_up with the GLU in the epilogue against norm_glu's route without gemm_xd
+                # (the fused-GLU gemm_w4 from W4_GLU_MIN_M rows, else the route + act_glu)
+                if name == "gate_up":
                     act = "silu"
-                    rec = measure(G, x, ws, N // 2, K, act,
-                                  lambda w: ops.act_glu(G.linear(x, w), act), name, model, tp, M)
+                    if M >= G.W4_GLU_MIN_M:
+                        def glu_base(w, act=act):
+                            return G.mfma_gemm(x, w, act, variant=G._w4v(K),
+                                               group_m=G.w4_group_m(M, N // 2, K, glu=True))
+                    else:
+                        def glu_base(w, act=act):
+                            return ops.act_glu(G.linear(x, w), act)
+                    rec = measure(G, x, ws, N // 2, K, act, glu_base, name, model, tp, M)
                     if rec and rec["xd_us"] < rec["base_us"] * (1 - a.min_gain):
                         ent.update(xd_glu=rec["xd_form"], xd_glu_us=rec["xd_us"],
                                    xd_glu_base_us=rec["base_us"])
