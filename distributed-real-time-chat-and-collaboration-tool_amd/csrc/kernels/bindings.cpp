@@ -100,10 +100,10 @@ PYBIND11_MODULE(_hipk, m) {
   });
   // gemm_xd (ops.gemm.xd_gemm): decode-shaped tiles, XCD-partitioned order, split-K 1..8
   m.def("gemm_xd", [](u64 c, u64 a, u64 b, u64 r, int M, int N, int K, int lda, int ldb, int ldc,
-                      int ldr, int epi, int mt, int nf, int splitk, int pf, u64 slab,
-                      int64_t slab_bytes, u64 counters, int n_counters, u64 st) {
+                      int ldr, int epi, int mt, int nf, int splitk, u64 slab, int64_t slab_bytes,
+                      u64 counters, int n_counters, u64 st) {
     return drtc::launch_gemm_xd(P<void>(c), P<const void>(a), P<const void>(b), P<const void>(r),
-                                M, N, K, lda, ldb, ldc, ldr, epi, mt, nf, splitk, pf, P<void>(slab),
+                                M, N, K, lda, ldb, ldc, ldr, epi, mt, nf, splitk, P<void>(slab),
                                 slab_bytes, P<int>(counters), n_counters, S(st));
   });
   m.def("gemm_xd_workspace_bytes", &drtc::gemm_xd_workspace_bytes);

@@ -56,15 +56,10 @@ enum { XD_STORE = 0, XD_RESIDUAL = 1, XD_SILU = 2, XD_GELU = 3 };
 template <int EPI>
 DRTC_DEVICE constexpr bool xd_glu() { return EPI == XD_SILU || EPI == XD_GELU; }
 
-template <int MT_, int NF_, int S_, bool SPLIT_, bool PF_ = false>
+template <int MT_, int NF_, int S_, bool SPLIT_>
 struct XdCfg {
   static constexpr int MT = MT_, NF = NF_, S = S_;
   static constexpr bool SPLIT = SPLIT_;            // split-K combine compiled in
-  // PF: each wave also touches its quarter of the weight tile PFD K tiles ahead with one
-  // dword-per-row LDS-DMA into a dummy LDS slot - an L2 prefetch of the weight stream, so
-  // the ring's own DMA of those rows hits the L2 instead of waiting on HBM
-  static constexpr bool PF = PF_;
-  static constexpr int PFD = S + 4;
   static constexpr int TM = 128 * MT;              // tile rows
   static constexpr int TN = 32 * NF;               // tile columns
   static constexpr int FA = 4 * MT;                // A fragments per wave (16 rows each)
@@ -76,9 +71,7 @@ struct XdCfg {
   static constexpr int LDS = S * STAGE;            // the K-tile ring
   static constexpr int PITCH = 32 * NF + 16;       // epilogue bytes per wave-tile row (padded)
   static constexpr int IMAGE = 4 * 64 * MT * PITCH;  // the epilogue's bf16 tile image
-  static constexpr int PF_OFF = LDS > IMAGE ? LDS : IMAGE;  // prefetch dummy slot (256 B)
-  static constexpr int ALLOC = PF_OFF + (PF ? 256 : 0);
-  static constexpr int DV = D + (PF ? 1 : 0);      // vector-memory ops per wave per K tile
+  static constexpr int ALLOC = LDS > IMAGE ? LDS : IMAGE;
   static_assert(ALLOC <= 160 * 1024, "LDS exceeds the CU's 160 KiB");
   static_assert(NR < H, "half-0 fragment reads must fit the half");
 };
@@ -102,7 +95,6 @@ struct XdDma {
   unsigned va[C::DA];
   unsigned vb[C::DB];
   unsigned lds_a, lds_b;  // LDS byte address of this wave's first DMA block in stage 0
-  unsigned vpf, lds_pf;   // PF: this lane's weight row offset, the dummy LDS slot
 };
 
 // Fragment read offsets within a stage (bytes): row 64 MT wm + l16 (A) / 16 NF wn + l16 (B),
@@ -125,25 +117,15 @@ DRTC_DEVICE bf16x8 xd_rd(const char* lds, int off) {
   return *reinterpret_cast<const bf16x8*>(lds + off);
 }
 
-// One LDS-DMA wave-instruction outside the main loop: M0 saved and restored (dword: the PF
-// prefetch form, 4 B per lane).
-DRTC_DEVICE void xd_dma(unsigned dst, unsigned voff, __amdgpu_buffer_rsrc_t rsrc, unsigned soff,
-                        bool dword = false) {
+// One LDS-DMA wave-instruction outside the main loop: M0 saved and restored.
+DRTC_DEVICE void xd_dma(unsigned dst, unsigned voff, __amdgpu_buffer_rsrc_t rsrc, unsigned soff) {
   unsigned keep;
-  if (dword)
-    asm volatile(
-        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
-        "buffer_load_dword %2, %3, %4 offen lds\n\ts_mov_b32 m0, %0"
-        : "=&s"(keep)
-        : "s"(dst), "v"(voff), "s"(rsrc), "s"(soff)
-        : "memory");
-  else
-    asm volatile(
-        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
-        "buffer_load_dwordx4 %2, %3, %4 offen lds\n\ts_mov_b32 m0, %0"
-        : "=&s"(keep)
-        : "s"(dst), "v"(voff), "s"(rsrc), "s"(soff)
-        : "memory");
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
+      "buffer_load_dwordx4 %2, %3, %4 offen lds\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "s"(dst), "v"(voff), "s"(rsrc), "s"(soff)
+      : "memory");
 }
 
 // Fragment r of a K half in consumption order (A row block 0, every B column block, then the
@@ -196,22 +178,12 @@ DRTC_DEVICE void xd_dmas(const XdDma<C>& d, int cur, unsigned kb) {
   }
 }
 
-// PF: one dword per weight row of this wave's quarter of the tile at K tile byte offset kbp,
-// landing in the dummy LDS slot (the point is the L2 fill on the way).  Main loop form: M0 is
-// re-set by the DMA group that follows.
-template <class C>
-DRTC_DEVICE void xd_pf(const XdDma<C>& d, unsigned kbp) {
-  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dword %1, %2, %3 offen lds"
-               : : "s"(d.lds_pf), "v"(d.vpf), "s"(d.rb), "s"(kbp) : "memory");
-}
-
 // Step Q of a K tile (0 .. 2 H - 1): MFMA Q, then the memory work scheduled behind it.  All
 // conditions are compile-time constants; sched_barrier(0) pins the emitted order.
 template <class C, bool DMA, bool NEXT, int WT, bool Z, int Q>
 DRTC_DEVICE void xd_step(f32x4 (&acc)[C::FA][C::NF], bf16x8 (&fa0)[C::FA], bf16x8 (&fb0)[C::NF],
                          bf16x8 (&fa1)[C::FA], bf16x8 (&fb1)[C::NF], const char* lds, int cur,
-                         int nxt, unsigned kb, unsigned kbp, const XdFrag& f,
-                         const XdDma<C>& d) {
+                         int nxt, unsigned kb, const XdFrag& f, const XdDma<C>& d) {
   constexpr int H = C::H, NF = C::NF;
   constexpr int h = Q / H, rem = Q % H, i = rem / NF, j = rem % NF;
   if constexpr (h == 0 && Z)  // first K tile: accumulate onto 0 (no zeroed AGPRs to coalesce)
@@ -225,14 +197,12 @@ DRTC_DEVICE void xd_step(f32x4 (&acc)[C::FA][C::NF], bf16x8 (&fa0)[C::FA], bf16x
     xd_read<C, Q - 1>(fa1, fb1, lds, cur, f.ra1, f.rb1);
   // ---- boundary: tile t + 1 landed for every wave; every read of this stage is done
   if constexpr (NEXT && Q == H - 1) {
-    xd_vmcnt<WT * C::DV>();  // WT younger K tiles of this wave may still be in flight
+    xd_vmcnt<WT * C::D>();  // WT younger K tiles of this wave may still be in flight
     xd_lgkm0();
     xd_barrier();
   }
   // ---- half 1: DMA of tile t + S into this stage, spread over the half; the next tile's
   // half-0 fragments in between
-  if constexpr (C::PF && DMA && h == 1 && rem == 0)
-    xd_pf<C>(d, kbp);  // before the DMA group: [prefetch, DMA of tile t + S] per K tile
   if constexpr (DMA && h == 1)
     xd_dmas<C, (rem * C::D + H - 1) / H, ((rem + 1) * C::D + H - 1) / H>(d, cur, kb);
   if constexpr (NEXT && h == 1)
@@ -245,16 +215,16 @@ template <class C, bool DMA, bool NEXT, int WT, bool Z, int... Qs>
 DRTC_DEVICE void xd_steps(std::integer_sequence<int, Qs...>, f32x4 (&acc)[C::FA][C::NF],
                           bf16x8 (&fa0)[C::FA], bf16x8 (&fb0)[C::NF], bf16x8 (&fa1)[C::FA],
                           bf16x8 (&fb1)[C::NF], const char* lds, int cur, int nxt, unsigned kb,
-                          unsigned kbp, const XdFrag& f, const XdDma<C>& d) {
-  (xd_step<C, DMA, NEXT, WT, Z, Qs>(acc, fa0, fb0, fa1, fb1, lds, cur, nxt, kb, kbp, f, d), ...);
+                          const XdFrag& f, const XdDma<C>& d) {
+  (xd_step<C, DMA, NEXT, WT, Z, Qs>(acc, fa0, fb0, fa1, fb1, lds, cur, nxt, kb, f, d), ...);
 }
 
 template <class C, bool DMA, bool NEXT, int WT, bool Z = false>
 DRTC_DEVICE void xd_tile(f32x4 (&acc)[C::FA][C::NF], bf16x8 (&fa0)[C::FA], bf16x8 (&fb0)[C::NF],
                          bf16x8 (&fa1)[C::FA], bf16x8 (&fb1)[C::NF], const char* lds, int cur,
-                         int nxt, unsigned kb, unsigned kbp, const XdFrag& f, const XdDma<C>& d) {
+                         int nxt, unsigned kb, const XdFrag& f, const XdDma<C>& d) {
   xd_steps<C, DMA, NEXT, WT, Z>(std::make_integer_sequence<int, 2 * C::H>{}, acc, fa0, fb0, fa1,
-                                fb1, lds, cur, nxt, kb, kbp, f, d);
+                                fb1, lds, cur, nxt, kb, f, d);
 }
 
 // The last S tiles: nothing more to load; WT = S - 2, ..., 0 younger tiles still in flight.
@@ -263,10 +233,10 @@ DRTC_DEVICE void xd_tail(f32x4 (&acc)[C::FA][C::NF], bf16x8 (&fa0)[C::FA], bf16x
                          bf16x8 (&fa1)[C::FA], bf16x8 (&fb1)[C::NF], const char* lds, int cur,
                          const XdFrag& f, const XdDma<C>& d) {
   if constexpr (WT < 0) {
-    xd_tile<C, false, false, 0>(acc, fa0, fb0, fa1, fb1, lds, cur, cur, 0u, 0u, f, d);
+    xd_tile<C, false, false, 0>(acc, fa0, fb0, fa1, fb1, lds, cur, cur, 0u, f, d);
   } else {
     const int nxt = cur + C::STAGE == C::LDS ? 0 : cur + C::STAGE;
-    xd_tile<C, false, true, WT>(acc, fa0, fb0, fa1, fb1, lds, cur, nxt, 0u, 0u, f, d);
+    xd_tile<C, false, true, WT>(acc, fa0, fb0, fa1, fb1, lds, cur, nxt, 0u, f, d);
     xd_tail<C, WT - 1>(acc, fa0, fb0, fa1, fb1, lds, nxt, f, d);
   }
 }
@@ -407,18 +377,6 @@ __global__ __launch_bounds__(kXdThreads, 1) void gemm_xd_kernel(XdParams p) {
     }
     d.lds_a = __builtin_amdgcn_readfirstlane(lds0 + 32 * MT * wv * 128);
     d.lds_b = __builtin_amdgcn_readfirstlane(lds0 + C::BOFF + 8 * NF * wv * 128);
-    if constexpr (C::PF) {
-      // this wave's 8 NF stage rows (lanes past them repeat rows: one L2 request per line)
-      const int R = 8 * NF * wv + lane % (8 * NF);
-      int src = R;
-      if constexpr (xd_glu<EPI>()) {
-        const int w = R / (16 * NF), jb = (R % (16 * NF)) / 16;
-        const int col = w * 8 * NF + (jb % (NF / 2)) * 16 + (R & 15);
-        src = jb < NF / 2 ? col : p.up_off + col;
-      }
-      d.vpf = (unsigned)(src * p.ldb * 2);
-      d.lds_pf = lds0 + C::PF_OFF;
-    }
   }
   XdFrag f;
   {
@@ -435,8 +393,6 @@ __global__ __launch_bounds__(kXdThreads, 1) void gemm_xd_kernel(XdParams p) {
   // ---- prologue: K tiles 0 .. S-1 into the S stages (the launcher guarantees nk > S)
 #pragma unroll
   for (int u = 0; u < C::S; ++u) {
-    if constexpr (C::PF)  // the same [prefetch, DMA group] order as the main loop
-      xd_dma(d.lds_pf, d.vpf, d.rb, (unsigned)min(u + C::PFD, nk - 1) * 128u, true);
 #pragma unroll
     for (int i = 0; i < C::DA; ++i)
       xd_dma(d.lds_a + u * C::STAGE + 1024 * i, d.va[i], d.ra, (unsigned)u * 128u);
@@ -444,21 +400,19 @@ __global__ __launch_bounds__(kXdThreads, 1) void gemm_xd_kernel(XdParams p) {
     for (int i = 0; i < C::DB; ++i)
       xd_dma(d.lds_b + u * C::STAGE + 1024 * i, d.vb[i], d.rb, (unsigned)u * 128u);
   }
-  xd_vmcnt<(C::S - 1) * C::DV>();
+  xd_vmcnt<(C::S - 1) * C::D>();
   xd_barrier();
   bf16x8 fa0[FA], fb0[NF], fa1[FA], fb1[NF];
   xd_reads<C, 0, C::NR>(fa0, fb0, lds, 0, f.ra0, f.rb0);
 
   // ---- main loop: tile t in stage cur; its half 1 DMAs tile t + S into the same stage
   xd_tile<C, true, true, C::S - 2, true>(acc, fa0, fb0, fa1, fb1, lds, 0, C::STAGE % C::LDS,
-                                         (unsigned)C::S * 128u,
-                                         (unsigned)min(C::PFD, nk - 1) * 128u, f, d);
+                                         (unsigned)C::S * 128u, f, d);
   int cur = C::STAGE % C::LDS;
   for (int t = 1; t + C::S < nk; ++t) {
     const int nxt = cur + C::STAGE == C::LDS ? 0 : cur + C::STAGE;
     xd_tile<C, true, true, C::S - 2>(acc, fa0, fb0, fa1, fb1, lds, cur, nxt,
-                                     (unsigned)(t + C::S) * 128u,
-                                     (unsigned)min(t + C::PFD, nk - 1) * 128u, f, d);
+                                     (unsigned)(t + C::S) * 128u, f, d);
     cur = nxt;
   }
   xd_tail<C, C::S - 2>(acc, fa0, fb0, fa1, fb1, lds, cur, f, d);
@@ -559,18 +513,18 @@ int xd_cfg() {
 
 // Forms built (mt, nf) -> ring depth: 128-row tiles nf 2 / 4 / 6 (4 / 4 / 3 stages), 256-row
 // tiles nf 4 / 6 / 8 (3 / 2 / 2 stages); each with and without the split-K combine.
-template <bool SP, bool PF = false>
-using Xd1x2 = XdCfg<1, 2, 4, SP, PF>;
-template <bool SP, bool PF = false>
-using Xd1x4 = XdCfg<1, 4, 4, SP, PF>;
-template <bool SP, bool PF = false>
-using Xd1x6 = XdCfg<1, 6, 3, SP, PF>;
-template <bool SP, bool PF = false>
-using Xd2x4 = XdCfg<2, 4, 3, SP, PF>;
-template <bool SP, bool PF = false>
-using Xd2x6 = XdCfg<2, 6, 2, SP, PF>;
-template <bool SP, bool PF = false>
-using Xd2x8 = XdCfg<2, 8, 2, SP, PF>;
+template <bool SP>
+using Xd1x2 = XdCfg<1, 2, 4, SP>;
+template <bool SP>
+using Xd1x4 = XdCfg<1, 4, 4, SP>;
+template <bool SP>
+using Xd1x6 = XdCfg<1, 6, 3, SP>;
+template <bool SP>
+using Xd2x4 = XdCfg<2, 4, 3, SP>;
+template <bool SP>
+using Xd2x6 = XdCfg<2, 6, 2, SP>;
+template <bool SP>
+using Xd2x8 = XdCfg<2, 8, 2, SP>;
 
 int xd_stages(int mt, int nf) {
   if (mt == 1) return nf == 6 ? 3 : (nf == 2 || nf == 4 ? 4 : 0);
@@ -579,15 +533,7 @@ int xd_stages(int mt, int nf) {
 }
 
 template <bool SP>
-int xd_dispatch(const XdParams& p, int mt, int nf, int epi, bool pf, hipStream_t st) {
-  if (pf) {  // weight prefetch forms: the weight-streaming shapes (small M)
-    switch (mt * 10 + nf) {
-      case 12: return xd_launch<Xd1x2<SP, true>>(p, epi, st);
-      case 14: return xd_launch<Xd1x4<SP, true>>(p, epi, st);
-      case 24: return xd_launch<Xd2x4<SP, true>>(p, epi, st);
-      default: return -1;
-    }
-  }
+int xd_dispatch(const XdParams& p, int mt, int nf, int epi, hipStream_t st) {
   switch (mt * 10 + nf) {
     case 12: return xd_launch<Xd1x2<SP>>(p, epi, st);
     case 14: return xd_launch<Xd1x4<SP>>(p, epi, st);
@@ -609,7 +555,7 @@ int64_t gemm_xd_workspace_bytes(int M, int N, int mt, int nf, int splitk, int gl
 }
 
 int launch_gemm_xd(void* c, const void* a, const void* b, const void* r, int M, int N, int K,
-                   int lda, int ldb, int ldc, int ldr, int epi, int mt, int nf, int splitk, int pf,
+                   int lda, int ldb, int ldc, int ldr, int epi, int mt, int nf, int splitk,
                    void* slab, int64_t slab_bytes, int* counters, int n_counters,
                    hipStream_t st) {
   if (epi < XD_STORE || epi > XD_GELU) return -1;
@@ -646,19 +592,16 @@ int launch_gemm_xd(void* c, const void* a, const void* b, const void* r, int M, 
       return -2;
     p.slab = (float*)slab;
     p.counters = counters;
-    return xd_dispatch<true>(p, mt, nf, epi, pf != 0, st);
+    return xd_dispatch<true>(p, mt, nf, epi, st);
   }
-  return xd_dispatch<false>(p, mt, nf, epi, pf != 0, st);
+  return xd_dispatch<false>(p, mt, nf, epi, st);
 }
 
 int configure_gemm_xd() {
   return xd_cfg<Xd1x2<false>>() | xd_cfg<Xd1x4<false>>() | xd_cfg<Xd1x6<false>>() |
          xd_cfg<Xd2x4<false>>() | xd_cfg<Xd2x6<false>>() | xd_cfg<Xd1x2<true>>() |
          xd_cfg<Xd1x4<true>>() | xd_cfg<Xd1x6<true>>() | xd_cfg<Xd2x4<true>>() |
-         xd_cfg<Xd2x6<true>>() | xd_cfg<Xd2x8<false>>() | xd_cfg<Xd2x8<true>>() |
-         xd_cfg<Xd1x2<false, true>>() | xd_cfg<Xd1x4<false, true>>() |
-         xd_cfg<Xd2x4<false, true>>() | xd_cfg<Xd1x2<true, true>>() |
-         xd_cfg<Xd1x4<true, true>>() | xd_cfg<Xd2x4<true, true>>();
+         xd_cfg<Xd2x6<true>>() | xd_cfg<Xd2x8<false>>() | xd_cfg<Xd2x8<true>>();
 }
 
 }  // namespace drtc

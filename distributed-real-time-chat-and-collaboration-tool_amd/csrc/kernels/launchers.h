@@ -124,9 +124,8 @@ int configure_gemm_w4();
 // tiles ((mt, nf) in (1, 2/4/6), (2, 4/6); gated: 16 nf output columns, nf even), K split over
 // splitk = 1..8 slices (splitk > 1: slab + counters zeroed once, gemm_xd_workspace_bytes), one
 // workgroup per tile and slice; N % tile columns == 0, K % 64 == 0, K / 64 / splitk > ring.
-// pf != 0: the weight-prefetch forms ((mt, nf) in (1, 2), (1, 4), (2, 4)).
 int launch_gemm_xd(void* c, const void* a, const void* b, const void* r, int M, int N, int K,
-                   int lda, int ldb, int ldc, int ldr, int epi, int mt, int nf, int splitk, int pf,
+                   int lda, int ldb, int ldc, int ldr, int epi, int mt, int nf, int splitk,
                    void* slab, int64_t slab_bytes, int* counters, int n_counters,
                    hipStream_t st);
 int64_t gemm_xd_workspace_bytes(int M, int N, int mt, int nf, int splitk, int glu);

@@ -616,17 +616,14 @@ XD_EPI = {"store": 0, "residual": 1, "silu": 2, "gelu_tanh": 3}
 # tile shapes built in gemm_xd.hip, (mt, nf) -> LDS ring depth (128 mt x 32 nf tiles); a form
 # is mt * 100 + nf * 10 + splitk (K split over 1..8 slices)
 XD_TILES = {(1, 2): 4, (1, 4): 4, (1, 6): 3, (2, 4): 3, (2, 6): 2, (2, 8): 2}
-XD_PF_TILES = {(1, 2), (1, 4), (2, 4)}  # built with the weight prefetch (form + 1000)
 XD_MAX_SPLITK = 8
 # the forms the tuner (scripts/tune_xd.py) measures
 XD_FORMS = tuple(sorted([mt * 100 + nf * 10 + 1 for mt, nf in XD_TILES] +
-                        [200 + nf * 10 + sk for nf in (4, 6, 8) for sk in (2, 3, 4)] +
-                        [1121, 1141] + [1240 + sk for sk in (1, 2, 3, 4)]))
+                        [200 + nf * 10 + sk for nf in (4, 6, 8) for sk in (2, 3, 4)]))
 
 
 def xd_form(form: int) -> tuple[int, int, int]:
-    """(mt, nf, splitk) of a form (the thousands digit is the weight-prefetch flag)."""
-    return form // 100 % 10, form // 10 % 10, form % 10
+    return form // 100, form // 10 % 10, form % 10
 
 
 def xd_supported(M: int, N: int, K: int, form: int, glu: bool = False) -> bool:
@@ -634,8 +631,6 @@ def xd_supported(M: int, N: int, K: int, form: int, glu: bool = False) -> bool:
     columns (gated: half the rows of the [gate; up] weight)."""
     mt, nf, sk = xd_form(form)
     if (mt, nf) not in XD_TILES or not 1 <= sk <= XD_MAX_SPLITK or (glu and nf % 2):
-        return False
-    if form // 1000 and (form // 1000 != 1 or (mt, nf) not in XD_PF_TILES):
         return False
     tno = 16 * nf if glu else 32 * nf
     if not (M >= 1 and N % tno == 0 and K % 64 == 0 and K // 64 // sk > XD_TILES[(mt, nf)]):
@@ -692,8 +687,7 @@ def xd_gemm(x: torch.Tensor, w: torch.Tensor, epi: str = "store",
     check(hipk().gemm_xd(out.data_ptr(), x.data_ptr(), w.data_ptr(), ptr(residual), M, N, K,
                          x.stride(0), w.stride(0), out.stride(0),
                          residual.stride(0) if residual is not None else 0, XD_EPI[epi], mt, nf,
-                         sk, form // 1000, ptr(slab), slab.numel() * 4 if slab is not None else 0,
-                         ptr(cnt),
+                         sk, ptr(slab), slab.numel() * 4 if slab is not None else 0, ptr(cnt),
                          cnt.numel() if cnt is not None else 0, stream_ptr(x)), "gemm_xd")
     return out
 

@@ -41,7 +41,7 @@ def main():
     def run(pad, i):
         xa, ws = arms[pad]
         rc = k.gemm_xd(out.data_ptr(), xa.data_ptr(), ws[i % len(ws)].data_ptr(), 0, M, N, K,
-                       K + pad, K + pad, N, 0, 0, 1, a.nf, 1, 0, 0, 0, 0, 0, st)
+                       K + pad, K + pad, N, 0, 0, 1, a.nf, 1, 0, 0, 0, 0, st)
         assert rc == 0, rc
     for pad, (xa, ws) in arms.items():  # correctness
         run(pad, 0)

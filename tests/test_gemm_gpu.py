@@ -344,7 +344,7 @@ def test_xd_gemm_matches_fp32(hipk, epi, form, M, N, K):
 
 
 @pytest.mark.parametrize("act", ["silu", "gelu_tanh"])
-@pytest.mark.parametrize("form", [121, 141, 161, 241, 242, 243, 261, 264, 281, 283, 1141, 1243])
+@pytest.mark.parametrize("form", [121, 141, 161, 241, 242, 243, 261, 264, 281, 283])
 @pytest.mark.parametrize("M,I,K", [(256, 1536, 1024), (200, 768, 1600), (1024, 384, 832)])
 def test_xd_gemm_glu_matches_fp32(hipk, act, form, M, I, K):
     if not G.xd_supported(M, I, K, form, glu=True):
@@ -357,7 +357,7 @@ def test_xd_gemm_glu_matches_fp32(hipk, act, form, M, I, K):
     _check(out, _ref(x, w, act, None))
 
 
-@pytest.mark.parametrize("form", [143, 145, 247, 268, 285, 1123, 1247])
+@pytest.mark.parametrize("form", [143, 145, 247, 268, 285])
 def test_xd_gemm_uneven_splitk(hipk, form):
     """K tiles that the slices do not divide evenly (K / 64 = 61 over 3, 5, 7, 8 slices)."""
     M, N, K = 384, 768, 61 * 64
@@ -403,7 +403,7 @@ def test_xd_gemm_rejects_bad_shapes(hipk):
         y = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
         slab, cnt = ws or (None, None)
         return hipk.gemm_xd(y.data_ptr(), x.data_ptr(), w.data_ptr(), 0, M, N, K, K, K, N, 0,
-                            epi, mt, nf, sk, 0, slab.data_ptr() if slab is not None else 0,
+                            epi, mt, nf, sk, slab.data_ptr() if slab is not None else 0,
                             slab.numel() * 4 if slab is not None else 0,
                             cnt.data_ptr() if cnt is not None else 0,
                             cnt.numel() if cnt is not None else 0, 0)
