@@ -615,6 +615,7 @@ def test_tuned_linear(hipk, M, N, K):
     saved = gemm._table
     try:
         gemm._table = {(M, N, K, K): (r["algo"], 0, 0, 0, 0)}
+        gemm._routes.clear()
         y = ops.linear(x, w)
         _close(y, ref, 2e-2, 2e-2, "tuned linear")
         g = torch.cuda.CUDAGraph()
@@ -626,6 +627,7 @@ def test_tuned_linear(hipk, M, N, K):
         _close(yg, x.float() @ w.float().t(), 2e-2, 2e-2, "tuned linear (graph)")
     finally:
         gemm._table = saved
+        gemm._routes.clear()
 
 
 @pytest.mark.parametrize("M,N,K", [(2304, 1024, 512), (4352, 2048, 1536)])
@@ -717,6 +719,7 @@ def test_skinny_norm_gemm(hipk, M, K, resid, gemma):
     try:
         gemm.NORM_FUSE_MAX_M = 4  # the kernel covers M <= 4; the engine fuses at M = 1
         gemm._table = {(M, N, K, K): (-1, 1, 0, 0, 0)}  # measured pick: dot2 kernel
+        gemm._routes.clear()  # routes are resolved once per shape: re-resolve from this table
         p = ops.PendingNorm(x, res.clone() if resid else None, nw, 1e-5, gemma)
         y = ops.norm_linear(p, w)
         torch.cuda.synchronize()
@@ -725,6 +728,7 @@ def test_skinny_norm_gemm(hipk, M, K, resid, gemma):
         _close(y, y_ref, 3e-2, 2e-2, "norm gemm")
         # unfused path gives the same stream and (within rounding) the same y
         gemm._table = {(M, N, K, K): (-1, 0, 0, 0, 0)}
+        gemm._routes.clear()
         q = ops.PendingNorm(x, res.clone() if resid else None, nw, 1e-5, gemma)
         y2 = ops.norm_linear(q, w)
         assert q._out is not None
@@ -732,6 +736,7 @@ def test_skinny_norm_gemm(hipk, M, K, resid, gemma):
         _close(y2, y, 3e-2, 2e-2, "fused vs unfused")
     finally:
         gemm._table, gemm.NORM_FUSE_MAX_M = saved, saved_max
+        gemm._routes.clear()
 
 
 @pytest.mark.parametrize("M", [1, 2])
@@ -753,6 +758,7 @@ def test_skinny_glu_gemm(hipk, M, I, act):
     try:
         gemm.GLU_FUSE_MAX_M = 2
         gemm._table = {(M, N, I, I): (-1, 1, 0, 0, 0)}
+        gemm._routes.clear()
         y = ops.glu_linear(gu, w, act)
         _close(y, y_ref, 2e-2, 2e-2, "glu gemm")
         y_unfused = gemm.skinny_linear(a, w, 1)
@@ -760,6 +766,7 @@ def test_skinny_glu_gemm(hipk, M, I, act):
         assert torch.equal(y, y_unfused)  # same operand, same kernel order
     finally:
         gemm._table, gemm.GLU_FUSE_MAX_M = saved, saved_max
+        gemm._routes.clear()
 
 
 @pytest.mark.parametrize("e_off,e_local", [(0, 8), (2, 3)])
