@@ -188,6 +188,8 @@ def _resolve(M: int, N: int, K: int, ldx: int) -> tuple[str, int]:
         v = skinny_variant(M, N, K, ldx)
         return ("skinny", v) if v else ("torch", 0)
     _, (algo, sk, midm, xd, _) = found
+    if algo < 0 and not (sk or midm or xd):
+        return ("torch", 0)  # measured: the library's heuristic pick beat every candidate
     if sk and M <= SKINNY_MAX_M and skinny_supports(sk, M, N, K, ldx):
         return ("skinny", sk)
     if xd and xd_supported(M, N, K, xd):
