@@ -7,10 +7,12 @@
 // set by the operand bytes each CU must read: (rows + columns of its tile) x K x 2.  This
 // kernel picks the tile per shape:
 //
-//   * 128 MT x 32 NF output tiles (MT 1 / 2, NF 2 / 4 / 6), K split over splitk = 1..8 slices
+//   * 128 MT x 32 NF output tiles (MT 1 / 2, NF 2 / 4 / 6 / 8), K split over splitk = 1..8 slices
 //     (whole K tiles, as even as they divide), one workgroup per (tile, slice) and per CU
 //     (o / down at M = 1024: 8 x 32 tiles of 128 x 128, or 4 x 32 x 2 slices of 256 x 128;
-//     qkv N = 6144: 8 x 32 of 128 x 192; Llama-3-70B at M = 256: 256 x 128 x 3-4 slices).
+//     qkv N = 6144: 8 x 32 of 128 x 192; Llama-3-70B at M = 256: 256 x 128 x 3-4 slices;
+//     gated gate_up at M = 512-1024: 256 x 256).  Per shape the tuning table picks the form
+//     (scripts/tune_xd.py, ops/gemm.py route / glu_form).
 //   * Tile order partitioned by XCD (workgroup b runs on XCD b % 8 under round-robin dispatch -
 //     used for speed only, the map below is a bijection of blockIdx): XCD x owns one K slice of
 //     a contiguous range of the column-major tile order, i.e. a contiguous set of weight column
