@@ -58,10 +58,11 @@ enum { XD_STORE = 0, XD_RESIDUAL = 1, XD_SILU = 2, XD_GELU = 3 };
 template <int EPI>
 DRTC_DEVICE constexpr bool xd_glu() { return EPI == XD_SILU || EPI == XD_GELU; }
 
-template <int MT_, int NF_, int S_, bool SPLIT_>
+template <int MT_, int NF_, int S_, bool SPLIT_, bool NT_ = false>
 struct XdCfg {
   static constexpr int MT = MT_, NF = NF_, S = S_;
   static constexpr bool SPLIT = SPLIT_;            // split-K combine compiled in
+  static constexpr bool NT = NT_;                  // weight (B) LDS-DMA non-temporal
   static constexpr int TM = 128 * MT;              // tile rows
   static constexpr int TN = 32 * NF;               // tile columns
   static constexpr int FA = 4 * MT;                // A fragments per wave (16 rows each)
@@ -119,15 +120,25 @@ DRTC_DEVICE bf16x8 xd_rd(const char* lds, int off) {
   return *reinterpret_cast<const bf16x8*>(lds + off);
 }
 
-// One LDS-DMA wave-instruction outside the main loop: M0 saved and restored.
+// One LDS-DMA wave-instruction outside the main loop: M0 saved and restored.  NT: the
+// non-temporal policy (a weight byte that one CU reads once, MI355X_MICROARCH.md nt-weights).
+template <bool NT = false>
 DRTC_DEVICE void xd_dma(unsigned dst, unsigned voff, __amdgpu_buffer_rsrc_t rsrc, unsigned soff) {
   unsigned keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
-      "buffer_load_dwordx4 %2, %3, %4 offen lds\n\ts_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "s"(dst), "v"(voff), "s"(rsrc), "s"(soff)
-      : "memory");
+  if constexpr (NT)
+    asm volatile(
+        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
+        "buffer_load_dwordx4 %2, %3, %4 offen nt lds\n\ts_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "s"(dst), "v"(voff), "s"(rsrc), "s"(soff)
+        : "memory");
+  else
+    asm volatile(
+        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
+        "buffer_load_dwordx4 %2, %3, %4 offen lds\n\ts_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "s"(dst), "v"(voff), "s"(rsrc), "s"(soff)
+        : "memory");
 }
 
 // Fragment r of a K half in consumption order (A row block 0, every B column block, then the
@@ -166,8 +177,12 @@ DRTC_DEVICE void xd_dma_step(const XdDma<C>& d, int cur, unsigned kb) {
   } else {
     if constexpr (Sd == C::DA)
       asm volatile("s_mov_b32 m0, %0\n\ts_nop 0" : : "s"(d.lds_b + cur) : "memory");
-    asm volatile("buffer_load_dwordx4 %0, %1, %2 offen lds"
-                 : : "v"(d.vb[Sd - C::DA]), "s"(d.rb), "s"(kb) : "memory");
+    if constexpr (C::NT)
+      asm volatile("buffer_load_dwordx4 %0, %1, %2 offen nt lds"
+                   : : "v"(d.vb[Sd - C::DA]), "s"(d.rb), "s"(kb) : "memory");
+    else
+      asm volatile("buffer_load_dwordx4 %0, %1, %2 offen lds"
+                   : : "v"(d.vb[Sd - C::DA]), "s"(d.rb), "s"(kb) : "memory");
     if constexpr (Sd + 1 < C::D) asm volatile("s_add_u32 m0, m0, 0x400" ::: "memory");
   }
 }
@@ -400,7 +415,7 @@ __global__ __launch_bounds__(kXdThreads, 1) void gemm_xd_kernel(XdParams p) {
       xd_dma(d.lds_a + u * C::STAGE + 1024 * i, d.va[i], d.ra, (unsigned)u * 128u);
 #pragma unroll
     for (int i = 0; i < C::DB; ++i)
-      xd_dma(d.lds_b + u * C::STAGE + 1024 * i, d.vb[i], d.rb, (unsigned)u * 128u);
+      xd_dma<C::NT>(d.lds_b + u * C::STAGE + 1024 * i, d.vb[i], d.rb, (unsigned)u * 128u);
   }
   xd_vmcnt<(C::S - 1) * C::D>();
   xd_barrier();
@@ -515,18 +530,20 @@ int xd_cfg() {
 
 // Forms built (mt, nf) -> ring depth: 128-row tiles nf 2 / 4 / 6 (4 / 4 / 3 stages), 256-row
 // tiles nf 4 / 6 / 8 (3 / 2 / 2 stages); each with and without the split-K combine.
-template <bool SP>
-using Xd1x2 = XdCfg<1, 2, 4, SP>;
-template <bool SP>
-using Xd1x4 = XdCfg<1, 4, 4, SP>;
-template <bool SP>
-using Xd1x6 = XdCfg<1, 6, 3, SP>;
-template <bool SP>
-using Xd2x4 = XdCfg<2, 4, 3, SP>;
-template <bool SP>
-using Xd2x6 = XdCfg<2, 6, 2, SP>;
-template <bool SP>
-using Xd2x8 = XdCfg<2, 8, 2, SP>;
+// The 128 x 128 .. 256 x 256 tiles also with non-temporal weight loads (decode batches of one
+// row tile, where each weight byte enters one CU once).
+template <bool SP, bool NT = false>
+using Xd1x2 = XdCfg<1, 2, 4, SP, NT>;
+template <bool SP, bool NT = false>
+using Xd1x4 = XdCfg<1, 4, 4, SP, NT>;
+template <bool SP, bool NT = false>
+using Xd1x6 = XdCfg<1, 6, 3, SP, NT>;
+template <bool SP, bool NT = false>
+using Xd2x4 = XdCfg<2, 4, 3, SP, NT>;
+template <bool SP, bool NT = false>
+using Xd2x6 = XdCfg<2, 6, 2, SP, NT>;
+template <bool SP, bool NT = false>
+using Xd2x8 = XdCfg<2, 8, 2, SP, NT>;
 
 int xd_stages(int mt, int nf) {
   if (mt == 1) return nf == 6 ? 3 : (nf == 2 || nf == 4 ? 4 : 0);
@@ -535,7 +552,17 @@ int xd_stages(int mt, int nf) {
 }
 
 template <bool SP>
-int xd_dispatch(const XdParams& p, int mt, int nf, int epi, hipStream_t st) {
+int xd_dispatch(const XdParams& p, int mt, int nf, bool nt, int epi, hipStream_t st) {
+  if (nt) {
+    switch (mt * 10 + nf) {
+      case 14: return xd_launch<Xd1x4<SP, true>>(p, epi, st);
+      case 16: return xd_launch<Xd1x6<SP, true>>(p, epi, st);
+      case 24: return xd_launch<Xd2x4<SP, true>>(p, epi, st);
+      case 26: return xd_launch<Xd2x6<SP, true>>(p, epi, st);
+      case 28: return xd_launch<Xd2x8<SP, true>>(p, epi, st);
+      default: return -1;
+    }
+  }
   switch (mt * 10 + nf) {
     case 12: return xd_launch<Xd1x2<SP>>(p, epi, st);
     case 14: return xd_launch<Xd1x4<SP>>(p, epi, st);
@@ -560,6 +587,8 @@ int launch_gemm_xd(void* c, const void* a, const void* b, const void* r, int M, 
                    int lda, int ldb, int ldc, int ldr, int epi, int mt, int nf, int splitk,
                    void* slab, int64_t slab_bytes, int* counters, int n_counters,
                    hipStream_t st) {
+  const bool nt = (mt & 16) != 0;  // mt bit 4: non-temporal weight loads
+  mt &= 15;
   if (epi < XD_STORE || epi > XD_GELU) return -1;
   const bool glu = epi == XD_SILU || epi == XD_GELU;
   const int stages = xd_stages(mt, nf);
@@ -594,16 +623,21 @@ int launch_gemm_xd(void* c, const void* a, const void* b, const void* r, int M, 
       return -2;
     p.slab = (float*)slab;
     p.counters = counters;
-    return xd_dispatch<true>(p, mt, nf, epi, st);
+    return xd_dispatch<true>(p, mt, nf, nt, epi, st);
   }
-  return xd_dispatch<false>(p, mt, nf, epi, st);
+  return xd_dispatch<false>(p, mt, nf, nt, epi, st);
 }
 
 int configure_gemm_xd() {
   return xd_cfg<Xd1x2<false>>() | xd_cfg<Xd1x4<false>>() | xd_cfg<Xd1x6<false>>() |
          xd_cfg<Xd2x4<false>>() | xd_cfg<Xd2x6<false>>() | xd_cfg<Xd1x2<true>>() |
          xd_cfg<Xd1x4<true>>() | xd_cfg<Xd1x6<true>>() | xd_cfg<Xd2x4<true>>() |
-         xd_cfg<Xd2x6<true>>() | xd_cfg<Xd2x8<false>>() | xd_cfg<Xd2x8<true>>();
+         xd_cfg<Xd2x6<true>>() | xd_cfg<Xd2x8<false>>() | xd_cfg<Xd2x8<true>>() |
+         xd_cfg<Xd1x4<false, true>>() | xd_cfg<Xd1x6<false, true>>() |
+         xd_cfg<Xd2x4<false, true>>() | xd_cfg<Xd2x6<false, true>>() |
+         xd_cfg<Xd2x8<false, true>>() | xd_cfg<Xd1x4<true, true>>() |
+         xd_cfg<Xd1x6<true, true>>() | xd_cfg<Xd2x4<true, true>>() |
+         xd_cfg<Xd2x6<true, true>>() | xd_cfg<Xd2x8<true, true>>();
 }
 
 }  // namespace drtc

@@ -61,6 +61,10 @@ _enabled = os.environ.get("DRTC_TUNED_GEMM", "1") != "0"
 _prefill_enabled = os.environ.get("DRTC_PREFILL_TUNED", "1") != "0"
 _midm_enabled = os.environ.get("DRTC_MIDM_GEMM", "1") != "0"
 _xd_enabled = os.environ.get("DRTC_XD_GEMM", "1") != "0"
+# tuned gemm_xd forms whose batch fits one row tile take non-temporal weight loads (each weight
+# byte enters one CU once: MI355X_MICROARCH.md nt-weights; profiles/r4aa: Llama-3-70B down at
+# M = 256 159.6 -> 136.8 us, gated gate_up 265.7 -> 230.2, the 70B ask wave +5.2 %)
+_xd_nt = os.environ.get("DRTC_XD_NT", "1") != "0"
 # decode batches up to this many rows may take the skinny kernel: the table's choice where
 # the shape was measured, skinny_variant()'s default otherwise; 0 disables it
 SKINNY_MAX_M = int(os.environ.get("DRTC_SKINNY_MAX_M", "16"))
@@ -102,8 +106,8 @@ def _activate() -> dict:
                     continue
                 tab[(M, N, K, ldx)] = (int(e.get("algo", -1)), int(e.get("skinny", 0)),
                                        int(e.get("midm", 0)) if _midm_enabled else 0,
-                                       int(e.get("xd", 0)) if _xd_enabled else 0,
-                                       int(e.get("xd_glu", 0)) if _xd_enabled else 0)
+                                       _xd_policy(M, int(e.get("xd", 0))),
+                                       _xd_policy(M, int(e.get("xd_glu", 0))))
         for v in pre.values():
             v.sort()
         _prefill.clear()
@@ -112,6 +116,23 @@ def _activate() -> dict:
         _routes.clear()
         _table = tab
     return _table
+
+
+def xd_nt_ok(M: int, form: int) -> bool:
+    """Whether ``form`` (plain) has a non-temporal build and M fits one of its row tiles."""
+    mt, nf, _ = xd_form(form)
+    return form < 1000 and (mt, nf) in XD_NT_TILES and M <= 128 * mt
+
+
+def _xd_policy(M: int, form: int) -> int:
+    """A tuned gemm_xd form as the router runs it (0: none / gemm_xd disabled): a plain form
+    the tuner picked before the non-temporal forms existed takes its non-temporal twin where
+    the batch fits one row tile (DRTC_XD_NT=0 keeps the plain form)."""
+    if not (_xd_enabled and form):
+        return 0
+    if _xd_nt and xd_nt_ok(M, form):
+        return form + 1000
+    return form
 
 
 def reset() -> None:
@@ -616,8 +637,10 @@ def norm_glu(p, w: torch.Tensor, act: str = "silu") -> torch.Tensor:
 # ------------------------------------------------------------------ XCD-partitioned decode GEMM
 XD_EPI = {"store": 0, "residual": 1, "silu": 2, "gelu_tanh": 3}
 # tile shapes built in gemm_xd.hip, (mt, nf) -> LDS ring depth (128 mt x 32 nf tiles); a form
-# is mt * 100 + nf * 10 + splitk (K split over 1..8 slices)
+# is mt * 100 + nf * 10 + splitk (K split over 1..8 slices), + 1000 for non-temporal weight
+# loads (the tiles of XD_NT_TILES)
 XD_TILES = {(1, 2): 4, (1, 4): 4, (1, 6): 3, (2, 4): 3, (2, 6): 2, (2, 8): 2}
+XD_NT_TILES = {(1, 4), (1, 6), (2, 4), (2, 6), (2, 8)}
 XD_MAX_SPLITK = 8
 # the forms the tuner (scripts/tune_xd.py) measures
 XD_FORMS = tuple(sorted([mt * 100 + nf * 10 + 1 for mt, nf in XD_TILES] +
@@ -625,7 +648,12 @@ XD_FORMS = tuple(sorted([mt * 100 + nf * 10 + 1 for mt, nf in XD_TILES] +
 
 
 def xd_form(form: int) -> tuple[int, int, int]:
-    return form // 100, form // 10 % 10, form % 10
+    return form % 1000 // 100, form // 10 % 10, form % 10
+
+
+def xd_nt(form: int) -> bool:
+    """Form with non-temporal weight loads (MI355X_MICROARCH.md nt-weights)."""
+    return form >= 1000
 
 
 def xd_supported(M: int, N: int, K: int, form: int, glu: bool = False) -> bool:
@@ -633,6 +661,8 @@ def xd_supported(M: int, N: int, K: int, form: int, glu: bool = False) -> bool:
     columns (gated: half the rows of the [gate; up] weight)."""
     mt, nf, sk = xd_form(form)
     if (mt, nf) not in XD_TILES or not 1 <= sk <= XD_MAX_SPLITK or (glu and nf % 2):
+        return False
+    if form // 1000 > 1 or (xd_nt(form) and (mt, nf) not in XD_NT_TILES):
         return False
     tno = 16 * nf if glu else 32 * nf
     if not (M >= 1 and N % tno == 0 and K % 64 == 0 and K // 64 // sk > XD_TILES[(mt, nf)]):
@@ -670,7 +700,7 @@ def xd_gemm(x: torch.Tensor, w: torch.Tensor, epi: str = "store",
     its own weight column panels through its L2 for every row tile).  epi "store";
     "residual" (``out`` may be ``residual``); "silu" / "gelu_tanh": w is the fused [gate; up]
     weight [2I, K] and y[:, n] = act(x . gate_n) * (x . up_n).  ``form`` = mt * 100 +
-    nf * 10 + splitk (0: ``xd_default_form``)."""
+    nf * 10 + splitk (+ 1000: non-temporal weight loads; 0: ``xd_default_form``)."""
     M, K = x.shape
     glu = epi in ("silu", "gelu_tanh")
     N = w.shape[0] // 2 if glu else w.shape[0]
@@ -688,7 +718,8 @@ def xd_gemm(x: torch.Tensor, w: torch.Tensor, epi: str = "store",
     slab, cnt = ((ws or gemm_workspace(x.device)) if sk > 1 else (None, None))
     check(hipk().gemm_xd(out.data_ptr(), x.data_ptr(), w.data_ptr(), ptr(residual), M, N, K,
                          x.stride(0), w.stride(0), out.stride(0),
-                         residual.stride(0) if residual is not None else 0, XD_EPI[epi], mt, nf,
+                         residual.stride(0) if residual is not None else 0, XD_EPI[epi],
+                         mt | (16 if xd_nt(form) else 0), nf,
                          sk, ptr(slab), slab.numel() * 4 if slab is not None else 0, ptr(cnt),
                          cnt.numel() if cnt is not None else 0, stream_ptr(x)), "gemm_xd")
     return out

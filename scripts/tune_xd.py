@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Measure the XCD-partitioned decode GEMM (csrc/kernels/gemm_xd.hip) against the engine's
 path without it (ops.linear: tuned hipBLASLt / midm / F.linear) for every decode projection
-of a model at the larger decode buckets, and write a tuning entry {"xd": form} where the hand
+of a model at the larger decode buckets (forms with non-temporal weight loads, form + 1000,
+where the batch fits one row tile), and write a tuning entry {"xd": form} where the hand
 kernel wins by at least --min-gain; for gate_up below the fused-GLU gemm_w4 batches also the
 GLU epilogue form against the route + act_glu ({"xd_glu": form}).
 
@@ -33,6 +34,8 @@ def measure(G, x, ws, N, K, epi, base_fn, name, model, tp, M):
     (epi "store" or a GLU: N = output columns); print and return the record."""
     glu = epi != "store"
     forms = [f for f in G.XD_FORMS if G.xd_supported(M, N, K, f, glu)]
+    # non-temporal weight loads where the batch fits one row tile (nobody re-reads a weight)
+    forms += [f + 1000 for f in forms if G.xd_nt_ok(M, f)]
     if not forms:
         return None
     base = time_arm(base_fn, ws)

@@ -357,6 +357,31 @@ def test_xd_gemm_glu_matches_fp32(hipk, act, form, M, I, K):
     _check(out, _ref(x, w, act, None))
 
 
+@pytest.mark.parametrize("epi", ["store", "residual", "silu"])
+@pytest.mark.parametrize("form", [1141, 1161, 1241, 1244, 1261, 1281, 1282])
+def test_xd_gemm_nontemporal_weights_match_fp32(hipk, epi, form):
+    """Forms with non-temporal weight loads (form + 1000): same numerics as the plain form."""
+    glu = epi == "silu"
+    M, N, K = 256, 1536, 2048
+    assert G.xd_supported(M, N, K, form, glu) and G.xd_nt(form)
+    g = torch.Generator(device="cuda").manual_seed(form)
+    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16, generator=g)
+    w = torch.randn(2 * N if glu else N, K, device="cuda", dtype=torch.bfloat16, generator=g) * 0.05
+    res = torch.randn(M, N, device="cuda", dtype=torch.bfloat16, generator=g) \
+        if epi == "residual" else None
+    out = G.xd_gemm(x, w, epi, residual=res.clone() if res is not None else None, form=form)
+    plain = G.xd_gemm(x, w, epi, residual=res.clone() if res is not None else None,
+                      form=form - 1000)
+    torch.cuda.synchronize()
+    _check(out, _ref(x, w, epi, res))
+    assert torch.equal(out, plain)
+
+
+def test_xd_nontemporal_forms_rejected_outside_built_tiles():
+    assert not G.xd_supported(256, 1536, 2048, 1121)  # 128 x 64 tile: no nt build
+    assert not G.xd_supported(256, 1536, 2048, 2241)
+
+
 @pytest.mark.parametrize("form", [143, 145, 247, 268, 285])
 def test_xd_gemm_uneven_splitk(hipk, form):
     """K tiles that the slices do not divide evenly (K / 64 = 61 over 3, 5, 7, 8 slices)."""
