@@ -371,7 +371,7 @@ def test_default_engine_batch_per_model():
     assert default_max_batch("llama-3-8b") == 1024
     assert default_max_batch("mixtral-8x7b") == 1024
     assert default_max_batch("gemma-2b") == 2048
-    assert default_max_batch("llama-3-70b") == 192      # p50 9.45 s < 10 s ask-AI deadline
+    assert default_max_batch("llama-3-70b") == 224      # p50 9.15 s < 10 s ask-AI deadline
     assert default_max_batch("llama-3-70b", tp=8) == 256
     assert default_max_batch("tiny-llama") == 256
 
