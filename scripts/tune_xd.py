@@ -29,13 +29,15 @@ from tune_midm import time_arm  # noqa: E402
 BUCKETS = (128, 160, 192, 224, 256, 320, 384, 448, 512, 640, 768, 896, 1024)
 
 
-def measure(G, x, ws, N, K, epi, base_fn, name, model, tp, M):
+def measure(G, x, ws, N, K, epi, base_fn, name, model, tp, M, nt_any=False):
     """Time the engine's current route (base_fn) and every gemm_xd form for one shape
     (epi "store" or a GLU: N = output columns); print and return the record."""
     glu = epi != "store"
     forms = [f for f in G.XD_FORMS if G.xd_supported(M, N, K, f, glu)]
     # non-temporal weight loads where the batch fits one row tile (nobody re-reads a weight)
-    forms += [f + 1000 for f in forms if G.xd_nt_ok(M, f)]
+    # (--nt-any: at every M, for the tiles built with them)
+    forms += [f + 1000 for f in forms
+              if G.xd_nt_ok(M, f) or (nt_any and G.xd_supported(M, N, K, f + 1000, glu))]
     if not forms:
         return None
     base = time_arm(base_fn, ws)
@@ -69,6 +71,9 @@ def main() -> None:
     ap.add_argument("--min-gain", type=float, default=0.03)
     ap.add_argument("--out", default="gpurun_out/xd_tuned.json")
     ap.add_argument("--gemms", default="qkv,o,gate_up,down", help="projections to tune")
+    ap.add_argument("--nt-any", action="store_true",
+                    help="non-temporal forms among the candidates at every M, not only where "
+                         "the batch fits one row tile")
     a = ap.parse_args()
     from drtc_amd import ops
     from drtc_amd.ops import gemm as G
@@ -95,7 +100,8 @@ def main() -> None:
                 key = f"{M},{N},{K},{K}"
                 ent = {}
                 # plain projection (ops.linear) against the engine's route without gemm_xd
-                rec = measure(G, x, ws, N, K, "store", lambda w: G.linear(x, w), name, model, tp, M)
+                rec = measure(G, x, ws, N, K, "store", lambda w: G.linear(x, w), name, model, tp, M,
+                              a.nt_any)
                 if rec and rec["xd_us"] < rec["base_us"] * (1 - a.min_gain):
                     ent.update(xd=rec["xd_form"], xd_us=rec["xd_us"], xd_base_us=rec["base_us"])
                 # gate_up with the GLU in the epilogue against norm_glu's route without gemm_xd
@@ -109,7 +115,7 @@ def main() -> None:
                     else:
                         def glu_base(w, act=act):
                             return ops.act_glu(G.linear(x, w), act)
-                    rec = measure(G, x, ws, N // 2, K, act, glu_base, name, model, tp, M)
+                    rec = measure(G, x, ws, N // 2, K, act, glu_base, name, model, tp, M, a.nt_any)
                     if rec and rec["xd_us"] < rec["base_us"] * (1 - a.min_gain):
                         ent.update(xd_glu=rec["xd_form"], xd_glu_us=rec["xd_us"],
                                    xd_glu_base_us=rec["base_us"])
