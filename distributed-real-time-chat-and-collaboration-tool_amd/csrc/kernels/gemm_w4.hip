@@ -75,6 +75,9 @@ struct W4Params {
   int up_off;
   int group_m;
   int xk;  // K-slice-by-XCD tile order (split-K forms; see gemm_w4_kernel)
+  int* err;        // split-K fault word: the workspace's last counter, outside every ticket
+                   // range; read and cleared by the host
+  int spin_limit;  // bound of the parallel combine's arrival poll (< 0: test hook, always fault)
 };
 
 template <int EPI>
@@ -421,19 +424,23 @@ DRTC_DEVICE void w4_splitk_par(const W4Params& p, f32x4 (&acc)[8][8], int tile, 
   __syncthreads();
   int* arrive = p.counters + 2 * tile;
   int* depart = arrive + 1;
+  __shared__ int faulted;
   if (threadIdx.x == 0) {
     __hip_atomic_fetch_add(arrive, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    int spins = 0;
-    while (__hip_atomic_load(arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < sk) {
+    int spins = 0, fault = 0;
+    while (p.spin_limit < 0 ||
+           __hip_atomic_load(arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < sk) {
       __builtin_amdgcn_s_sleep(1);
-      if (++spins > (1 << 24)) {  // a slice never arrived: give up (never hang the GPU)
-        __hip_atomic_store(p.counters + 2 * p.tiles_m * p.tiles_n, 1, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
+      if (++spins > p.spin_limit) {  // a slice never arrived: give up (never hang the GPU)
+        __hip_atomic_store(p.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        fault = 1;
         break;
       }
     }
+    faulted = fault;
   }
   __syncthreads();
+  const bool rearm = !faulted;  // after a fault the counters stay as they are (host resets)
   // my row band: thread t takes column chunk t & 31 (8 columns) of rows band0 + t / 32 + 8 k
   const int band = 256 / sk, band0 = slice * band;
   const int t = threadIdx.x, cc = t & 31;
@@ -480,7 +487,7 @@ DRTC_DEVICE void w4_splitk_par(const W4Params& p, f32x4 (&acc)[8][8], int tile, 
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (threadIdx.x == 0) {
+  if (threadIdx.x == 0 && rearm) {
     const int d = __hip_atomic_fetch_add(depart, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (d == sk - 1) {  // every slice of the tile has read the slabs: re-arm
       __hip_atomic_store(arrive, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -809,9 +816,12 @@ int launch_gemm_w4(void* c, const void* a, const void* b, const void* r, int M, 
   }
   if (splitk > 1) {
     const int64_t tiles = (int64_t)p.tiles_m * p.tiles_n;
-    if (slab == nullptr || counters == nullptr || n_counters < 2 * tiles + 1 ||
+    // tile counters [0, 2 tiles) and the error word at the workspace's last slot
+    if (slab == nullptr || counters == nullptr || n_counters < 2 * tiles + 2 ||
         slab_bytes < tiles * splitk * 64ll * kW4Threads * 16)
       return -2;
+    p.err = counters + n_counters - 1;
+    p.spin_limit = splitk_spin_limit();
     // parallel combine: slices wait for each other, so every workgroup must be resident at
     // once (one per CU: the LDS ring) and a row band per slice (splitk | 256)
     if ((v & 4) && (256 % splitk || tiles * splitk > w4_num_cus())) return -1;

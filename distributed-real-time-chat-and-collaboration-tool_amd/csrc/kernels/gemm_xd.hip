@@ -90,6 +90,9 @@ struct XdParams {
   int lda, ldb, ldc, ldr;
   int tiles_m, tiles_n, per_xcd;
   int splitk, up_off;
+  int* err;        // split-K fault word: a fixed slot of the workspace (the last counter),
+                   // outside every launch's ticket range; read and cleared by the host
+  int spin_limit;  // bound of the last ticket's ready poll (< 0: test hook, always fault)
 };
 
 template <class C>
@@ -259,11 +262,12 @@ DRTC_DEVICE void xd_tail(f32x4 (&acc)[C::FA][C::NF], bf16x8 (&fa0)[C::FA], bf16x
 }
 
 // Split-K, ticket-first combine (see the file comment).  Counters of tile t: [2 t] ticket,
-// [2 t + 1] ready count; [2 tiles] the error word (a partial that never arrived).  The slab
-// holds one partial slot per slice and tile.  Returns false for a slice that published its
-// partial (it is done), true for the last ticket, which sums the slices inside the epilogue
-// (xd_sum: one fragment at a time, so the accumulators stay in place) and re-arms the
-// counters.
+// [2 t + 1] ready count; the error word p.err is a fixed slot outside every ticket range (a
+// partial that never arrived).  The slab holds one partial slot per slice and tile.  Returns
+// 0 for a slice that published its partial (it is done), 1 for the last ticket, which sums
+// the slices inside the epilogue (xd_sum: one fragment at a time, so the accumulators stay in
+// place) and re-arms the counters, 2 for a last ticket whose poll timed out: it records the
+// fault and does NOT re-arm (the host reads the word, zeroes the counters and raises).
 template <class C>
 constexpr int xd_tile_bytes() { return C::FA * C::NF * kXdThreads * 16; }
 constexpr int kXdSc1 = 16;  // cache-policy bits of the buffer op: sc1 (write-through)
@@ -277,8 +281,8 @@ DRTC_DEVICE __amdgpu_buffer_rsrc_t xd_slab(const XdParams& p, int tile) {
 }
 
 template <class C>
-DRTC_DEVICE bool xd_combine(const XdParams& p, f32x4 (&acc)[C::FA][C::NF], int tile, int slice,
-                            char* lds) {
+DRTC_DEVICE int xd_combine(const XdParams& p, f32x4 (&acc)[C::FA][C::NF], int tile, int slice,
+                           char* lds) {
   const __amdgpu_buffer_rsrc_t slab = xd_slab<C>(p, tile);
   int* ticket = p.counters + 2 * tile;
   int* ready = ticket + 1;
@@ -303,22 +307,25 @@ DRTC_DEVICE bool xd_combine(const XdParams& p, f32x4 (&acc)[C::FA][C::NF], int t
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) __hip_atomic_fetch_add(ready, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return false;
+    return 0;
   }
   // the last ticket: every other slice holds a ticket (resident, past its K loop)
+  __syncthreads();  // every wave has read the ticket before the flag word is reused
   if (tid == 0) {
-    int spins = 0;
-    while (__hip_atomic_load(ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < p.splitk - 1) {
+    int spins = 0, fault = 0;
+    while (p.spin_limit < 0 ||
+           __hip_atomic_load(ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < p.splitk - 1) {
       __builtin_amdgcn_s_sleep(1);
-      if (++spins > (1 << 24)) {  // never hang the GPU: record the fault and go on
-        __hip_atomic_store(p.counters + 2 * p.tiles_m * p.tiles_n, 1, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
+      if (++spins > p.spin_limit) {  // never hang the GPU: record the fault, keep the counters
+        __hip_atomic_store(p.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        fault = 1;
         break;
       }
     }
+    *flag = fault;
   }
   __syncthreads();
-  return true;
+  return *flag ? 2 : 1;
 }
 
 // Fragment (i, j) of the tile summed over the slices in slice order; `own` (this workgroup's
@@ -435,10 +442,13 @@ __global__ __launch_bounds__(kXdThreads, 1) void gemm_xd_kernel(XdParams p) {
   xd_tail<C, C::S - 2>(acc, fa0, fb0, fa1, fb1, lds, cur, f, d);
   xd_vmcnt<0>();
 
-  bool part = false;  // split-K: this workgroup adds the other slices' partials
+  bool part = false;   // split-K: this workgroup adds the other slices' partials
+  bool rearm = false;  // ... and re-arms the tile's counters (not after a fault)
   if constexpr (C::SPLIT) {
-    if (!xd_combine<C>(p, acc, tile, slice, xd_lds)) return;
+    const int st = xd_combine<C>(p, acc, tile, slice, xd_lds);
+    if (st == 0) return;
     part = true;
+    rearm = st == 1;
   }
 
   // ---- epilogue: the wave's tile as bf16 into LDS, then 16-B global stores of whole row
@@ -476,7 +486,7 @@ __global__ __launch_bounds__(kXdThreads, 1) void gemm_xd_kernel(XdParams p) {
       }
     }
   }
-  if (C::SPLIT && part && threadIdx.x == 0) {
+  if (C::SPLIT && rearm && threadIdx.x == 0) {
     // re-arm (the next launch on this stream starts after this one ends)
     __hip_atomic_store(p.counters + 2 * tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(p.counters + 2 * tile + 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -574,7 +584,12 @@ int xd_dispatch(const XdParams& p, int mt, int nf, bool nt, int epi, hipStream_t
   }
 }
 
+int g_spin_limit = 1 << 24;
+
 }  // namespace
+
+int splitk_spin_limit() { return g_spin_limit; }
+void set_splitk_spin_limit(int limit) { g_spin_limit = limit; }
 
 int64_t gemm_xd_workspace_bytes(int M, int N, int mt, int nf, int splitk, int glu) {
   if (splitk < 2 || mt < 1 || nf < 1) return 0;
@@ -618,11 +633,14 @@ int launch_gemm_xd(void* c, const void* a, const void* b, const void* r, int M, 
   if (tiles * splitk * 8 >= (1ll << 31)) return -1;
   p.per_xcd = (int)((tiles * splitk + 7) / 8);
   if (splitk > 1) {
-    if (slab == nullptr || counters == nullptr || n_counters < 2 * tiles + 1 ||
+    // tile counters [0, 2 tiles) and the error word at the workspace's last slot
+    if (slab == nullptr || counters == nullptr || n_counters < 2 * tiles + 2 ||
         slab_bytes < gemm_xd_workspace_bytes(M, N, mt, nf, splitk, glu))
       return -2;
     p.slab = (float*)slab;
     p.counters = counters;
+    p.err = counters + n_counters - 1;
+    p.spin_limit = splitk_spin_limit();
     return xd_dispatch<true>(p, mt, nf, nt, epi, st);
   }
   return xd_dispatch<false>(p, mt, nf, nt, epi, st);

@@ -66,7 +66,7 @@ class LLMEngine:
     def __init__(self, model: TransformerLM, max_batch: int = 256, max_model_len: int = 4096,
                  max_prefill_tokens: int = 16384, num_blocks: int | None = None,
                  kv_fraction: float = 0.85, use_graphs: bool = True, seed: int = 0,
-                 buckets=DEFAULT_BUCKETS):
+                 buckets=DEFAULT_BUCKETS, hbm_budget: float | None = None):
         self.model = model
         cfg = model.cfg
         self.cfg = cfg
@@ -79,8 +79,13 @@ class LLMEngine:
         # chunks: equal tok/s, p50 TTFT 0.85 / 1.02 / 1.37 s
         self.prefill_chunk_tokens = int(os.environ.get("DRTC_PREFILL_CHUNK", "16384"))
         self.max_blocks = math.ceil(self.max_model_len / BS)
+        # hbm_budget: the fraction of the GPU's HBM this engine may hold (engine groups that
+        # share a GPU, llm.server --serve ...:mem=F); every TP / EP rank gets the same
+        # fraction and the ranks agree on the smallest resulting block count
+        self.hbm_budget = hbm_budget
         if num_blocks is None:
-            num_blocks = PagedKVCache.auto_num_blocks(cfg, model.sh.hkv, self.device, kv_fraction)
+            num_blocks = PagedKVCache.auto_num_blocks(cfg, model.sh.hkv, self.device, kv_fraction,
+                                                      hbm_budget=hbm_budget)
         # lockstep (SPMD) TP/EP ranks must schedule identically: every rank
         # sizes its cache from the same (smallest) block count
         num_blocks = model.pc.agree_min(num_blocks)
@@ -142,6 +147,7 @@ class LLMEngine:
         self.admit_gap_s = float(os.environ.get("DRTC_ADMIT_GAP_MS", "3")) / 1000.0
         self.admit_max_delay_s = float(os.environ.get("DRTC_ADMIT_MAX_MS", "100")) / 1000.0
         self._last_arrival = 0.0
+        self._steps = 0  # scheduler steps (health checks every HEALTH_EVERY)
 
     # ------------------------------------------------------------ API
     def add_request(self, req: Request) -> Request:
@@ -214,9 +220,23 @@ class LLMEngine:
         return done
 
     def warmup(self, capture: bool = True, up_to: int | None = None) -> None:
-        """Capture decode graphs up front (zeroed staging: no cache reads/writes)."""
+        """Capture decode graphs up front (zeroed staging: no cache reads/writes), then check
+        the split-K fault word of the GEMM workspaces (the capture's eager warm-up ran every
+        split-K form the graphs hold)."""
         if capture and self.runner.use_graphs:
             self.runner.capture_all(up_to)
+        self.check_health()
+
+    # steps between two split-K fault checks while serving (each is one device sync)
+    HEALTH_EVERY = int(os.environ.get("DRTC_HEALTH_EVERY", "512"))
+
+    def check_health(self) -> None:
+        """Raise ops.gemm.SplitKFault if a split-K GEMM combine on this engine's device timed
+        out since the last check (its output was wrong; the workspace counters are reset)."""
+        if self.device.type == "cuda":
+            from ..ops import gemm as _gemm
+
+            _gemm.check_splitk_fault(self.device)
 
     def generate(self, prompts: list[list[int]], params: SamplingParams | list) -> list[Request]:
         if isinstance(params, SamplingParams):
@@ -277,6 +297,9 @@ class LLMEngine:
         """Serving metrics: TTFT / TPOT / end-to-end latency per finished
         request, KV-cache occupancy and queue depths per step."""
         M = METRICS
+        self._steps += 1
+        if self.HEALTH_EVERY > 0 and self._steps % self.HEALTH_EVERY == 0:
+            self.check_health()
         if done:
             M.observe_many("engine.ttft_s", [r.ttft for r in done])
             M.observe_many("engine.e2e_s", [r.finish_time - r.arrival_time for r in done])

@@ -64,11 +64,21 @@ class PagedKVCache:
 
     @staticmethod
     def auto_num_blocks(cfg: ModelConfig, hkv_local: int, device, kv_fraction: float = 0.85,
-                        reserve_bytes: int = 8 << 30, max_blocks: int | None = None) -> int:
+                        reserve_bytes: int = 8 << 30, max_blocks: int | None = None,
+                        hbm_budget: float | None = None) -> int:
+        """KV blocks for an engine on ``device``: ``kv_fraction`` of the HBM free beyond
+        ``reserve_bytes`` (activations, GEMM workspaces, graphs) - or, with ``hbm_budget``
+        (engine groups sharing a GPU, llm.server --serve ...:mem=F), what is left of
+        hbm_budget x the GPU's total HBM after this process's own allocations (weights) and
+        the reserve, whatever the other groups on the GPU hold or start in what order."""
         dev = torch.device(device)
         if dev.type == "cuda":
-            free, _total = torch.cuda.mem_get_info(dev)
+            free, total = torch.cuda.mem_get_info(dev)
             budget = int(max(0, free - reserve_bytes) * kv_fraction)
+            if hbm_budget is not None:
+                mine = torch.cuda.memory_reserved(dev)
+                budget = min(budget, int(hbm_budget * total) - mine - reserve_bytes)
+                budget = max(budget, 0)
         else:
             budget = 256 << 20
         n = blocks_for_budget(cfg, hkv_local, cfg.num_layers, budget)

@@ -101,9 +101,8 @@ def _worker_main(rank: int, device: str, model_name: str, engine_kw: dict, inq, 
     """One engine replica per GPU (separate process: one process per GPU).
 
     Requests arrive on ``inq`` as (front-end, request id, prompt ids or text, params); the
-    completions of each engine step go back to the front-end that sent them, one message
-    per front-end (``outqs[fe]``: several gRPC front-end processes can share one replica,
-    llm/frontends.py).  Besides results, the worker sends a heartbeat with its engine
+    completions of each engine step go back on ``outqs[fe]`` (one front-end, index 0, in
+    this service).  Besides results, the worker sends a heartbeat with its engine
     counters every ``hb_interval`` s on ``ctlq``; the owner's health monitor evicts a replica
     whose process died or whose heartbeats stopped (SURVEY §5 failure detection: per-GPU
     replica eviction)."""
@@ -174,7 +173,9 @@ def _worker_main(rank: int, device: str, model_name: str, engine_kw: dict, inq, 
                 st = dict(eng.stats)
                 st.update(running=len(eng.running), waiting=len(eng.waiting),
                           pending=len(pending), alive=loop.alive(),
-                          fe_requests=dict(fe_requests))
+                          fe_requests=dict(fe_requests), kv_blocks=eng.kv.num_blocks,
+                          kv_tokens=eng.kv.capacity_tokens, kv_gb=round(eng.kv.bytes / 1e9, 2),
+                          hbm_budget=eng.hbm_budget)
                 ctlq.put(("hb", rank, st))
 
     threading.Thread(target=watcher, daemon=True).start()

@@ -10,13 +10,22 @@ on-node inference:
                      ``--tp N`` runs one tensor-parallel engine over N GPUs
                      (RCCL all-reduce over xGMI), e.g. Llama-3-70B TP=8;
   --backend scripted deterministic format-correct text (no model; CPU tests).
-  --serve FEATURE=MODEL[@GPUS][:tpN] (repeatable) hosts one engine group per feature
-                     on its own GPUs of the node: the per-feature model matrix of
+  --serve FEATURE=MODEL[@GPUS][:tpN][:mem=F] (repeatable) hosts one engine group per
+                     feature on GPUs of the node: the per-feature model matrix of
                      BASELINE.json (Gemma-2B smart reply, Llama-3-8B summarize,
                      Llama-3-70B TP=8 ask-AI, Mixtral suggestions) behind ONE service
-                     address, e.g. --serve smart=gemma-2b@0 --serve summary=llama-3-8b@1
-                     --serve answer=llama-3-70b@0-7:tp8 --serve suggest=mixtral-8x7b@2,3
-                     (features without a --serve use --model).
+                     address (features without a --serve use --model).  Groups may share
+                     a GPU only with an explicit HBM budget each (mem=F: the fraction of
+                     the GPU's total HBM the group may hold - weights, KV cache,
+                     workspaces; at most 0.95 per GPU in all), so the split does not
+                     depend on start order.  The five BASELINE configs on one 8-GPU node:
+                       --serve answer=llama-3-70b@0-7:tp8:mem=0.35
+                       --serve smart=gemma-2b@0,4:mem=0.6
+                       --serve summary=llama-3-8b@1,5:mem=0.6
+                       --serve suggest=mixtral-8x7b@2,3,6,7:mem=0.6
+                     (the 70B TP group holds 101 GB of every GPU: 17.6 GB of weight shard
+                     and ~80 GB of KV cache; each data-parallel replica beside it 173 GB;
+                     the Raft cluster of the first config needs no GPU).
 
 Port 50055 and the thread-pool server match the reference.
 """
@@ -70,6 +79,8 @@ def build_backend(args, devices: list[int] | None = None):
     tok = ChatTokenizer(cfg.vocab_size, cfg.bos_token_id, cfg.eos_token_id)
     engine_kw = dict(max_batch=args.max_batch, max_model_len=args.max_model_len,
                      use_graphs=not args.no_graphs)
+    if getattr(args, "hbm_budget", None):
+        engine_kw["hbm_budget"] = float(args.hbm_budget)
     if args.tp > 1:
         from ..parallel.tp_engine import TPEngineGroup
 
@@ -102,19 +113,29 @@ _FEATURE_ALIAS = {"smart_reply": "smart", "summarize": "summary", "ask": "answer
                   "suggestions": "suggest"}
 
 
-def parse_serve(spec: str) -> tuple[str, str, list[int] | None, int]:
-    """``FEATURE=MODEL[@GPUS][:tpN]`` -> (feature, model, devices or None, tp); GPUS is a
-    comma list of ids and ranges ("0", "1,2", "0-7")."""
+def parse_serve(spec: str) -> tuple[str, str, list[int] | None, int, float | None]:
+    """``FEATURE=MODEL[@GPUS][:tpN][:mem=F]`` -> (feature, model, devices or None, tp, HBM
+    budget fraction or None); GPUS is a comma list of ids and ranges ("0", "1,2", "0-7")."""
     feat, eq, rest = spec.partition("=")
     feat = _FEATURE_ALIAS.get(feat.strip(), feat.strip())
     if not eq or feat not in FEATURES or not rest:
-        raise ValueError(f"--serve {spec!r}: expected FEATURE=MODEL[@GPUS][:tpN], "
+        raise ValueError(f"--serve {spec!r}: expected FEATURE=MODEL[@GPUS][:tpN][:mem=F], "
                          f"FEATURE in {FEATURES}")
-    tp = 1
-    if ":tp" in rest:
-        rest, _, t = rest.rpartition(":tp")
-        tp = int(t)
-    model, _, gpus = rest.partition("@")
+    tp, mem = 1, None
+    head, *opts = rest.split(":")
+    for o in opts:
+        if o.startswith("tp") and o[2:].isdigit():
+            tp = int(o[2:])
+        elif o.startswith("mem="):
+            try:
+                mem = float(o[4:])
+            except ValueError:
+                raise ValueError(f"--serve {spec!r}: bad mem={o[4:]!r}") from None
+            if not 0.0 < mem <= 0.95:
+                raise ValueError(f"--serve {spec!r}: mem must be in (0, 0.95]")
+        else:
+            raise ValueError(f"--serve {spec!r}: unknown option {o!r}")
+    model, _, gpus = head.partition("@")
     devices = None
     if gpus:
         devices = []
@@ -125,7 +146,35 @@ def parse_serve(spec: str) -> tuple[str, str, list[int] | None, int]:
             raise ValueError(f"--serve {spec!r}: a GPU is listed twice")
         if tp > 1 and len(devices) != tp:
             raise ValueError(f"--serve {spec!r}: tp{tp} needs exactly {tp} GPUs")
-    return feat, model.strip(), devices, tp
+    return feat, model.strip(), devices, tp, mem
+
+
+def _group_devices(devices: list[int] | None, tp: int, gpus: int) -> list[int]:
+    """GPUs an engine group occupies (the defaults of build_backend when none are named)."""
+    if devices:
+        return list(devices)
+    return list(range(tp if tp > 1 else max(1, gpus)))
+
+
+def check_placement(groups: list[tuple[str, list[int], float | None]]) -> dict[int, float]:
+    """Validate the GPU placement of engine groups [(name, devices, mem fraction or None)]:
+    a GPU shared by several groups needs an explicit budget for every one of them, and the
+    budgets on a GPU add up to at most 0.95.  Returns {gpu: budgeted fraction}."""
+    on: dict[int, list[tuple[str, float | None]]] = {}
+    for name, devs, mem in groups:
+        for d in devs:
+            on.setdefault(d, []).append((name, mem))
+    used = {}
+    for d, gs in sorted(on.items()):
+        if len(gs) > 1 and any(m is None for _, m in gs):
+            raise ValueError(f"GPU {d} is shared by {[n for n, _ in gs]}: give every group on "
+                             "a shared GPU an HBM budget (:mem=F)")
+        tot = sum(m or 0.0 for _, m in gs)
+        if tot > 0.95 + 1e-9:
+            raise ValueError(f"GPU {d}: HBM budgets of {[n for n, _ in gs]} add up to "
+                             f"{tot:.2f} > 0.95")
+        used[d] = tot
+    return used
 
 
 def build_feature_backends(args, specs: list[str]):
@@ -139,32 +188,45 @@ def build_feature_backends(args, specs: list[str]):
         if f in seen:
             raise ValueError(f"feature {f!r} given twice")
         seen.add(f)
+    # one engine group per distinct (model, GPUs, tp, budget); validate the placement of all
+    # of them (and of the --model group serving the remaining features) before building any
+    groups: dict = {}
+    for feat, model, devices, tp, mem in parsed:
+        groups.setdefault((model, tuple(devices) if devices else None, tp, mem), []).append(feat)
+    need_default = len(seen) < len(FEATURES)
+    gpu_free = args.backend == "scripted"  # scripted stand-ins hold no GPU memory
+    placement = [(f"{'+'.join(fs)}={m}", _group_devices(list(d) if d else None, tp,
+                                                         1 if tp > 1 else
+                                                         (len(d) if d else args.gpus)), mem)
+                 for (m, d, tp, mem), fs in groups.items() if not (gpu_free or m == "scripted")]
+    if need_default and not (gpu_free or args.model == "scripted"):
+        placement.append((f"default={args.model}", _group_devices(None, args.tp, args.gpus),
+                          getattr(args, "hbm_budget", None)))
+    check_placement(placement)
     made: dict = {}
     by_feature = {}
-    for feat, model, devices, tp in parsed:
-        key = (model, tuple(devices) if devices else None, tp)
+    for feat, model, devices, tp, mem in parsed:
+        key = (model, tuple(devices) if devices else None, tp, mem)
         if key not in made:
             sub = argparse.Namespace(**vars(args))
-            sub.model, sub.tp = model, tp
+            sub.model, sub.tp, sub.hbm_budget = model, tp, mem
             sub.gpus = len(devices) if devices and tp == 1 else (1 if tp == 1 else args.gpus)
             sub.max_batch = args.max_batch or default_max_batch(model, tp)
             made[key] = build_backend(sub, devices=devices)
         by_feature[feat] = made[key]
     default = None
-    if len(by_feature) < len(FEATURES):
+    if need_default:
         sub = argparse.Namespace(**vars(args))
         sub.max_batch = args.max_batch or default_max_batch(args.model, args.tp)
         default = build_backend(sub)
     return FeatureRouter(by_feature, default)
 
 
-def serve(backend, port: int = 50055, workers: int = 64, bind: str = "[::]", params=None,
-          reuse_port: bool = False):
-    """Thread-pool gRPC server of the four RPCs over ``backend``.  ``reuse_port``: several
-    front-end processes bind the same port (SO_REUSEPORT, llm/frontends.py); off by default
-    so that a second server on a taken port fails instead of silently sharing it."""
+def serve(backend, port: int = 50055, workers: int = 64, bind: str = "[::]", params=None):
+    """Thread-pool gRPC server of the four RPCs over ``backend`` (SO_REUSEPORT off: a second
+    server on a taken port fails instead of silently sharing it)."""
     server = grpc.server(futures.ThreadPoolExecutor(max_workers=workers),
-                         options=[("grpc.so_reuseport", 1 if reuse_port else 0)])
+                         options=[("grpc.so_reuseport", 0)])
     add_servicer(server, LLM_SERVICE, LLMServicer(backend, params))
     if server.add_insecure_port(f"{bind}:{port}") == 0:
         raise RuntimeError(f"cannot bind port {port}")
@@ -252,47 +314,22 @@ def main(argv=None):
     ap.add_argument("--frontend", choices=("threads", "aio"), default="threads",
                     help="gRPC front-end: a handler thread per in-flight RPC, or grpc.aio "
                          "coroutines on one event-loop thread")
-    ap.add_argument("--frontends", type=int, default=1,
-                    help="gRPC front-end processes sharing the port (SO_REUSEPORT) over the "
-                         "engine replicas (llm/frontends.py); 1 = this process")
-    ap.add_argument("--serve", action="append", default=[], metavar="FEATURE=MODEL[@GPUS][:tpN]",
+    ap.add_argument("--serve", action="append", default=[],
+                    metavar="FEATURE=MODEL[@GPUS][:tpN][:mem=F]",
                     help="host FEATURE (smart | summary | answer | suggest) on its own engine "
                          "group (repeatable; see the module docstring)")
+    ap.add_argument("--hbm-budget", type=float, default=None, metavar="F",
+                    help="fraction of each GPU's HBM the --model engine group may hold "
+                         "(default: 85 %% of what is free when it starts)")
     ap.add_argument("--log-level", default="INFO")
     args = parse_with_config(ap, argv)
     setup_logging(args.log_level)
-    if args.frontends > 1 and not args.serve and args.backend == "engine" and args.tp == 1:
-        import torch
-
-        from ..models import get_config
-        from .frontends import serve_fleet
-
-        if not args.max_batch:
-            args.max_batch = default_max_batch(args.model, args.tp)
-        cfg = get_config(args.model)
-        n = max(1, args.gpus)
-        devices = [f"cuda:{i}" for i in range(n)] if torch.cuda.is_available() else ["cpu"] * n
-        group = serve_fleet(args.model, devices,
-                            dict(max_batch=args.max_batch, max_model_len=args.max_model_len,
-                                 use_graphs=not args.no_graphs),
-                            args.frontends, args.port,
-                            (cfg.vocab_size, cfg.bos_token_id, cfg.eos_token_id),
-                            args.max_model_len,
-                            workers=args.workers or args.max_batch * n // args.frontends + 64)
-        log.info("LLM server on port %d: %d front-end processes over %d engine replicas (%s)",
-                 args.port, args.frontends, n, args.model)
-        stop = threading.Event()
-        signal.signal(signal.SIGINT, lambda *a: stop.set())
-        signal.signal(signal.SIGTERM, lambda *a: stop.set())
-        stop.wait()
-        group.stop()
-        return
     if args.serve:
         backend = build_feature_backends(args, args.serve)
         # a handler thread per request any of the engine groups can hold at once
-        groups = {(m, tuple(d or ()), tp) for _, m, d, tp in map(parse_serve, args.serve)}
+        groups = {(m, tuple(d or ()), tp, mem) for _, m, d, tp, mem in map(parse_serve, args.serve)}
         slots = sum((args.max_batch or default_max_batch(m, tp)) * (len(d) if d and tp == 1 else 1)
-                    for m, d, tp in groups)
+                    for m, d, tp, _ in groups)
         workers = args.workers or slots + 16
     else:
         if not args.max_batch:

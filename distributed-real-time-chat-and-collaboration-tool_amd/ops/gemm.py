@@ -104,10 +104,11 @@ def _activate() -> dict:
                         pre.setdefault((N, K, ldx), []).append(
                             (M, int(e["algo"]), bool(e.get("beta0")), bool(e.get("beta1"))))
                     continue
+                nt_tuned = bool(e.get("nt_tuned"))
                 tab[(M, N, K, ldx)] = (int(e.get("algo", -1)), int(e.get("skinny", 0)),
                                        int(e.get("midm", 0)) if _midm_enabled else 0,
-                                       _xd_policy(M, int(e.get("xd", 0))),
-                                       _xd_policy(M, int(e.get("xd_glu", 0))))
+                                       _xd_policy(M, int(e.get("xd", 0)), nt_tuned),
+                                       _xd_policy(M, int(e.get("xd_glu", 0)), nt_tuned))
         for v in pre.values():
             v.sort()
         _prefill.clear()
@@ -124,13 +125,17 @@ def xd_nt_ok(M: int, form: int) -> bool:
     return form < 1000 and (mt, nf) in XD_NT_TILES and M <= 128 * mt
 
 
-def _xd_policy(M: int, form: int) -> int:
-    """A tuned gemm_xd form as the router runs it (0: none / gemm_xd disabled): a plain form
-    the tuner picked before the non-temporal forms existed takes its non-temporal twin where
-    the batch fits one row tile (DRTC_XD_NT=0 keeps the plain form)."""
+def _xd_policy(M: int, form: int, nt_tuned: bool = False) -> int:
+    """A tuned gemm_xd form as the router runs it (0: none / gemm_xd disabled).  An entry the
+    tuner measured with the non-temporal forms among its candidates (``nt_tuned``: the
+    profiles/r4ab re-tune, M = 128-256) runs exactly the form it picked - a plain winner
+    stays plain; a plain form picked before the nt forms existed takes its nt twin where the
+    batch fits one row tile.  DRTC_XD_NT=0 runs every form plain (an nt pick included)."""
     if not (_xd_enabled and form):
         return 0
-    if _xd_nt and xd_nt_ok(M, form):
+    if not _xd_nt:
+        return form % 1000
+    if not nt_tuned and xd_nt_ok(M, form):
         return form + 1000
     return form
 
@@ -416,12 +421,17 @@ WS_SLAB_BYTES = 128 << 20   # fp32 split-K slabs (per device)
 WS_COUNTERS = 1 << 16
 
 
+# every split-K workspace created in this process (the shared per-device ones and the private
+# ones of second streams): check_splitk_fault reads the fault word of each
+_all_ws: list[tuple[torch.Tensor, torch.Tensor]] = []
+
+
 def gemm_workspace(dev: torch.device) -> tuple[torch.Tensor, torch.Tensor]:
     """Split-K workspace of a device: fp32 slabs + per-tile arrival counters (zeroed once;
-    the last arriver of each tile re-arms its counter).  One per device, shared by every GEMM
-    on the engine's stream (and the medium-M kernel's partial slabs); a GEMM issued
-    concurrently on another stream passes its own (``ws=``).  Created before any graph
-    capture (the engine's eager warm-up does)."""
+    the last arriver of each tile re-arms its counter; the LAST counter is the fault word,
+    ``check_splitk_fault``).  One per device, shared by every GEMM on the engine's stream (and
+    the medium-M kernel's partial slabs); a GEMM issued concurrently on another stream passes
+    its own (``ws=``).  Created before any graph capture (the engine's eager warm-up does)."""
     key = dev.index if dev.index is not None else torch.cuda.current_device()
     ws = _ws.get(key)
     if ws is None:
@@ -431,13 +441,51 @@ def gemm_workspace(dev: torch.device) -> tuple[torch.Tensor, torch.Tensor]:
                 ws = (torch.empty(WS_SLAB_BYTES // 4, dtype=torch.float32, device=dev),
                       torch.zeros(WS_COUNTERS, dtype=torch.int32, device=dev))
                 _ws[key] = ws
+                _all_ws.append(ws)
     return ws
 
 
 def new_gemm_workspace(dev: torch.device) -> tuple[torch.Tensor, torch.Tensor]:
     """A private split-K workspace (for GEMMs on a second stream)."""
-    return (torch.empty(WS_SLAB_BYTES // 4, dtype=torch.float32, device=dev),
-            torch.zeros(WS_COUNTERS, dtype=torch.int32, device=dev))
+    ws = (torch.empty(WS_SLAB_BYTES // 4, dtype=torch.float32, device=dev),
+          torch.zeros(WS_COUNTERS, dtype=torch.int32, device=dev))
+    with _ws_lock:
+        _all_ws.append(ws)
+    return ws
+
+
+class SplitKFault(RuntimeError):
+    """A split-K combine gave up waiting for another slice's partial (gemm_xd / gemm_w4): the
+    GEMM that recorded it stored a wrong sum."""
+
+
+def check_splitk_fault(dev: torch.device | None = None) -> None:
+    """Read the fault word (the last counter) of every split-K workspace on ``dev`` (all
+    devices: None).  A combine whose poll for the other slices timed out sets it and leaves
+    its tile's counters un-armed, so on a fault the counters are zeroed (the next GEMM starts
+    clean) and SplitKFault is raised.  Synchronises with the workspace's device: call it after
+    warm-up / graph capture and from health checks, not per GEMM."""
+    if dev is not None:
+        dev = torch.device(dev)
+        if dev.type == "cuda" and dev.index is None:
+            dev = torch.device("cuda", torch.cuda.current_device())
+    with _ws_lock:
+        wss = list(_all_ws)
+    for slab, cnt in wss:
+        if dev is not None and cnt.device != dev:
+            continue
+        if int(cnt[-1].item()):
+            cnt.zero_()
+            raise SplitKFault(f"split-K combine timed out on {cnt.device}: a GEMM result since "
+                              "the last check is wrong (counters reset)")
+
+
+def set_splitk_spin_limit(limit: int) -> int:
+    """Bound of the split-K combines' poll for the other slices (polls of ~64 cycles;
+    default 1 << 24); < 0 makes every combine fault (tests).  Returns the previous bound."""
+    prev = int(hipk().splitk_spin_limit())
+    hipk().set_splitk_spin_limit(int(limit))
+    return prev
 
 
 def gemm_w4_variant(variant: int) -> bool:
@@ -475,6 +523,33 @@ def mfma_gemm(x: torch.Tensor, w: torch.Tensor, epi: str = "store",
                       N if glu else 0, variant, splitk, group_m, ptr(slab),
                       slab.numel() * 4 if slab is not None else 0, ptr(cnt),
                       cnt.numel() if cnt is not None else 0, stream_ptr(x)), "gemm")
+    return out
+
+
+def ring_supported(M: int, N: int, K: int, glu: bool = False) -> bool:
+    """Shapes gemm_ring.hip takes (N = output columns; gated: half the [gate; up] rows)."""
+    return M >= 1 and K >= 256 and K % 128 == 0 and N % (128 if glu else 256) == 0
+
+
+def ring_gemm(x: torch.Tensor, w: torch.Tensor, epi: str = "store",
+              residual: torch.Tensor | None = None, out: torch.Tensor | None = None,
+              group_m: int = 8) -> torch.Tensor:
+    """Ring-pipelined persistent hand GEMM (csrc/kernels/gemm_ring.hip): y = epi(x @ w.T) with
+    the epilogues of ``mfma_gemm``; 32-deep K stages in a 4-slot LDS ring, one barrier per
+    stage.  K % 128 == 0, K >= 256, N % 256 == 0 (gated: I % 128 == 0)."""
+    M, K = x.shape
+    glu = epi in ("silu", "gelu_tanh")
+    N = w.shape[0] // 2 if glu else w.shape[0]
+    assert ring_supported(M, N, K, glu) and w.shape[1] == K, (M, N, K, epi)
+    if out is None:
+        out = torch.empty((M, N), dtype=x.dtype, device=x.device)
+    assert out.shape == (M, N) and out.stride(1) == 1, (out.shape, M, N)
+    if epi == "residual":
+        assert residual is not None and residual.shape == (M, N) and residual.stride(1) == 1
+    check(hipk().gemm_ring(out.data_ptr(), x.data_ptr(), w.data_ptr(), ptr(residual), M, N, K,
+                           x.stride(0), w.stride(0), out.stride(0),
+                           residual.stride(0) if residual is not None else 0, EPI[epi],
+                           group_m, stream_ptr(x)), "gemm_ring")
     return out
 
 
@@ -553,12 +628,13 @@ W4_MAX_K = int(os.environ.get("DRTC_W4_MAX_K", "8192"))
 
 
 def w4_group_m(M: int, N: int, K: int, glu: bool = False) -> int:
-    """Row-tile group of the XCD-aware tile order (scripts/gpu_w4_groups.sh): a group's A
-    panels must stay cache-resident while it sweeps the columns - 2 for the long-K down
-    projection (7 MB per 256-row panel), 8 for the gated gate_up, 4 otherwise."""
-    if K >= 12288:
-        return 2
-    return 8 if glu else 4
+    """Row-tile group of the XCD-aware tile order.  An XCD's 32 workgroups take 32 consecutive
+    tiles: with groups of 8 (4) rows that is an 8 x 4 (4 x 8) block of tiles, whose 12 operand
+    panels stream through the XCD's L2 per K step, against 18 for the 2 x 16 block of groups
+    of 2 (round 5, profiles/r5c: hipBLASLt's down kernel 23.4 M L2 misses, gemm_w4 at group 2
+    34.1 M).  Interleaved on one box (profiles/r5d): down at K = 14336 1217 us at 8 vs 1247 at
+    2; qkv 524 vs 532 at 4; o + residual 376 vs 378; the gated gate_up 2513 at 4 vs 2537 at 8."""
+    return 4 if glu else 8
 
 
 def w4_shape_ok(M: int, N: int, K: int) -> bool:
@@ -670,7 +746,7 @@ def xd_supported(M: int, N: int, K: int, form: int, glu: bool = False) -> bool:
     # split-K: the partial slots and tile counters fit the device workspace
     tiles = -(-M // (128 * mt)) * (N // tno)
     return sk == 1 or (tiles * sk * (128 * mt) * (32 * nf) * 4 <= WS_SLAB_BYTES
-                       and 2 * tiles + 1 <= WS_COUNTERS)
+                       and 2 * tiles + 2 <= WS_COUNTERS)  # + the fault word (last counter)
 
 
 def xd_default_form(M: int, N: int, K: int, glu: bool = False) -> int:
@@ -787,9 +863,10 @@ def midm_gemm(x: torch.Tensor, w: torch.Tensor, epi: str = "store",
     return out
 
 
-__all__ = ["linear", "route", "norm_linear", "glu_linear", "norm_glu", "fused_glu_ok",
+__all__ = ["linear", "route", "ring_gemm", "ring_supported", "norm_linear", "glu_linear", "norm_glu", "fused_glu_ok",
            "linear_residual",
            "residual_fusable", "w4_glu_ok", "w4_ok", "w4_shape_ok", "w4_group_m", "mfma_gemm",
-           "gemm_workspace", "new_gemm_workspace", "skinny_linear", "skinny_ok",
+           "gemm_workspace", "new_gemm_workspace", "check_splitk_fault", "SplitKFault",
+           "set_splitk_spin_limit", "skinny_linear", "skinny_ok",
            "skinny_variant", "skinny_supports", "midm_gemm", "midm_supported", "midm_splits",
            "xd_gemm", "xd_supported", "xd_default_form", "tune", "save_entries", "load_table", "reset", "set_enabled", "table_path"]

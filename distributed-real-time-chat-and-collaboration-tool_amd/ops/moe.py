@@ -25,13 +25,6 @@ from .activation import ACTS, act_glu_ref
 # rows of [I] and [H] intermediates) while keeping >10k workgroups per GEMM.
 MOE_CHUNK = 8192
 
-# Eager (prefill) calls with at least this many tokens take the sorted
-# per-expert hipBLASLt path (one host sync per layer for the expert counts);
-# graph-captured decode and smaller calls take the fused HIP kernels.
-# scripts/moe_bench.py on Mixtral shapes: T=8192 fused 7.1 ms vs per-expert
-# 5.9 ms; T=2048 fused 1.9 ms vs 2.5 ms.
-MOE_LIBRARY_MIN_TOKENS = int(os.environ.get("DRTC_MOE_LIBRARY_MIN_TOKENS", "4096"))
-
 # Grouped-GEMM structure (csrc/kernels/moe.hip): 0 = 128-row two-barrier,
 # 1 = 128-row 3-stage pipeline, 2 = 256-row 3-stage pipeline, -1 = by rows
 # per expert.
@@ -89,9 +82,9 @@ def fused_moe(x: torch.Tensor, router_logits: torch.Tensor, w_gu: torch.Tensor,
             return out
         return r
     T, H = x.shape
-    if (T >= MOE_LIBRARY_MIN_TOKENS and variant is None
-            and not torch.cuda.is_current_stream_capturing()):
-        return moe_sorted_gemm(x, router_logits, w_gu, w_dn, top_k, act, e_off, out)
+    # every token count takes the fused kernels (prefill included: no host sync per layer;
+    # the round-4 per-expert hipBLASLt path for T >= 4096 measured slower at T = 8192,
+    # 6.05 / 5.86 ms fused vs 6.25 / 5.95 ms, profiles/r4ah, r4ak)
     E = num_experts if num_experts is not None else router_logits.shape[1]
     e_local, two_i, h2 = w_gu.shape
     inter = two_i // 2
@@ -116,52 +109,6 @@ def fused_moe(x: torch.Tensor, router_logits: torch.Tensor, w_gu: torch.Tensor,
                       w_gu.data_ptr(), w_dn.data_ptr(), n, H, inter, E, top_k, e_off, e_local,
                       ACTS[act], workspace.data_ptr(), workspace.numel(),
                       MOE_GEMM_VARIANT if variant is None else variant, st), "moe")
-    return out
-
-
-def moe_sorted_gemm(x: torch.Tensor, router_logits: torch.Tensor, w_gu: torch.Tensor,
-                    w_dn: torch.Tensor, top_k: int, act: str = "silu", e_off: int = 0,
-                    out: torch.Tensor | None = None) -> torch.Tensor:
-    """Large-batch (prefill) MoE through the GEMM library: route on the
-    device, sort the (token, expert) pairs by expert, one hipBLASLt GEMM pair
-    per local expert over its contiguous rows (the fused act*up kernel in
-    between, over all rows at once), then a weighted gather-combine.  One
-    host sync per call (expert row counts); not graph-capturable."""
-    from .activation import act_glu
-
-    T, H = x.shape
-    e_local = w_gu.shape[0]
-    topi, wts = route_ref(router_logits, top_k)      # ties: lower expert id first
-    flat = topi.reshape(-1) - e_off
-    local = (flat >= 0) & (flat < e_local)
-    key = torch.where(local, flat, torch.full_like(flat, e_local))
-    order = torch.argsort(key, stable=True)
-    counts = torch.bincount(key, minlength=e_local + 1)[:e_local].tolist()
-    n_rows = sum(counts)
-    rows = order[:n_rows]
-    xs = x.index_select(0, rows // top_k)
-    inter = w_gu.shape[1] // 2
-    gu = torch.empty((n_rows, 2 * inter), dtype=x.dtype, device=x.device)
-    r0 = 0
-    for e, c in enumerate(counts):
-        if c:
-            torch.matmul(xs[r0:r0 + c], w_gu[e].t(), out=gu[r0:r0 + c])
-        r0 += c
-    h = act_glu(gu, act)
-    del gu
-    ys = torch.empty((n_rows, H), dtype=x.dtype, device=x.device)
-    r0 = 0
-    for e, c in enumerate(counts):
-        if c:
-            torch.matmul(h[r0:r0 + c], w_dn[e].t(), out=ys[r0:r0 + c])
-        r0 += c
-    # combine in fp32 in the fixed (token, slot) order: deterministic
-    y = torch.zeros((T * top_k, H), dtype=torch.float32, device=x.device)
-    y.index_copy_(0, rows, ys.float())
-    y = (y.view(T, top_k, H) * wts.unsqueeze(-1)).sum(1)
-    if out is None:
-        return y.to(x.dtype)
-    out.copy_(y)
     return out
 
 

@@ -27,7 +27,6 @@ from __future__ import annotations
 
 import datetime as _dt
 import hashlib
-import itertools
 import logging
 import mimetypes
 import threading
@@ -90,7 +89,6 @@ class NodeConfig:
     llm_ask: str | None = None
     llm_suggest: str | None = None
     forward_timeout_s: float = 5.0                  # follower -> leader forwarded calls
-    llm_channels: int = 4                           # connections per LLM service (LLMClient)
 
     def llm_routes(self) -> dict:
         """feature -> LLM service address (the per-feature override or ``llm_address``)."""
@@ -101,35 +99,24 @@ class NodeConfig:
 
 
 class LLMClient:
-    """Node -> llm.LLMService client with a circuit breaker.
+    """Node -> llm.LLMService client (one HTTP/2 connection) with a circuit breaker."""
 
-    ``channels`` separate HTTP/2 connections (no shared subchannel), used round-robin: an
-    LLM service running several front-end processes on one port (SO_REUSEPORT,
-    llm/frontends.py) balances per connection, so one connection would pin all of this
-    node's AI traffic to one front-end."""
-
-    def __init__(self, address: str | None, cooldown: float = 5.0, channels: int = 4):
+    def __init__(self, address: str | None, cooldown: float = 5.0):
         self.address = address
         self.cooldown = cooldown
         self._down_until = 0.0
         self.stub = None
-        self._stubs = []
-        self._rr = itertools.count()
         if address:
-            opts = [("grpc.keepalive_time_ms", 30000), ("grpc.keepalive_timeout_ms", 5000),
-                    ("grpc.use_local_subchannel_pool", 1)]
-            self.channels = [grpc.insecure_channel(address, options=opts)
-                             for _ in range(max(1, channels))]
-            self._stubs = [make_stub(ch, LLM_SERVICE) for ch in self.channels]
-            self.stub = self._stubs[0]
+            opts = [("grpc.keepalive_time_ms", 30000), ("grpc.keepalive_timeout_ms", 5000)]
+            self.channel = grpc.insecure_channel(address, options=opts)
+            self.stub = make_stub(self.channel, LLM_SERVICE)
 
     def available(self) -> bool:
         return self.stub is not None and time.monotonic() >= self._down_until
 
     def call(self, method: str, req, timeout: float):
-        stub = self._stubs[next(self._rr) % len(self._stubs)]
         try:
-            return getattr(stub, method)(req, timeout=timeout)
+            return getattr(self.stub, method)(req, timeout=timeout)
         except grpc.RpcError as e:
             if e.code() in (grpc.StatusCode.UNAVAILABLE,):
                 self._down_until = time.monotonic() + self.cooldown
@@ -163,7 +150,7 @@ class ChatNode:
         self.llms = {}
         for f, a in cfg.llm_routes().items():
             if a not in by_addr:
-                by_addr[a] = LLMClient(a, channels=cfg.llm_channels)
+                by_addr[a] = LLMClient(a)
             self.llms[f] = by_addr[a]
         self.llm = self.llms["smart"]
         self.genesis_done = threading.Event()

@@ -195,9 +195,6 @@ def main():
     ap.add_argument("--mode", choices=("direct", "raft"), default="direct")
     ap.add_argument("--frontend", choices=("threads", "aio"), default="threads",
                     help="LLM service front-end (llm/server.py --frontend)")
-    ap.add_argument("--frontends", type=int, default=1,
-                    help="--backend pool: gRPC front-end processes sharing the port over the "
-                         "engine replica (llm/frontends.py)")
     ap.add_argument("--in-process-nodes", action="store_true",
                     help="--mode raft: run the 3 Raft nodes in this process (default: one "
                          "process per node, as deployed)")
@@ -211,25 +208,8 @@ def main():
 
     fp = FeatureParams(ignore_eos=True)  # full 48-token budget per reply (random weights)
     port = free_port()
-    group = None
-    if args.frontends > 1:
-        assert args.backend == "pool", "--frontends needs --backend pool"
-        from drtc_amd.llm.frontends import serve_fleet
-        from drtc_amd.models import get_config
-
-        cfg = get_config(args.model)
-        group = serve_fleet(args.model, ["cuda:0"], dict(max_batch=args.max_batch,
-                                                        max_model_len=2048),
-                            args.frontends, port,
-                            (cfg.vocab_size, cfg.bos_token_id, cfg.eos_token_id), 2048,
-                            workers=args.concurrency // args.frontends + 64, bind="127.0.0.1",
-                            params=fp)
-        backend, eng, llm_srv = None, None, group
-    else:
-        backend, eng = build_backend(args)
-    if group is not None:
-        pass
-    elif args.frontend == "aio":
+    backend, eng = build_backend(args)
+    if args.frontend == "aio":
         llm_srv = serve_aio(backend, port=port, bind="127.0.0.1", params=fp)
     else:
         llm_srv = serve_llm(backend, port=port, bind="127.0.0.1", params=fp,

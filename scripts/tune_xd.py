@@ -104,6 +104,7 @@ def main() -> None:
                               a.nt_any)
                 if rec and rec["xd_us"] < rec["base_us"] * (1 - a.min_gain):
                     ent.update(xd=rec["xd_form"], xd_us=rec["xd_us"], xd_base_us=rec["base_us"])
+                    ent.update(nt_tuned=True)  # nt forms were candidates: the router keeps the pick
                 # gate_up with the GLU in the epilogue against norm_glu's route without gemm_xd
                 # (the fused-GLU gemm_w4 from W4_GLU_MIN_M rows, else the route + act_glu)
                 if name == "gate_up":
@@ -117,6 +118,7 @@ def main() -> None:
                             return ops.act_glu(G.linear(x, w), act)
                     rec = measure(G, x, ws, N // 2, K, act, glu_base, name, model, tp, M, a.nt_any)
                     if rec and rec["xd_us"] < rec["base_us"] * (1 - a.min_gain):
+                        ent.update(nt_tuned=True)
                         ent.update(xd_glu=rec["xd_form"], xd_glu_us=rec["xd_us"],
                                    xd_glu_base_us=rec["base_us"])
                 if ent:

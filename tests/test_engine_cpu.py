@@ -284,23 +284,6 @@ def test_tracing_spans_and_serving_metrics(tmp_path):
     assert 0.0 <= snap["gauges"]["engine.kv_used_frac"] <= 1.0
 
 
-def test_moe_sorted_gemm_matches_reference():
-    from drtc_amd.ops import moe as moe_ops
-
-    torch.manual_seed(0)
-    T, H, I, E, k = 300, 128, 64, 8, 2
-    x = torch.randn(T, H).to(torch.bfloat16)
-    lg = torch.randn(T, E).to(torch.bfloat16)  # bf16 logits: ties occur, lower id wins
-    wgu = (torch.randn(E, 2 * I, H) * 0.05).to(torch.bfloat16)
-    wdn = (torch.randn(E, H, I) * 0.05).to(torch.bfloat16)
-    for e_off, n in ((0, E), (2, 3)):
-        out = moe_ops.moe_sorted_gemm(x, lg, wgu[e_off:e_off + n], wdn[e_off:e_off + n], k,
-                                      e_off=e_off)
-        ref = moe_ops.fused_moe_ref(x, lg, wgu[e_off:e_off + n], wdn[e_off:e_off + n], k,
-                                    e_off=e_off)
-        assert (out.float() - ref.float()).abs().max() < 0.01
-
-
 def test_engine_abort_waiting_running_and_inflight():
     """abort(): a queued request leaves the queue, running ones (one of them in
     a pipelined in-flight step) finish with reason "abort" and free their slot

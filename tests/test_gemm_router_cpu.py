@@ -34,9 +34,26 @@ def test_router_policy_picks_nontemporal_twin(monkeypatch, M, form, want):
     monkeypatch.setattr(G, "_xd_enabled", True)
     assert G._xd_policy(M, form) == want
     monkeypatch.setattr(G, "_xd_nt", False)
-    assert G._xd_policy(M, form) == form
+    assert G._xd_policy(M, form) == form % 1000  # DRTC_XD_NT=0: every form plain
     monkeypatch.setattr(G, "_xd_enabled", False)
     assert G._xd_policy(M, form) == 0
+
+
+def test_router_keeps_nt_tuned_plain_winner(monkeypatch):
+    """An entry the nt-aware re-tune measured (profiles/r4ab: Llama-3-8B gate_up at M = 160-256
+    picked plain 241 over 1241) runs exactly its pick; its nt picks stay nt unless
+    DRTC_XD_NT=0; the committed table marks those entries."""
+    monkeypatch.setattr(G, "_xd_enabled", True)
+    monkeypatch.setattr(G, "_xd_nt", True)
+    assert G._xd_policy(160, 241, nt_tuned=True) == 241
+    assert G._xd_policy(160, 241, nt_tuned=False) == 1241
+    assert G._xd_policy(256, 1244, nt_tuned=True) == 1244
+    monkeypatch.setattr(G, "_xd_nt", False)
+    assert G._xd_policy(256, 1244, nt_tuned=True) == 244
+    with open(G.table_path()) as f:
+        data = json.load(f)
+    e = next(iter(data.values()))["160,28672,4096,4096"]
+    assert e["xd"] == 241 and e["nt_tuned"]
 
 
 def test_every_tuned_xd_form_fits_its_shape():

@@ -770,19 +770,20 @@ def test_skinny_glu_gemm(hipk, M, I, act):
 
 
 @pytest.mark.parametrize("e_off,e_local", [(0, 8), (2, 3)])
-def test_moe_sorted_library_path(hipk, e_off, e_local):
-    """Large eager MoE calls take the sorted per-expert hipBLASLt path."""
+def test_moe_large_eager_call_fused(hipk, e_off, e_local):
+    """A prefill-sized eager MoE call (more tokens than one kernel chunk) on the fused
+    kernels, with expert-parallel slices."""
     from drtc_amd.ops import moe as moe_ops
 
     torch.manual_seed(5)
-    T, H, I, E, k = moe_ops.MOE_LIBRARY_MIN_TOKENS + 37, 256, 128, 8, 2
+    T, H, I, E, k = moe_ops.MOE_CHUNK + 4133, 256, 128, 8, 2
     x = torch.randn(T, H, device=DEV).to(torch.bfloat16)
     lg = torch.randn(T, E, device=DEV).to(torch.bfloat16)
     wgu = (torch.randn(e_local, 2 * I, H, device=DEV) * 0.05).to(torch.bfloat16)
     wdn = (torch.randn(e_local, H, I, device=DEV) * 0.05).to(torch.bfloat16)
     out = ops.fused_moe(x, lg, wgu, wdn, k, num_experts=E, e_off=e_off)
     ref = moe_ops.fused_moe_ref(x, lg, wgu, wdn, k, e_off=e_off)
-    _close(out, ref, 1e-2, 2e-2, "moe library path")
+    _close(out, ref, 1e-2, 2e-2, "moe large eager call")
 
 
 @pytest.mark.parametrize("M,N,K", [(4096, 4096, 4096), (4352, 2048, 5632)])

@@ -54,9 +54,10 @@ def test_llm_service_on_gpu_through_raft_cluster(hipk, tmp_path):
 
 
 def test_llm_server_serves_two_models_side_by_side_on_one_gpu(hipk):
-    """``llm.server --serve smart=tiny-llama@0 --serve summary=tiny-gemma@0``: two engine
-    groups (different model families) share one MI355X behind one service address; each RPC
-    runs on its feature's engine (its engine's step counters move, the other's do not)."""
+    """``llm.server --serve smart=tiny-llama@0:mem=0.1 --serve summary=tiny-gemma@0:mem=0.1``:
+    two engine groups (different model families) share one MI355X behind one service address,
+    each inside its HBM budget; each RPC runs on its feature's engine (its engine's step
+    counters move, the other's do not)."""
     import argparse
 
     from drtc_amd.llm import server as S
@@ -64,8 +65,9 @@ def test_llm_server_serves_two_models_side_by_side_on_one_gpu(hipk):
 
     args = argparse.Namespace(backend="engine", model="tiny-llama", tp=1, gpus=1, max_batch=8,
                               max_model_len=512, no_graphs=False, custom_allreduce=False,
-                              in_process=True)
-    router = S.build_feature_backends(args, ["smart=tiny-llama@0", "summary=tiny-gemma@0"])
+                              in_process=True, hbm_budget=0.1)
+    router = S.build_feature_backends(args, ["smart=tiny-llama@0:mem=0.1",
+                                             "summary=tiny-gemma@0:mem=0.1"])
     smart, summ = router.route("smart"), router.route("summary")
     assert smart is not summ
     assert smart.engine.model.cfg.name == "tiny-llama"
