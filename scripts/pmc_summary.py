@@ -4,6 +4,9 @@ def short(n):
         m=re.search(r'XdCfg<(\d), (\d), (\d), (\d)>', n); return 'xd%s%s%s'%(m.group(1),m.group(2),m.group(4))
     if 'gemm_w4' in n: return 'w4'
     if 'gemm_ring' in n: return 'ring'
+    if 'ingest_kernel' in n:
+        m=re.search(r'ingest_kernel<(\d+), (\d+), (\d+), (\d+)>', n)
+        return 'ingest S%s W%s %sx%s' % m.groups() if m else n[:40]
     if 'Cijk' in n: return 'lib:'+n[:40]
     return n[:30]
 agg=collections.defaultdict(lambda: collections.defaultdict(float)); cnt=collections.Counter()
