@@ -93,6 +93,16 @@ struct XdParams {
   int* err;        // split-K fault word: a fixed slot of the workspace (the last counter),
                    // outside every launch's ticket range; read and cleared by the host
   int spin_limit;  // bound of the last ticket's ready poll (< 0: test hook, always fault)
+  // grouped (mixture-of-experts) mode, kernel template G: row tile tm of the launch is entry tm
+  // of a device tile table - rows [g_row0[tm], + g_rows[tm]) of A and C, weights of expert
+  // g_expert[tm] (b + expert * g_bstride); A rows gathered through g_aidx (token of each
+  // (token, expert) pair) when given; entries at or past *g_ntiles are empty
+  const int* g_row0;
+  const int* g_rows;
+  const int* g_expert;
+  const int* g_ntiles;
+  const int* g_aidx;
+  int64_t g_bstride;
 };
 
 template <class C>
@@ -344,7 +354,7 @@ DRTC_DEVICE f32x4 xd_sum(const XdParams& p, const __amdgpu_buffer_rsrc_t& slab, 
   return v;
 }
 
-template <class C, int EPI>
+template <class C, int EPI, bool G = false>
 __global__ __launch_bounds__(kXdThreads, 1) void gemm_xd_kernel(XdParams p) {
   constexpr int MT = C::MT, NF = C::NF, FA = C::FA;
   extern __shared__ __attribute__((aligned(16))) char xd_lds[];
@@ -358,7 +368,18 @@ __global__ __launch_bounds__(kXdThreads, 1) void gemm_xd_kernel(XdParams p) {
   const int slice = item / ntiles, tile = item - slice * ntiles;
   const int tn = tile / p.tiles_m, tm = tile - tn * p.tiles_m;
   constexpr int TNO = xd_glu<EPI>() ? C::TN / 2 : C::TN;  // output columns per tile
-  const int m0 = C::TM * tm, n0 = TNO * tn;
+  const int n0 = TNO * tn;
+  int m0, rows_a;  // first row of the tile in A / C, valid rows
+  const bf16_t* bmat = p.b;
+  if constexpr (G) {
+    if (tm >= p.g_ntiles[0]) return;  // an empty entry of the tile table
+    m0 = p.g_row0[tm];
+    rows_a = p.g_rows[tm];
+    bmat += (int64_t)p.g_expert[tm] * p.g_bstride;
+  } else {
+    m0 = C::TM * tm;
+    rows_a = min(C::TM, p.M - m0);
+  }
 
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -374,16 +395,19 @@ __global__ __launch_bounds__(kXdThreads, 1) void gemm_xd_kernel(XdParams p) {
   XdDma<C> d;
   const unsigned lds0 = (unsigned)(uintptr_t)(xd_lds_ptr)xd_lds;
   {
-    const int rows_a = min(C::TM, p.M - m0);
-    const char* abase = reinterpret_cast<const char*>(p.a + (int64_t)m0 * p.lda + k0);
-    const char* bbase = reinterpret_cast<const char*>(p.b + (int64_t)n0 * p.ldb + k0);
+    const bool gather = G && p.g_aidx != nullptr;
+    const char* abase =
+        reinterpret_cast<const char*>(p.a + (gather ? 0 : (int64_t)m0 * p.lda) + k0);
+    const char* bbase = reinterpret_cast<const char*>(bmat + (int64_t)n0 * p.ldb + k0);
     d.ra = __builtin_amdgcn_make_buffer_rsrc((void*)abase, (short)0, 0x7FFFFFFF, 0x00020000);
     d.rb = __builtin_amdgcn_make_buffer_rsrc((void*)bbase, (short)0, 0x7FFFFFFF, 0x00020000);
 #pragma unroll
     for (int i = 0; i < C::DA; ++i) {
       const int R = 32 * MT * wv + 8 * i + (lane >> 3);
       const int c = (lane & 7) ^ ((R >> 1) & 7);
-      d.va[i] = (unsigned)(min(R, rows_a - 1) * p.lda * 2 + c * 16);
+      const int row = min(R, rows_a - 1);
+      const int src = gather ? p.g_aidx[m0 + row] : row;  // A row (a token, grouped mode)
+      d.va[i] = (unsigned)(src * p.lda * 2 + c * 16);
     }
 #pragma unroll
     for (int i = 0; i < C::DB; ++i) {
@@ -497,8 +521,8 @@ __global__ __launch_bounds__(kXdThreads, 1) void gemm_xd_kernel(XdParams p) {
   for (int s = 0; s < CPR * MT; ++s) {
     const int q = lane + 64 * s;
     const int row = q / CPR, ch = q - row * CPR;
+    if (64 * MT * wm + row >= rows_a) continue;
     const int m = m0 + 64 * MT * wm + row;
-    if (m >= p.M) continue;
     const int n = n0 + OC * wn + 8 * ch;
     bf16x8 v = *reinterpret_cast<const bf16x8*>(ep + row * PITCH + ch * 16);
     if constexpr (EPI == XD_RESIDUAL) {
@@ -510,9 +534,9 @@ __global__ __launch_bounds__(kXdThreads, 1) void gemm_xd_kernel(XdParams p) {
   }
 }
 
-template <class C, int EPI>
+template <class C, int EPI, bool G = false>
 int xd_launch_e(const XdParams& p, hipStream_t st) {
-  hipLaunchKernelGGL((gemm_xd_kernel<C, EPI>), dim3(8 * p.per_xcd), dim3(kXdThreads),
+  hipLaunchKernelGGL((gemm_xd_kernel<C, EPI, G>), dim3(8 * p.per_xcd), dim3(kXdThreads),
                      (C::ALLOC), st, p);
   return (int)hipGetLastError();
 }
@@ -527,6 +551,17 @@ int xd_launch(const XdParams& p, int epi, hipStream_t st) {
   }
 }
 
+// grouped mode: store (expert down projection) and the gated epilogues (expert gate_up)
+template <class C>
+int xd_launch_g(const XdParams& p, int epi, hipStream_t st) {
+  switch (epi) {
+    case XD_STORE: return xd_launch_e<C, XD_STORE, true>(p, st);
+    case XD_SILU: return xd_launch_e<C, XD_SILU, true>(p, st);
+    case XD_GELU: return xd_launch_e<C, XD_GELU, true>(p, st);
+    default: return -1;
+  }
+}
+
 template <class C>
 int xd_cfg() {
   int e = 0;
@@ -534,6 +569,15 @@ int xd_cfg() {
                         (const void*)gemm_xd_kernel<C, XD_RESIDUAL>,
                         (const void*)gemm_xd_kernel<C, XD_SILU>,
                         (const void*)gemm_xd_kernel<C, XD_GELU>})
+    e |= (int)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, C::ALLOC);
+  return e;
+}
+template <class C>
+int xd_cfg_g() {
+  int e = 0;
+  for (const void* f : {(const void*)gemm_xd_kernel<C, XD_STORE, true>,
+                        (const void*)gemm_xd_kernel<C, XD_SILU, true>,
+                        (const void*)gemm_xd_kernel<C, XD_GELU, true>})
     e |= (int)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, C::ALLOC);
   return e;
 }
@@ -580,6 +624,20 @@ int xd_dispatch(const XdParams& p, int mt, int nf, bool nt, int epi, hipStream_t
     case 24: return xd_launch<Xd2x4<SP>>(p, epi, st);
     case 26: return xd_launch<Xd2x6<SP>>(p, epi, st);
     case 28: return xd_launch<Xd2x8<SP>>(p, epi, st);
+    default: return -1;
+  }
+}
+
+// grouped (MoE) mode: the 128 x 128, 256 x 128 and 256 x 256 tiles
+template <bool SP>
+int xd_dispatch_g(const XdParams& p, int mt, int nf, bool nt, int epi, hipStream_t st) {
+  switch (mt * 10 + nf + (nt ? 100 : 0)) {
+    case 14: return xd_launch_g<Xd1x4<SP>>(p, epi, st);
+    case 24: return xd_launch_g<Xd2x4<SP>>(p, epi, st);
+    case 28: return xd_launch_g<Xd2x8<SP>>(p, epi, st);
+    case 114: return xd_launch_g<Xd1x4<SP, true>>(p, epi, st);
+    case 124: return xd_launch_g<Xd2x4<SP, true>>(p, epi, st);
+    case 128: return xd_launch_g<Xd2x8<SP, true>>(p, epi, st);
     default: return -1;
   }
 }
@@ -646,7 +704,68 @@ int launch_gemm_xd(void* c, const void* a, const void* b, const void* r, int M, 
   return xd_dispatch<false>(p, mt, nf, nt, epi, st);
 }
 
+int launch_gemm_xd_grouped(void* c, const void* a, const void* b, int a_rows, int N, int K,
+                           int lda, int ldb, int ldc, int epi, int mt, int nf, int splitk,
+                           int max_tiles, const int* tile_row0, const int* tile_rows,
+                           const int* tile_expert, const int* n_tiles, const int* a_index,
+                           int64_t b_stride, void* slab, int64_t slab_bytes, int* counters,
+                           int n_counters, hipStream_t st) {
+  const bool nt = (mt & 16) != 0;
+  mt &= 15;
+  if (epi != XD_STORE && epi != XD_SILU && epi != XD_GELU) return -1;
+  const bool glu = epi != XD_STORE;
+  const int stages = xd_stages(mt, nf);
+  if (stages == 0 || splitk < 1 || splitk > 8 || (glu && nf % 2)) return -1;
+  if (lda % 8 || ldb % 8 || ldc % 8 || max_tiles < 1 || a_rows < 1) return -1;
+  if ((uintptr_t)a % 16 || (uintptr_t)b % 16 || (uintptr_t)c % 16) return -1;
+  if (tile_row0 == nullptr || tile_rows == nullptr || tile_expert == nullptr || n_tiles == nullptr)
+    return -1;
+  const int tm_rows = 128 * mt, tno = glu ? 16 * nf : 32 * nf;
+  if (N <= 0 || N % tno || K % 64 || K / 64 / splitk <= stages) return -1;
+  // 32-bit buffer offsets: a gathered A row anywhere in A, a tile's rows of contiguous A, the
+  // weight rows of one expert
+  if ((int64_t)(a_index ? a_rows : tm_rows) * lda * 2 >= (1ll << 31) ||
+      (int64_t)(glu ? N + tno : 32 * nf) * ldb * 2 >= (1ll << 31))
+    return -1;
+  XdParams p{};
+  p.c = (bf16_t*)c;
+  p.a = (const bf16_t*)a;
+  p.b = (const bf16_t*)b;
+  p.M = max_tiles * tm_rows; p.N = N; p.K = K;
+  p.lda = lda; p.ldb = ldb; p.ldc = ldc;
+  p.tiles_m = max_tiles;
+  p.tiles_n = N / tno;
+  p.splitk = splitk;
+  p.up_off = glu ? N : 0;
+  p.g_row0 = tile_row0;
+  p.g_rows = tile_rows;
+  p.g_expert = tile_expert;
+  p.g_ntiles = n_tiles;
+  p.g_aidx = a_index;
+  p.g_bstride = b_stride;
+  const int64_t tiles = (int64_t)p.tiles_m * p.tiles_n;
+  if (tiles * splitk * 8 >= (1ll << 31)) return -1;
+  p.per_xcd = (int)((tiles * splitk + 7) / 8);
+  if (splitk > 1) {
+    if (slab == nullptr || counters == nullptr || n_counters < 2 * tiles + 2 ||
+        slab_bytes < tiles * splitk * tm_rows * (32 * nf) * 4)
+      return -2;
+    p.slab = (float*)slab;
+    p.counters = counters;
+    p.err = counters + n_counters - 1;
+    p.spin_limit = splitk_spin_limit();
+    return xd_dispatch_g<true>(p, mt, nf, nt, epi, st);
+  }
+  return xd_dispatch_g<false>(p, mt, nf, nt, epi, st);
+}
+
 int configure_gemm_xd() {
+  const int g = xd_cfg_g<Xd1x4<false>>() | xd_cfg_g<Xd2x4<false>>() | xd_cfg_g<Xd2x8<false>>() |
+                xd_cfg_g<Xd1x4<true>>() | xd_cfg_g<Xd2x4<true>>() | xd_cfg_g<Xd2x8<true>>() |
+                xd_cfg_g<Xd1x4<false, true>>() | xd_cfg_g<Xd2x4<false, true>>() |
+                xd_cfg_g<Xd2x8<false, true>>() | xd_cfg_g<Xd1x4<true, true>>() |
+                xd_cfg_g<Xd2x4<true, true>>() | xd_cfg_g<Xd2x8<true, true>>();
+  if (g) return g;
   return xd_cfg<Xd1x2<false>>() | xd_cfg<Xd1x4<false>>() | xd_cfg<Xd1x6<false>>() |
          xd_cfg<Xd2x4<false>>() | xd_cfg<Xd2x6<false>>() | xd_cfg<Xd1x2<true>>() |
          xd_cfg<Xd1x4<true>>() | xd_cfg<Xd1x6<true>>() | xd_cfg<Xd2x4<true>>() |

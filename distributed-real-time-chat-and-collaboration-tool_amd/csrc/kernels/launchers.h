@@ -51,9 +51,13 @@ int launch_sample(int* out_tokens, const void* logits, int B, int V, int ld,
                   const float* temperature, const int* top_k, const float* top_p,
                   uint64_t seed, const int64_t* step, hipStream_t st);
 
+// variant 0 / 1 / 2: the moe.hip grouped GEMMs; 3: gemm_xd grouped mode with xd forms gu_form
+// (gated gate_up) / dn_form (down), 0 = by rows per expert; slab / counters: the split-K
+// workspace of the gemm_xd forms (may be null: no split-K); -1: by rows per expert
 int launch_moe(void* out, const void* x, const void* router_logits, const void* w_gu,
                const void* w_dn, int T, int H, int I, int E, int k, int e_off, int e_local,
-               int act, void* workspace, int64_t ws_bytes, int variant, hipStream_t st);
+               int act, void* workspace, int64_t ws_bytes, int variant, int gu_form, int dn_form,
+               void* slab, int64_t slab_bytes, int* counters, int n_counters, hipStream_t st);
 int64_t moe_workspace_bytes(int T, int H, int I, int e_local, int k);
 // Expert-parallel dispatch / combine with a static per-destination capacity (moe_ep.hip).
 int launch_ep_plan(const int* topi, int P, int e_local, int world, int cap, int* dst_row,
@@ -137,6 +141,17 @@ int launch_gemm_xd(void* c, const void* a, const void* b, const void* r, int M, 
                    void* slab, int64_t slab_bytes, int* counters, int n_counters,
                    hipStream_t st);
 int64_t gemm_xd_workspace_bytes(int M, int N, int mt, int nf, int splitk, int glu);
+// Grouped (mixture-of-experts) gemm_xd: row tile i of C / A is entry i < *n_tiles of a device
+// tile table (rows [tile_row0[i], + tile_rows[i]), expert tile_expert[i]: weights b +
+// expert * b_stride elements); A rows gathered through a_index when given (a_rows = rows of A
+// then).  Forms (mt, nf) in (1, 4), (2, 4), (2, 8), + 16 in mt for non-temporal weight loads;
+// epi 0 store, 2 / 3 SiLU / GELU gated.  Grid: max_tiles x column tiles x splitk workgroups.
+int launch_gemm_xd_grouped(void* c, const void* a, const void* b, int a_rows, int N, int K,
+                           int lda, int ldb, int ldc, int epi, int mt, int nf, int splitk,
+                           int max_tiles, const int* tile_row0, const int* tile_rows,
+                           const int* tile_expert, const int* n_tiles, const int* a_index,
+                           int64_t b_stride, void* slab, int64_t slab_bytes, int* counters,
+                           int n_counters, hipStream_t st);
 int configure_gemm_xd();
 // Split-K fault handling shared by gemm_xd and gemm_w4: a combine whose poll for the other
 // slices exceeds the spin limit stores 1 into the workspace's LAST counter (n_counters - 1,

@@ -20,6 +20,8 @@
 #include "common.h"
 #include "launchers.h"
 
+#include <initializer_list>
+
 namespace drtc {
 
 constexpr int kMoeBM = 128;   // rows per tile
@@ -424,22 +426,75 @@ __global__ __launch_bounds__(256) void moe_combine_kernel(
   }
 }
 
+// Whether grouped gemm_xd form `form` takes an expert GEMM with N output columns (gated: I)
+// and reduction K (the 1x4 / 2x4 / 2x8 tiles launch_gemm_xd_grouped builds).
+static bool moe_xd_ok(int form, int N, int K, bool glu) {
+  const int mt = (form % 1000) / 100, nf = form / 10 % 10, sk = form % 10;
+  const int st = mt == 1 ? (nf == 4 ? 4 : 0) : (mt == 2 ? (nf == 4 ? 3 : (nf == 8 ? 2 : 0)) : 0);
+  if (st == 0 || sk < 1 || sk > 8 || form >= 2000) return false;
+  const int tno = glu ? 16 * nf : 32 * nf;
+  return N % tno == 0 && K % 64 == 0 && K / 64 / sk > st;
+}
+
+// xd form (mt * 100 + nf * 10 + splitk, + 1000 non-temporal weights) -> launcher fields
+static void moe_xd_form(int form, int& mt, int& nf, int& sk) {
+  mt = (form % 1000) / 100 | (form >= 1000 ? 16 : 0);
+  nf = form / 10 % 10;
+  sk = form % 10;
+}
+
 int launch_moe(void* out, const void* x, const void* router_logits, const void* w_gu,
                const void* w_dn, int T, int H, int I, int E, int k, int e_off, int e_local,
-               int act, void* workspace, int64_t ws_bytes, int variant, hipStream_t st) {
+               int act, void* workspace, int64_t ws_bytes, int variant, int gu_form, int dn_form,
+               void* slab, int64_t slab_bytes, int* counters, int n_counters, hipStream_t st) {
   if (T == 0) return 0;
   if (E > 256 || k > kMoeMaxK || k < 1 || k > E || H % 128 != 0 || I % 64 != 0 || H % kBK != 0 ||
       e_off < 0 || e_local < 1 || e_off + e_local > E)
     return -1;
   const int P = T * k;
   // GEMM structure: 0 = 128-row 2-barrier (small tiles, decode), 1 = 128-row
-  // 3-stage pipeline, 2 = 256-row 3-stage pipeline; -1 = pick by rows/expert
-  // measured (scripts/moe_bench.py, Mixtral shapes): the 128-row pipeline wins
-  // below ~100 rows per expert (decode: 5.3 TB/s of expert weights at T=256),
-  // the 256-row one from there up (ties the two-barrier kernel at 8k tokens)
-  if (variant < 0) variant = (P / e_local >= 96) ? 2 : 1;
-  if (variant > 2) return -1;
-  const int bm = variant == 2 ? 256 : 128;
+  // 3-stage pipeline, 2 = 256-row 3-stage pipeline, 3 = gemm_xd grouped mode (gate_up with
+  // the GLU in its epilogue and down, forms gu_form / dn_form; 0 = by rows per expert);
+  // -1 = pick by rows per expert (scripts/moe_bench.py, Mixtral shapes)
+  const int rows_e = P / e_local;
+  const bool auto_v = variant < 0;
+  if (auto_v) variant = rows_e >= 96 ? 3 : 1;
+  if (variant > 3) return -1;
+  if (variant == 3) {
+    // 256-row tiles from ~1.5 tiles of rows per expert, else 128-row; 256 gated columns
+    // (128 outputs) for gate_up where I allows; down with split-K 2 while the grid is below
+    // ~2 rounds of CUs; non-temporal weights where an expert's rows fit one tile (each
+    // weight byte is read by one workgroup)
+    if (gu_form == 0) {
+      for (int f : rows_e >= 96 ? std::initializer_list<int>{281, 241} :
+                                  std::initializer_list<int>{141})
+        if (moe_xd_ok(f, I, H, true)) { gu_form = f; break; }
+    }
+    const int mt0 = (gu_form % 1000) / 100, bm0 = 128 * mt0;
+    if (gu_form && gu_form < 1000 && rows_e <= bm0) gu_form += 1000;
+    if (dn_form == 0 && gu_form) {
+      const int64_t max_t = (P + bm0 - 1) / bm0 + e_local;
+      for (int f : mt0 == 2 ? std::initializer_list<int>{282, 281, 242, 241} :
+                              std::initializer_list<int>{142, 141}) {
+        // split-K 2 while the grid is below ~2 rounds of CUs and its fp32 partial slots fit
+        const int nf = f / 10 % 10;
+        const int64_t tiles = max_t * (H / (32 * nf));
+        const bool split = tiles < 512 && slab != nullptr && n_counters >= 2 * tiles + 2 &&
+                           slab_bytes >= tiles * 2 * bm0 * (32 * nf) * 4;
+        if (!split && f % 10 > 1) continue;
+        if (moe_xd_ok(f, H, I, false)) { dn_form = f; break; }
+      }
+      if (dn_form && rows_e <= bm0) dn_form += 1000;
+    }
+    const bool ok = gu_form && dn_form && moe_xd_ok(gu_form, I, H, true) &&
+                    moe_xd_ok(dn_form, H, I, false) &&
+                    (gu_form % 1000) / 100 == (dn_form % 1000) / 100;  // one tile table
+    if (!ok) {
+      if (!auto_v) return -1;
+      variant = rows_e >= 96 ? 2 : 1;  // shapes the grouped gemm_xd forms do not take
+    }
+  }
+  const int bm = variant == 3 ? 128 * ((gu_form % 1000) / 100) : (variant == 2 ? 256 : 128);
   const int max_tiles = (P + bm - 1) / bm + e_local;
   // workspace carve (all 256-B aligned)
   auto align = [](int64_t v) { return (v + 255) & ~int64_t(255); };
@@ -461,7 +516,19 @@ int launch_moe(void* out, const void* x, const void* router_logits, const void* 
                      E, k, sorted_tok, sorted_w, inv_pos, topk_w, t_e, t_r0, t_n, n_tiles, local_range,
                      max_tiles, e_off, e_local, bm);
   const dim3 g_gu((I / 64) * max_tiles), g_dn((H / 128) * max_tiles);
-  if (variant == 0) {
+  if (variant == 3) {
+    int mt, nf, sk, e;
+    moe_xd_form(gu_form, mt, nf, sk);
+    e = launch_gemm_xd_grouped(hbuf, x, w_gu, T, I, H, H, H, I, 2 + act, mt, nf, sk, max_tiles,
+                               t_r0, t_n, t_e, n_tiles, sorted_tok, 2ll * I * H, slab,
+                               slab_bytes, counters, n_counters, st);
+    if (e) return e;
+    moe_xd_form(dn_form, mt, nf, sk);
+    e = launch_gemm_xd_grouped(zbuf, hbuf, w_dn, P, H, I, I, I, H, 0, mt, nf, sk, max_tiles,
+                               t_r0, t_n, t_e, n_tiles, nullptr, (int64_t)H * I, slab,
+                               slab_bytes, counters, n_counters, st);
+    if (e) return e;
+  } else if (variant == 0) {
     hipLaunchKernelGGL(moe_gemm_kernel<0>, g_gu, dim3(256), 0, st, hbuf, (const bf16_t*)x,
                        (const bf16_t*)w_gu, sorted_tok, t_e, t_r0, t_n, n_tiles, H, 2 * I, I, I,
                        max_tiles, act);

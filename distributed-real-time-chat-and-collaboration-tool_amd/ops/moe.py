@@ -26,9 +26,14 @@ from .activation import ACTS, act_glu_ref
 MOE_CHUNK = 8192
 
 # Grouped-GEMM structure (csrc/kernels/moe.hip): 0 = 128-row two-barrier,
-# 1 = 128-row 3-stage pipeline, 2 = 256-row 3-stage pipeline, -1 = by rows
-# per expert.
+# 1 = 128-row 3-stage pipeline, 2 = 256-row 3-stage pipeline, 3 = gemm_xd's grouped mode
+# (csrc/kernels/gemm_xd.hip: XCD-partitioned tiles, GLU epilogue, split-K, non-temporal
+# weights where an expert's rows fit one tile), -1 = by rows per expert.
 MOE_GEMM_VARIANT = int(os.environ.get("DRTC_MOE_VARIANT", "-1"))
+# gemm_xd forms of variant 3 (mt * 100 + nf * 10 + splitk, + 1000 non-temporal; 0 = by rows
+# per expert, csrc/kernels/moe.hip launch_moe)
+MOE_GU_FORM = int(os.environ.get("DRTC_MOE_GU_FORM", "0"))
+MOE_DN_FORM = int(os.environ.get("DRTC_MOE_DN_FORM", "0"))
 
 
 def route_ref(router_logits: torch.Tensor, top_k: int):
@@ -61,15 +66,21 @@ def workspace_bytes(tokens: int, hidden: int, inter: int, e_local: int, top_k: i
 def make_workspace(tokens: int, hidden: int, inter: int, e_local: int, top_k: int,
                    device) -> torch.Tensor:
     """Persistent scratch for up to ``tokens`` tokens per call (allocate once,
-    before any graph capture)."""
+    before any graph capture; also creates the device's split-K GEMM workspace that the
+    gemm_xd forms of variant 3 use)."""
+    from .gemm import gemm_workspace
+
     n = workspace_bytes(min(tokens, MOE_CHUNK), hidden, inter, e_local, top_k)
+    if torch.device(device).type == "cuda":
+        gemm_workspace(torch.device(device))
     return torch.empty(n, dtype=torch.uint8, device=device)
 
 
 def fused_moe(x: torch.Tensor, router_logits: torch.Tensor, w_gu: torch.Tensor,
               w_dn: torch.Tensor, top_k: int, act: str = "silu", num_experts: int | None = None,
               e_off: int = 0, workspace: torch.Tensor | None = None,
-              out: torch.Tensor | None = None, variant: int | None = None) -> torch.Tensor:
+              out: torch.Tensor | None = None, variant: int | None = None,
+              gu_form: int | None = None, dn_form: int | None = None) -> torch.Tensor:
     """y[t] = sum_j w[t,j] * down_e(act(gate_e x_t) * up_e x_t) over the top-k experts.
 
     x [T, H] bf16; router_logits [T, E] bf16; w_gu [E_local, 2I, H] ([gate | up]
@@ -103,12 +114,25 @@ def fused_moe(x: torch.Tensor, router_logits: torch.Tensor, w_gu: torch.Tensor,
             "fused_moe under graph capture needs a preallocated workspace"
         workspace = torch.empty(need, dtype=torch.uint8, device=x.device)
     lib, st = hipk(), stream_ptr(x)
+    # the split-K slabs / counters of the gemm_xd forms: the device's shared GEMM workspace
+    # (same stream), only when it exists already (never created inside a graph capture)
+    from . import gemm as _gemm
+
+    key = x.device.index if x.device.index is not None else torch.cuda.current_device()
+    gws = _gemm._ws.get(key)
+    slab, cnt = gws if gws is not None else (None, None)
     for t0 in range(0, T, MOE_CHUNK):
         n = min(MOE_CHUNK, T - t0)
         check(lib.moe(out[t0].data_ptr(), x[t0].data_ptr(), router_logits[t0].data_ptr(),
                       w_gu.data_ptr(), w_dn.data_ptr(), n, H, inter, E, top_k, e_off, e_local,
                       ACTS[act], workspace.data_ptr(), workspace.numel(),
-                      MOE_GEMM_VARIANT if variant is None else variant, st), "moe")
+                      MOE_GEMM_VARIANT if variant is None else variant,
+                      MOE_GU_FORM if gu_form is None else gu_form,
+                      MOE_DN_FORM if dn_form is None else dn_form,
+                      slab.data_ptr() if slab is not None else 0,
+                      slab.numel() * 4 if slab is not None else 0,
+                      cnt.data_ptr() if cnt is not None else 0,
+                      cnt.numel() if cnt is not None else 0, st), "moe")
     return out
 
 

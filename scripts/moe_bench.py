@@ -7,7 +7,7 @@ import sys
 import torch
 import torch.nn.functional as F
 
-sys.path.insert(0, ".")
+sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__))))
 from drtc_amd import ops  # noqa: E402
 from drtc_amd.ops import moe as moe_ops  # noqa: E402
 
@@ -32,15 +32,25 @@ def main():
     wgu = (torch.rand(E, 2 * I, H, device=dev, generator=g) * 2 - 1).to(torch.bfloat16) * 0.02
     wdn = (torch.rand(E, H, I, device=dev, generator=g) * 2 - 1).to(torch.bfloat16) * 0.02
     wbytes = (wgu.numel() + wdn.numel()) * 2
-    ws = moe_ops.make_workspace(moe_ops.MOE_CHUNK, H, I, E, k, dev)
-    for T in (64, 256, 512, 1024, 2048, 8192):
+    ws = moe_ops.make_workspace(moe_ops.MOE_CHUNK, H, I, E, k, dev)  # + the GEMM workspace
+    ts = [int(t) for t in sys.argv[2].split(",")] if len(sys.argv) > 2 else \
+        [64, 256, 512, 1024, 2048, 8192]
+    for T in ts:
         x = (torch.rand(T, H, device=dev, generator=g) * 2 - 1).to(torch.bfloat16)
         lg = torch.randn(T, E, device=dev, generator=g).to(torch.bfloat16)
         out = torch.empty_like(x)
         t_v = []
-        for v in (0, 1, 2):
+        for v in (0, 1, 2, 3):
             t_v.append(timeit(lambda: ops.fused_moe(x, lg, wgu, wdn, k, workspace=ws, out=out,
                                                     variant=v)))
+        # variant 3 with explicit gemm_xd forms (gate_up / down)
+        forms = {}
+        for gu, dn in ((281, 282), (281, 281), (1281, 1282), (241, 242), (141, 142), (1141, 1142)):
+            try:
+                forms[f"{gu}/{dn}"] = timeit(lambda: ops.fused_moe(
+                    x, lg, wgu, wdn, k, workspace=ws, out=out, variant=3, gu_form=gu, dn_form=dn))
+            except RuntimeError:
+                pass
         t_f = timeit(lambda: ops.fused_moe(x, lg, wgu, wdn, k, workspace=ws, out=out))
         topi, wts = moe_ops.route_ref(lg, k)
 
@@ -54,6 +64,7 @@ def main():
         t_b = timeit(blaslt, 5)
         flops = 2 * T * k * 3 * H * I
         vs = " ".join(f"v{v}:{flops / t / 1e9:6.0f}" for v, t in enumerate(t_v))
+        vs += " | xd " + " ".join(f"{f}:{flops / t / 1e9:6.0f}" for f, t in forms.items())
         print(f"T={T:5d}  fused(auto) {t_f:7.3f} ms {flops / t_f / 1e9:7.1f} TF/s "
               f"{wbytes / t_f / 1e6:7.0f} GB/s [{vs} TF/s] | per-expert hipBLASLt {t_b:7.3f} ms "
               f"{flops / t_b / 1e9:7.1f} TF/s", flush=True)

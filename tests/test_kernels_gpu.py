@@ -553,12 +553,33 @@ def _moe_inputs(T, H, I, E, seed=0):
                                         (300, 4096, 1792, 8, 2), (1000, 512, 256, 16, 4),
                                         (129, 256, 64, 8, 8)])
 @pytest.mark.parametrize("act", ["silu", "gelu_tanh"])
-@pytest.mark.parametrize("variant", [0, 1, 2])
+@pytest.mark.parametrize("variant", [0, 1, 2, -1])
 def test_fused_moe(hipk, T, H, I, E, k, act, variant):
     x, lg, wgu, wdn = _moe_inputs(T, H, I, E)
     y = ops.fused_moe(x, lg, wgu, wdn, k, act, variant=variant)
     yr = ops.fused_moe_ref(x, lg, wgu, wdn, k, act)
     _close(y, yr, 3e-2, 3e-2, "fused_moe")
+
+
+@pytest.mark.parametrize("T,H,I,E,k,gu,dn", [
+    (300, 4096, 1792, 8, 2, 141, 142),     # 128-row tiles, down split-K 2
+    (1000, 512, 256, 16, 4, 281, 281),     # 256 x 256 gated tiles, several row tiles / expert
+    (1024, 1024, 512, 8, 2, 1281, 1282),   # non-temporal weights, down split-K 2
+    (777, 1024, 512, 8, 2, 241, 242),      # 256 x 128 tiles
+    (64, 512, 384, 8, 2, 1141, 1141),      # mostly-empty tiles, rows per expert < 16
+])
+@pytest.mark.parametrize("act", ["silu", "gelu_tanh"])
+def test_fused_moe_grouped_xd_forms(hipk, T, H, I, E, k, gu, dn, act):
+    """MoE variant 3: the expert GEMMs on gemm_xd's grouped mode (device tile table, gathered
+    token rows for gate_up with the GLU in the epilogue, per-expert weight panels, split-K on
+    the shared GEMM workspace) against the fp32 reference."""
+    from drtc_amd.ops import gemm as G
+
+    G.gemm_workspace(torch.device(DEV))
+    x, lg, wgu, wdn = _moe_inputs(T, H, I, E, seed=T)
+    y = ops.fused_moe(x, lg, wgu, wdn, k, act, variant=3, gu_form=gu, dn_form=dn)
+    _close(y, ops.fused_moe_ref(x, lg, wgu, wdn, k, act), 3e-2, 3e-2, f"moe xd {gu}/{dn}")
+    G.check_splitk_fault()
 
 
 def test_fused_moe_expert_parallel_slices_sum(hipk):
