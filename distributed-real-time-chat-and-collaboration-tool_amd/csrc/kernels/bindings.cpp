@@ -108,13 +108,6 @@ PYBIND11_MODULE(_hipk, m) {
                                 M, N, K, lda, ldb, ldc, ldr, epi, mt, nf, splitk, P<void>(slab),
                                 slab_bytes, P<int>(counters), n_counters, S(st));
   });
-  // gemm_ring (ops.gemm.ring_gemm): 4-slot LDS ring of 32-deep K stages, persistent
-  m.def("gemm_ring", [](u64 c, u64 a, u64 b, u64 r, int M, int N, int K, int lda, int ldb,
-                        int ldc, int ldr, int epi, int group_m, u64 st) {
-    return drtc::launch_gemm_ring(P<void>(c), P<const void>(a), P<const void>(b),
-                                  P<const void>(r), M, N, K, lda, ldb, ldc, ldr, epi, group_m,
-                                  S(st));
-  });
   m.def("gemm_xd_workspace_bytes", &drtc::gemm_xd_workspace_bytes);
   m.def("splitk_spin_limit", &drtc::splitk_spin_limit);
   m.def("set_splitk_spin_limit", &drtc::set_splitk_spin_limit);

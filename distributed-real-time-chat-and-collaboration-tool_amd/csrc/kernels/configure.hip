@@ -11,8 +11,6 @@ int configure_kernels() {
   if (e) return e;
   e = configure_gemm_w4();
   if (e) return e;
-  e = configure_gemm_ring();
-  if (e) return e;
   return configure_gemm_xd();
 }
 }  // namespace drtc

@@ -123,13 +123,6 @@ int launch_gemm_w4(void* c, const void* a, const void* b, const void* r, int M, 
 int64_t gemm_w4_workspace_bytes(int64_t M, int64_t N, int splitk);
 int configure_gemm_w4();
 
-// Ring-pipelined persistent 4-wave GEMM (gemm_ring.hip): same epilogues and operand contract
-// as gemm_w4 (epi 0 store, 1 + r, 2 / 3 SiLU / GELU gated with up_off = N); 32-deep K stages
-// in a 4-slot LDS ring, one barrier per stage.  K % 128 == 0, K >= 256, N % 256 == 0 (gated
-// N % 128 == 0); group_m = row tiles per column sweep of the tile order.
-int launch_gemm_ring(void* c, const void* a, const void* b, const void* r, int M, int N, int K,
-                     int lda, int ldb, int ldc, int ldr, int epi, int group_m, hipStream_t st);
-int configure_gemm_ring();
 
 // XCD-partitioned decode GEMM (gemm_xd.hip): c[M,N] = epi(a[M,K] . b[N,K]^T); epi 0 store, 1 + r
 // (residual, may alias c), 2 / 3 SiLU / GELU gating of b = [gate; up] (2 N rows); 128 mt x 32 nf

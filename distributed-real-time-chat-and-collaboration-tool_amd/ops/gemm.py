@@ -526,33 +526,6 @@ def mfma_gemm(x: torch.Tensor, w: torch.Tensor, epi: str = "store",
     return out
 
 
-def ring_supported(M: int, N: int, K: int, glu: bool = False) -> bool:
-    """Shapes gemm_ring.hip takes (N = output columns; gated: half the [gate; up] rows)."""
-    return M >= 1 and K >= 256 and K % 128 == 0 and N % (128 if glu else 256) == 0
-
-
-def ring_gemm(x: torch.Tensor, w: torch.Tensor, epi: str = "store",
-              residual: torch.Tensor | None = None, out: torch.Tensor | None = None,
-              group_m: int = 8) -> torch.Tensor:
-    """Ring-pipelined persistent hand GEMM (csrc/kernels/gemm_ring.hip): y = epi(x @ w.T) with
-    the epilogues of ``mfma_gemm``; 32-deep K stages in a 4-slot LDS ring, one barrier per
-    stage.  K % 128 == 0, K >= 256, N % 256 == 0 (gated: I % 128 == 0)."""
-    M, K = x.shape
-    glu = epi in ("silu", "gelu_tanh")
-    N = w.shape[0] // 2 if glu else w.shape[0]
-    assert ring_supported(M, N, K, glu) and w.shape[1] == K, (M, N, K, epi)
-    if out is None:
-        out = torch.empty((M, N), dtype=x.dtype, device=x.device)
-    assert out.shape == (M, N) and out.stride(1) == 1, (out.shape, M, N)
-    if epi == "residual":
-        assert residual is not None and residual.shape == (M, N) and residual.stride(1) == 1
-    check(hipk().gemm_ring(out.data_ptr(), x.data_ptr(), w.data_ptr(), ptr(residual), M, N, K,
-                           x.stride(0), w.stride(0), out.stride(0),
-                           residual.stride(0) if residual is not None else 0, EPI[epi],
-                           group_m, stream_ptr(x)), "gemm_ring")
-    return out
-
-
 def tune(M: int, N: int, K: int, device, iters: int = 20, max_candidates: int = 12) -> dict:
     """Measure every hipBLASLt solution for y[M,N] = x[M,K] @ W[N,K]^T on random operands;
     returns {"algo", "us", "heuristic_us", "candidates"}."""
@@ -863,7 +836,7 @@ def midm_gemm(x: torch.Tensor, w: torch.Tensor, epi: str = "store",
     return out
 
 
-__all__ = ["linear", "route", "ring_gemm", "ring_supported", "norm_linear", "glu_linear", "norm_glu", "fused_glu_ok",
+__all__ = ["linear", "route", "norm_linear", "glu_linear", "norm_glu", "fused_glu_ok",
            "linear_residual",
            "residual_fusable", "w4_glu_ok", "w4_ok", "w4_shape_ok", "w4_group_m", "mfma_gemm",
            "gemm_workspace", "new_gemm_workspace", "check_splitk_fault", "SplitKFault",

@@ -45,7 +45,7 @@ def main():
                                                     variant=v)))
         # variant 3 with explicit gemm_xd forms (gate_up / down)
         forms = {}
-        for gu, dn in ((281, 282), (281, 281), (1281, 1282), (241, 242), (141, 142), (1141, 1142)):
+        for gu, dn in ((1281, 1282), (281, 282), (281, 281), (241, 242), (141, 142), (1141, 1142)):
             try:
                 forms[f"{gu}/{dn}"] = timeit(lambda: ops.fused_moe(
                     x, lg, wgu, wdn, k, workspace=ws, out=out, variant=3, gu_form=gu, dn_form=dn))

@@ -237,7 +237,7 @@ def main():
         if eng is not None:
             eng.stats.clear()
         METRICS.reset()
-        pool = getattr(backend, "pool", None) if group is None else group.fleet
+        pool = getattr(backend, "pool", None)
         if pool is not None:  # replica counters arrive with the heartbeats
             time.sleep(2 * pool.hb_interval)
         rs0 = pool.health() if pool is not None else None

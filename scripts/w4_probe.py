@@ -61,13 +61,6 @@ def main():
                 fns[arm] = lambda: ops.act_glu(ops.linear(x, nxt()), a.epi)
             else:
                 fns[arm] = lambda: ops.linear(x, nxt())
-        elif arm[0] == "r":  # "rG": gemm_ring with row group G (default --group-m)
-            gm = int(arm[1:] or a.group_m)
-            if a.epi == "residual":
-                fns[arm] = lambda gm=gm: G.ring_gemm(x, nxt(), "residual", residual=res, out=res,
-                                                     group_m=gm)
-            else:
-                fns[arm] = lambda gm=gm: G.ring_gemm(x, nxt(), a.epi, out=out, group_m=gm)
         elif arm[0] == "x":  # "xFORM": gemm_xd form mt*100 + nf*10 + splitk (x0: by shape)
             form = int(arm[1:] or 0)
             if a.epi == "residual":

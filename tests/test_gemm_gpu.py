@@ -466,62 +466,6 @@ def test_norm_glu_takes_tuned_xd_form(hipk, monkeypatch):
     G.reset()
 
 
-# ------------------------------------------------------------ gemm_ring (4-slot LDS ring)
-@pytest.mark.parametrize("epi", ["store", "residual", "silu", "gelu_tanh"])
-@pytest.mark.parametrize("M,N,K", [(256, 256, 256), (8192, 8192, 256), (4500, 4096, 640),
-                                   (2300, 8192, 384), (1024, 4096, 1152), (300, 512, 4096),
-                                   (70000, 512, 256)])
-def test_ring_gemm_matches_fp32(hipk, epi, M, N, K):
-    """gemm_ring: 32-deep K stages in a 4-slot LDS ring, persistent (several tiles per
-    workgroup, a partial last row tile, the DMA stream running across tile seams, in-place
-    residual; 70000 rows = 274 row tiles, more tiles than CUs with two column tiles)."""
-    g = torch.Generator(device="cuda").manual_seed(M + 5 * N + 11 * K)
-    x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16, generator=g)
-    w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16, generator=g) * 0.05
-    nout = N // 2 if epi in ("silu", "gelu_tanh") else N
-    res = torch.randn(M, nout, device="cuda", dtype=torch.bfloat16, generator=g) if epi == "residual" else None
-    ref = _ref(x, w, epi, res)
-    if epi == "residual":
-        out = G.ring_gemm(x, w, epi, residual=res, out=res, group_m=4)
-        assert out.data_ptr() == res.data_ptr()
-    else:
-        out = G.ring_gemm(x, w, epi, group_m=4)
-    _check(out, ref)
-
-
-def test_ring_gemm_strided_input_and_graph_replay(hipk):
-    """x a column slice of a wider buffer (lda > K); replayed from a hipGraph."""
-    g = torch.Generator(device="cuda").manual_seed(7)
-    buf = torch.randn(3000, 1536, device="cuda", dtype=torch.bfloat16, generator=g)
-    x = buf[:, 256:1280]
-    w = torch.randn(1024, 1024, device="cuda", dtype=torch.bfloat16, generator=g) * 0.05
-    out = torch.empty(3000, 1024, device="cuda", dtype=torch.bfloat16)
-    G.ring_gemm(x, w, out=out)
-    torch.cuda.synchronize()
-    _check(out, _ref(x, w, "store", None))
-    out.zero_()
-    graph = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(graph):
-        G.ring_gemm(x, w, out=out)
-    graph.replay()
-    torch.cuda.synchronize()
-    _check(out, _ref(x, w, "store", None))
-
-
-def test_ring_gemm_rejects_bad_shapes(hipk):
-    x = torch.randn(512, 192, device="cuda", dtype=torch.bfloat16)
-    w = torch.randn(256, 192, device="cuda", dtype=torch.bfloat16)
-    with pytest.raises(AssertionError):
-        G.ring_gemm(x, w)  # K % 128 != 0
-    x = torch.randn(512, 128, device="cuda", dtype=torch.bfloat16)
-    w = torch.randn(256, 128, device="cuda", dtype=torch.bfloat16)
-    with pytest.raises(AssertionError):
-        G.ring_gemm(x, w)  # K < 256: fewer than two ring trips
-    with pytest.raises(RuntimeError):
-        G.check(G.hipk().gemm_ring(0, 0, 0, 0, 512, 384, 256, 256, 256, 384, 0, 0, 8, 0),
-                     "gemm_ring")  # N % 256 != 0 rejected by the launcher
-
-
 # ------------------------------------------------------------ split-K fault visibility
 @pytest.mark.parametrize("kind", ["xd", "w4"])
 def test_splitk_timeout_is_raised_and_next_gemm_is_correct(hipk, kind):
