@@ -85,6 +85,28 @@ def main():
         for s, e, n in p:
             phase_k[ph][n] += e - s
             phase_busy[ph] += e - s
+    if "--gaps" in sys.argv:
+        # where a pass's wall goes beyond its kernels: idle gaps inside the pass by the
+        # (previous kernel -> next kernel) transition, and the gap BEFORE each pass's first
+        # kernel (host work between passes, not inside the wall)
+        for ph in ("prefill", "decode"):
+            agg, cnt = collections.Counter(), collections.Counter()
+            n = 0
+            for p in passes:
+                if phase_of(p) != ph or (full_only and sum(e - s for s, e, _ in p) < 0.8 * busy_max[ph]):
+                    continue
+                n += 1
+                end = p[0][1]
+                for (s0, e0, n0), (s1, e1, n1) in zip(p, p[1:]):
+                    end = max(end, e0)
+                    if s1 > end:
+                        agg[f"{n0} -> {n1}"] += s1 - end
+                        cnt[f"{n0} -> {n1}"] += 1
+            if n:
+                print(f"\n{ph}: idle inside a pass {sum(agg.values()) / n / 1e6:.3f} ms / pass; top:")
+                for k, v in agg.most_common(8):
+                    print(f"  {v / n / 1e6:8.3f} ms/pass  {cnt[k] / n:6.1f} x/pass  {k}")
+        print()
     print("| phase | passes | mean GPU wall / pass (ms) | mean kernel-busy / pass (ms) | kernels / pass |")
     print("|---|---|---|---|---|")
     for ph in ("prefill", "decode"):

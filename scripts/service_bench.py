@@ -73,9 +73,12 @@ def build_backend(args):
 _OPTS = [("grpc.use_local_subchannel_pool", 1)]
 
 
-def run_load(target, n_requests: int, threads: int, seed: int):
+def run_load(target, n_requests: int, threads: int, seed: int, ready=None, go=None):
     """``threads`` client threads issue ``n_requests`` GetSmartReply RPCs in
-    total; returns (latencies s, errors, wall start, wall end, finish wall times)."""
+    total; returns (latencies s, errors, wall start, wall end, finish wall times).
+    ``ready`` / ``go`` (multiprocessing primitives): the client processes connect their
+    channels, report ready and wait for one common start, so the load window starts with
+    every client (as bench.py's waves do) instead of with process-spawn skew."""
     mode, address, token = target
     rng = random.Random(seed)
     if mode == "raft":
@@ -83,7 +86,7 @@ def run_load(target, n_requests: int, threads: int, seed: int):
             r = stub.GetSmartReply(raft_pb.SmartReplyRequest(token=token, channel_id="general"),
                                    timeout=120)
             assert r.success and len(r.suggestions) == 3
-        stubs = [make_stub(grpc.insecure_channel(address, options=_OPTS), RAFT_SERVICE) for _ in range(8)]
+        service = RAFT_SERVICE
     else:
         histories = [[llm_pb.Message(sender=m.sender, content=m.content)
                       for m in channel_history(rng, 5)] for _ in range(64)]
@@ -92,7 +95,9 @@ def run_load(target, n_requests: int, threads: int, seed: int):
             r = stub.GetSmartReply(llm_pb.SmartReplyRequest(
                 recent_messages=histories[rng.randrange(len(histories))]), timeout=120)
             assert len(r.suggestions) == 3
-        stubs = [make_stub(grpc.insecure_channel(address, options=_OPTS), LLM_SERVICE) for _ in range(8)]
+        service = LLM_SERVICE
+    chans = [grpc.insecure_channel(address, options=_OPTS) for _ in range(8)]
+    stubs = [make_stub(ch, service) for ch in chans]
     lat, errors, lock, it = [], [], threading.Lock(), iter(range(n_requests))
     fin = []
 
@@ -113,6 +118,11 @@ def run_load(target, n_requests: int, threads: int, seed: int):
                 lat.append(time.perf_counter() - t)
                 fin.append(time.time())
     ths = [threading.Thread(target=worker, args=(k,)) for k in range(threads)]
+    if go is not None:
+        for ch in chans:
+            grpc.channel_ready_future(ch).result(timeout=60)
+        ready.release()
+        go.wait()
     t_start = time.time()
     [t.start() for t in ths]
     [t.join() for t in ths]
@@ -181,8 +191,8 @@ def _delta(before, pool):
     return out
 
 
-def _client_main(target, n_requests, threads, seed, q):
-    q.put(run_load(target, n_requests, threads, seed))
+def _client_main(target, n_requests, threads, seed, q, ready, go):
+    q.put(run_load(target, n_requests, threads, seed, ready, go))
 
 
 def main():
@@ -248,11 +258,19 @@ def main():
             ctx = mp.get_context("spawn")
             q = ctx.Queue()
             k = args.client_procs
+            ready, go = ctx.Semaphore(0), ctx.Event()
             procs = [ctx.Process(target=_client_main,
                                  args=(target, args.requests // k + (i < args.requests % k),
-                                       args.concurrency // k + (i < args.concurrency % k), i + 1, q))
+                                       args.concurrency // k + (i < args.concurrency % k), i + 1, q,
+                                       ready, go))
                      for i in range(k)]
             [p.start() for p in procs]
+            for _ in procs:
+                ready.acquire()
+            if pool is not None:  # counters from the common start on (not process spawn)
+                time.sleep(2 * pool.hb_interval)
+                rs0 = pool.health()
+            go.set()
             lat, errors, starts, ends, fin = [], [], [], [], []
             for _ in procs:
                 la, er, t_s, t_e, fi = q.get()

@@ -34,7 +34,7 @@ def main():
     busy = sum(b - a for a, b, _ in st) / 1e6
     print(f"timed step: span {span:.1f} ms, kernel-busy {busy:.1f} ms ({100 * busy / span:.1f} %), "
           f"{len(st)} kernels")
-    dec = [r for r in st if r[2] == "drtc::paged_decode_kernel"]
+    dec = [r for r in st if r[2].startswith("drtc::paged_decode")]
     if dec:
         print(f"first decode attention at {(dec[0][0] - s0) / 1e6:.1f} ms (prefill phase before it)")
     for a, b in zip(st, st[1:]):
