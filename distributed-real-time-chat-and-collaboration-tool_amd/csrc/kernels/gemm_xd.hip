@@ -90,6 +90,7 @@ struct XdParams {
   int lda, ldb, ldc, ldr;
   int tiles_m, tiles_n, per_xcd;
   int splitk, up_off;
+  int slab_bytes;  // the split-K slab descriptor's range
   int* err;        // split-K fault word: a fixed slot of the workspace (the last counter),
                    // outside every launch's ticket range; read and cleared by the host
   int spin_limit;  // bound of the last ticket's ready poll (< 0: test hook, always fault)
@@ -275,25 +276,32 @@ DRTC_DEVICE void xd_tail(f32x4 (&acc)[C::FA][C::NF], bf16x8 (&fa0)[C::FA], bf16x
 // [2 t + 1] ready count; the error word p.err is a fixed slot outside every ticket range (a
 // partial that never arrived).  The slab holds one partial slot per slice and tile.  Returns
 // 0 for a slice that published its partial (it is done), 1 for the last ticket, which sums
-// the slices inside the epilogue (xd_sum: one fragment at a time, so the accumulators stay in
-// place) and re-arms the counters, 2 for a last ticket whose poll timed out: it records the
-// fault and does NOT re-arm (the host reads the word, zeroes the counters and raises).
+// the slices inside the epilogue (xd_sum_frags: groups of fragments, in place) and
+// re-arms the counters, 2 for a last ticket whose poll timed out: it records the fault and
+// does NOT re-arm (the host reads the word, zeroes the counters and raises).
 template <class C>
 constexpr int xd_tile_bytes() { return C::FA * C::NF * kXdThreads * 16; }
 constexpr int kXdSc1 = 16;  // cache-policy bits of the buffer op: sc1 (write-through)
 
+// A work item's place in its tile's combine: n slices (K ranges of the tile, in K order), this
+// one at position c; position s publishes into slab slot base + s (tile * n + s), of
+// xd_tile_bytes each.
+struct XdPart {
+  int n, c, base;
+};
 template <class C>
-DRTC_DEVICE __amdgpu_buffer_rsrc_t xd_slab(const XdParams& p, int tile) {
-  const int64_t slot = (int64_t)xd_tile_bytes<C>();
-  return __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(reinterpret_cast<char*>(p.slab) + (int64_t)tile * p.splitk * slot), (short)0,
-      (int)(p.splitk * slot), 0x00020000);
+DRTC_DEVICE unsigned xd_slot_off(const XdPart& q, int s) {
+  return (unsigned)(q.base + s) * (unsigned)xd_tile_bytes<C>();
+}
+
+DRTC_DEVICE __amdgpu_buffer_rsrc_t xd_slab(const XdParams& p) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)p.slab, (short)0, p.slab_bytes, 0x00020000);
 }
 
 template <class C>
-DRTC_DEVICE int xd_combine(const XdParams& p, f32x4 (&acc)[C::FA][C::NF], int tile, int slice,
-                           char* lds) {
-  const __amdgpu_buffer_rsrc_t slab = xd_slab<C>(p, tile);
+DRTC_DEVICE int xd_combine(const XdParams& p, f32x4 (&acc)[C::FA][C::NF], int tile,
+                           const XdPart& q, char* lds) {
+  const __amdgpu_buffer_rsrc_t slab = xd_slab(p);
   int* ticket = p.counters + 2 * tile;
   int* ready = ticket + 1;
   int* flag = reinterpret_cast<int*>(lds);
@@ -303,10 +311,10 @@ DRTC_DEVICE int xd_combine(const XdParams& p, f32x4 (&acc)[C::FA][C::NF], int ti
     *flag = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
   const int t = *flag;
-  if (t < p.splitk - 1) {
-    // publish the partial in this slice's slot, fragment order (16 B per lane, coalesced),
+  if (t < q.n - 1) {
+    // publish the partial in this position's slot, fragment order (16 B per lane, coalesced),
     // then count it ready
-    const int base = slice * xd_tile_bytes<C>();
+    const unsigned base = xd_slot_off<C>(q, q.c);
 #pragma unroll
     for (int i = 0; i < C::FA; ++i)
 #pragma unroll
@@ -319,12 +327,12 @@ DRTC_DEVICE int xd_combine(const XdParams& p, f32x4 (&acc)[C::FA][C::NF], int ti
     if (tid == 0) __hip_atomic_fetch_add(ready, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return 0;
   }
-  // the last ticket: every other slice holds a ticket (resident, past its K loop)
+  // the last ticket: every other contributor holds a ticket (resident, past its K loop)
   __syncthreads();  // every wave has read the ticket before the flag word is reused
   if (tid == 0) {
     int spins = 0, fault = 0;
     while (p.spin_limit < 0 ||
-           __hip_atomic_load(ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < p.splitk - 1) {
+           __hip_atomic_load(ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < q.n - 1) {
       __builtin_amdgcn_s_sleep(1);
       if (++spins > p.spin_limit) {  // never hang the GPU: record the fault, keep the counters
         __hip_atomic_store(p.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -338,22 +346,51 @@ DRTC_DEVICE int xd_combine(const XdParams& p, f32x4 (&acc)[C::FA][C::NF], int ti
   return *flag ? 2 : 1;
 }
 
-// Fragment (i, j) of the tile summed over the slices in slice order; `own` (this workgroup's
-// accumulators) stands in for its own slice.
-template <class C>
-DRTC_DEVICE f32x4 xd_sum(const XdParams& p, const __amdgpu_buffer_rsrc_t& slab, int i, int j,
-                         int slice, f32x4 own) {
-  const int off = ((i * C::NF + j) * kXdThreads + (int)threadIdx.x) * 16;
-  f32x4 v = own;
-  if (slice != 0)
-    v = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(slab, off, 0, kXdSc1));
-  for (int s = 1; s < p.splitk; ++s)
-    v += s == slice ? own
-                    : __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                    slab, off + s * xd_tile_bytes<C>(), 0, kXdSc1));
-  return v;
+// Split-K: the NJ fragments (i, col(jj)) of the tile summed over the slices in slice order
+// (this workgroup's accumulators at its own position: bitwise deterministic whatever the
+// arrival order) into out[].  Every load of a group of QG slice positions is issued before the
+// first is used, so the combine pays one memory latency per fragment group and slice group
+// instead of one per fragment and slice (the per-fragment form cost 66 us of an 88 us 2x8
+// split-4 GEMM, profiles/r5t).  A position past n, and this item's own, reads outside
+// the slab descriptor's range: 0, no memory access.
+template <class C, int NJ, int QG, bool GLU>
+DRTC_DEVICE void xd_sum_frags(const XdParams& p, const __amdgpu_buffer_rsrc_t& slab, int i,
+                              int j0, const XdPart& pq, const f32x4 (&acc)[C::FA][C::NF],
+                              f32x4 (&out)[NJ]) {
+  constexpr int NF = C::NF;
+  // fragment column of group member jj: plain j0 + jj; gated: the gate columns j0 + jj, then
+  // the up columns of the same outputs
+  auto col = [&](int jj) {
+    return GLU ? (jj < NJ / 2 ? j0 + jj : NF / 2 + j0 + jj - NJ / 2) : j0 + jj;
+  };
+  const unsigned tid = threadIdx.x;
+  const unsigned oob = (unsigned)p.slab_bytes;
+#pragma unroll
+  for (int s0 = 0; s0 < 8; s0 += QG) {  // n <= 8; whole groups past n are skipped
+    if (s0 >= pq.n) continue;
+    f32x4 v[QG][NJ];
+#pragma unroll
+    for (int q = 0; q < QG; ++q) {
+      const int s = s0 + q;
+      const unsigned base = (s == pq.c || s >= pq.n) ? oob : xd_slot_off<C>(pq, s);
+#pragma unroll
+      for (int jj = 0; jj < NJ; ++jj)
+        v[q][jj] = __builtin_bit_cast(
+            f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                       slab, base + ((i * NF + col(jj)) * kXdThreads + tid) * 16u, 0, kXdSc1));
+    }
+    // positions past n loaded 0: adding them is exact
+#pragma unroll
+    for (int q = 0; q < QG; ++q) {
+      const int s = s0 + q;
+#pragma unroll
+      for (int jj = 0; jj < NJ; ++jj) {
+        const f32x4 x = s == pq.c ? acc[i][col(jj)] : v[q][jj];
+        out[jj] = s == 0 ? x : out[jj] + x;
+      }
+    }
+  }
 }
-
 template <class C, int EPI, bool G = false>
 __global__ __launch_bounds__(kXdThreads, 1) void gemm_xd_kernel(XdParams p) {
   constexpr int MT = C::MT, NF = C::NF, FA = C::FA;
@@ -366,6 +403,10 @@ __global__ __launch_bounds__(kXdThreads, 1) void gemm_xd_kernel(XdParams p) {
   const int item = (b & 7) * p.per_xcd + (b >> 3);
   if (item >= ntiles * p.splitk) return;
   const int slice = item / ntiles, tile = item - slice * ntiles;
+  const int nkt = p.K >> 6;  // slice s: K tiles [s nkt / splitk, (s + 1) nkt / splitk)
+  const int kt0 = slice * nkt / p.splitk;
+  const int nk = (slice + 1) * nkt / p.splitk - kt0;
+  const XdPart q{p.splitk, slice, tile * p.splitk};
   const int tn = tile / p.tiles_m, tm = tile - tn * p.tiles_m;
   constexpr int TNO = xd_glu<EPI>() ? C::TN / 2 : C::TN;  // output columns per tile
   const int n0 = TNO * tn;
@@ -384,9 +425,6 @@ __global__ __launch_bounds__(kXdThreads, 1) void gemm_xd_kernel(XdParams p) {
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wv >> 1, wn = wv & 1, l16 = lane & 15, g = lane >> 4;
-  const int nkt = p.K >> 6;  // slice s: K tiles [s nkt / splitk, (s + 1) nkt / splitk)
-  const int kt0 = slice * nkt / p.splitk;
-  const int nk = (slice + 1) * nkt / p.splitk - kt0;
   const int64_t k0 = (int64_t)kt0 * 64;
 
   // ---- DMA plan: instruction i of wave wv fills stage rows 32 MT wv + 8 i + (lane >> 3)
@@ -469,7 +507,7 @@ __global__ __launch_bounds__(kXdThreads, 1) void gemm_xd_kernel(XdParams p) {
   bool part = false;   // split-K: this workgroup adds the other slices' partials
   bool rearm = false;  // ... and re-arms the tile's counters (not after a fault)
   if constexpr (C::SPLIT) {
-    const int st = xd_combine<C>(p, acc, tile, slice, xd_lds);
+    const int st = xd_combine<C>(p, acc, tile, q, xd_lds);
     if (st == 0) return;
     part = true;
     rearm = st == 1;
@@ -482,31 +520,51 @@ __global__ __launch_bounds__(kXdThreads, 1) void gemm_xd_kernel(XdParams p) {
   constexpr int OC = xd_glu<EPI>() ? 8 * NF : 16 * NF;  // output columns per wave
   constexpr int PITCH = 2 * OC + 16;
   char* ep = xd_lds + wv * 64 * MT * PITCH;
-  const __amdgpu_buffer_rsrc_t slab = xd_slab<C>(p, C::SPLIT ? tile : 0);
+  const __amdgpu_buffer_rsrc_t slab = xd_slab(p);
+  // split-K combine groups (the sums are consumed here, the accumulators stay in place): a
+  // row block's fragments x 4 slice positions in flight, NF 6 / 8 one position at a time
+  // (more spills: those kernels hold 192 / 256 accumulator registers)
+  constexpr int QG = NF >= 6 ? 1 : 4;
+  constexpr int NP = NF >= 8 ? 4 : NF / 2;  // gated: column pairs per group
+  constexpr int JB = NF >= 8 ? 8 : NF;      // plain: fragments per group
+  static_assert(NF % JB == 0 && (NF / 2) % NP == 0, "combine groups tile the fragments");
 #pragma unroll
   for (int i = 0; i < FA; ++i) {
     if constexpr (xd_glu<EPI>()) {
 #pragma unroll
-      for (int j = 0; j < NF / 2; ++j) {
-        f32x4 gv = acc[i][j], uv = acc[i][j + NF / 2];
-        if (C::SPLIT && part) {
-          gv = xd_sum<C>(p, slab, i, j, slice, gv);
-          uv = xd_sum<C>(p, slab, i, j + NF / 2, slice, uv);
+      for (int jp0 = 0; jp0 < NF / 2; jp0 += NP) {
+        f32x4 v[2 * NP];
+#pragma unroll
+        for (int jj = 0; jj < NP; ++jj) {
+          v[jj] = acc[i][jp0 + jj];
+          v[NP + jj] = acc[i][NF / 2 + jp0 + jj];
+        }
+        if constexpr (C::SPLIT) {
+          if (part) xd_sum_frags<C, 2 * NP, QG, true>(p, slab, i, jp0, q, acc, v);
         }
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
-          *reinterpret_cast<bf16_t*>(ep + (16 * i + 4 * g + r) * PITCH + (16 * j + l16) * 2) =
-              f2bf(act_value<EPI == XD_SILU ? 0 : 1>(gv[r]) * uv[r]);
+        for (int jj = 0; jj < NP; ++jj)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            *reinterpret_cast<bf16_t*>(ep + (16 * i + 4 * g + r) * PITCH +
+                                       (16 * (jp0 + jj) + l16) * 2) =
+                f2bf(act_value<EPI == XD_SILU ? 0 : 1>(v[jj][r]) * v[NP + jj][r]);
       }
     } else {
 #pragma unroll
-      for (int j = 0; j < NF; ++j) {
-        f32x4 v = acc[i][j];
-        if (C::SPLIT && part) v = xd_sum<C>(p, slab, i, j, slice, v);
+      for (int j0 = 0; j0 < NF; j0 += JB) {
+        f32x4 v[JB];
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
-          *reinterpret_cast<bf16_t*>(ep + (16 * i + 4 * g + r) * PITCH + (16 * j + l16) * 2) =
-              f2bf(v[r]);
+        for (int jj = 0; jj < JB; ++jj) v[jj] = acc[i][j0 + jj];
+        if constexpr (C::SPLIT) {
+          if (part) xd_sum_frags<C, JB, QG, false>(p, slab, i, j0, q, acc, v);
+        }
+#pragma unroll
+        for (int jj = 0; jj < JB; ++jj)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            *reinterpret_cast<bf16_t*>(ep + (16 * i + 4 * g + r) * PITCH +
+                                       (16 * (j0 + jj) + l16) * 2) = f2bf(v[jj][r]);
       }
     }
   }
@@ -690,12 +748,14 @@ int launch_gemm_xd(void* c, const void* a, const void* b, const void* r, int M, 
   const int64_t tiles = (int64_t)p.tiles_m * p.tiles_n;
   if (tiles * splitk * 8 >= (1ll << 31)) return -1;
   p.per_xcd = (int)((tiles * splitk + 7) / 8);
+  const int64_t need = gemm_xd_workspace_bytes(M, N, mt, nf, splitk, glu);
   if (splitk > 1) {
     // tile counters [0, 2 tiles) and the error word at the workspace's last slot
     if (slab == nullptr || counters == nullptr || n_counters < 2 * tiles + 2 ||
-        slab_bytes < gemm_xd_workspace_bytes(M, N, mt, nf, splitk, glu))
+        slab_bytes < need || need >= (1ll << 31))
       return -2;
     p.slab = (float*)slab;
+    p.slab_bytes = (int)need;
     p.counters = counters;
     p.err = counters + n_counters - 1;
     p.spin_limit = splitk_spin_limit();
@@ -747,10 +807,12 @@ int launch_gemm_xd_grouped(void* c, const void* a, const void* b, int a_rows, in
   if (tiles * splitk * 8 >= (1ll << 31)) return -1;
   p.per_xcd = (int)((tiles * splitk + 7) / 8);
   if (splitk > 1) {
+    const int64_t need = tiles * splitk * tm_rows * (32 * nf) * 4;
     if (slab == nullptr || counters == nullptr || n_counters < 2 * tiles + 2 ||
-        slab_bytes < tiles * splitk * tm_rows * (32 * nf) * 4)
+        slab_bytes < need || need >= (1ll << 31))
       return -2;
     p.slab = (float*)slab;
+    p.slab_bytes = (int)need;
     p.counters = counters;
     p.err = counters + n_counters - 1;
     p.spin_limit = splitk_spin_limit();
