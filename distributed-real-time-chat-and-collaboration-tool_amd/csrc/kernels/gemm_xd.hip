@@ -46,6 +46,7 @@
 #include "common.h"
 #include "launchers.h"
 
+#include <cstdlib>
 #include <utility>
 
 namespace drtc {
@@ -755,7 +756,12 @@ int launch_gemm_xd(void* c, const void* a, const void* b, const void* r, int M, 
         slab_bytes < need || need >= (1ll << 31))
       return -2;
     p.slab = (float*)slab;
-    p.slab_bytes = (int)need;
+    // DRTC_XD_SLAB_TIMING=1: a timing-only build of the combine's memory traffic - a zero-range
+    // slab descriptor drops every partial load and store while the ticket protocol, the
+    // instruction stream and the waits stay (cdna_hip_programming.md pricing recipe); WRONG
+    // results, probes only
+    static const bool slab_timing = std::getenv("DRTC_XD_SLAB_TIMING") != nullptr;
+    p.slab_bytes = slab_timing ? 0 : (int)need;
     p.counters = counters;
     p.err = counters + n_counters - 1;
     p.spin_limit = splitk_spin_limit();

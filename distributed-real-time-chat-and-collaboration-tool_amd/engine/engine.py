@@ -247,51 +247,56 @@ class LLMEngine:
         return reqs
 
     def step(self) -> list[Request]:
-        """One scheduler iteration. Returns requests finished in it."""
-        if self._aborts:
-            done = self._apply_aborts()
+        """One scheduler iteration. Returns requests finished in it.  The host wall time of
+        each iteration is added to ``stats[<kind>_us]`` (kind: decode / mixed / prefill /
+        drain / abort): with one decode step in flight that is the step's GPU time, and it
+        shows what the synchronous mixed and prefill steps cost a served engine."""
+        t0 = time.perf_counter()
+        done, kind = self._step()
+        if kind:
+            self.stats[kind + "_us"] += int(1e6 * (time.perf_counter() - t0))
             self._record(done)
-            return done
+        return done
+
+    def _step(self) -> tuple[list[Request], str | None]:
+        if self._aborts:
+            return self._apply_aborts(), "abort"
         busy = self.running or self._inflight is not None
         if self.mixed and busy and self._could_admit() and not self._admit_ready():
             # gathering arrivals for one chunk-sized mixed step: decode meanwhile
             with tracing.span("engine.decode", batch=len(self.running)):
-                done = self._run_decode()
-            self._record(done)
-            return done
+                return self._run_decode(), "decode"
         if self.mixed and busy and self._could_admit():
             done = self._process_inflight() if self._inflight is not None else []
             with self.lock:
                 self._ensure_blocks()
                 batch = self._admit(self._mixed_budget()) if self.running else self._admit()
+            kind = "drain"
             if batch and self.running:
+                kind = "mixed"
                 with tracing.span("engine.mixed", seqs=len(batch), batch=len(self.running)):
                     done += self._run_mixed(batch)
             elif batch:
+                kind = "prefill"
                 with tracing.span("engine.prefill", seqs=len(batch)):
                     done += self._run_prefill(batch)
             elif self.running:
+                kind = "decode"
                 with tracing.span("engine.decode", batch=len(self.running)):
                     done += self._run_decode()
-            self._record(done)
-            return done
+            return done, kind
         if self._inflight is not None and self._could_admit():
             # a prefill changes the slot layout: read the in-flight step first
-            done = self._process_inflight()
-            self._record(done)
-            return done
+            return self._process_inflight(), "drain"
         with self.lock:
             batch = self._admit() if (not self.running or self._could_admit()) else []
         if batch:
             with tracing.span("engine.prefill", seqs=len(batch)):
-                done = self._run_prefill(batch)
-        elif self.running or self._inflight is not None:
+                return self._run_prefill(batch), "prefill"
+        if self.running or self._inflight is not None:
             with tracing.span("engine.decode", batch=len(self.running)):
-                done = self._run_decode()
-        else:
-            return []
-        self._record(done)
-        return done
+                return self._run_decode(), "decode"
+        return [], None
 
     def _record(self, done: list[Request]) -> None:
         """Serving metrics: TTFT / TPOT / end-to-end latency per finished

@@ -186,7 +186,9 @@ def _delta(before, pool):
     out = []
     for b, a in zip(before, pool.health()):
         out.append({k: a[k] - b.get(k, 0) for k in ("idle_ms", "burst_hold_us", "prefill_steps", "prefill_tokens",
-                                                   "decode_steps", "mixed_steps", "decode_tokens")
+                                                   "decode_steps", "mixed_steps", "decode_tokens",
+                                                   "decode_us", "mixed_us", "prefill_us",
+                                                   "drain_us")
                     if isinstance(a.get(k), int)})
     return out
 
