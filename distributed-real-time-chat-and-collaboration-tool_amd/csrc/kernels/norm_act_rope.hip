@@ -27,6 +27,14 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(
   const bf16_t* xr = x + (int64_t)row * x_stride;
   float v[VPT][8];
   float ss = 0.f;
+  // the weight row is loaded with the activations, not after the reduction: a decode-sized
+  // norm (one short workgroup per row) then pays one memory latency, not two
+  bf16x8 wv[VPT];
+#pragma unroll
+  for (int i = 0; i < VPT; ++i) {
+    const int idx = (tid + i * 256) * 8;
+    if (idx < H) wv[i] = load_bf16x8(w + idx);
+  }
 #pragma unroll
   for (int i = 0; i < VPT; ++i) {
     const int idx = (tid + i * 256) * 8;
@@ -59,11 +67,10 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(
   for (int i = 0; i < VPT; ++i) {
     const int idx = (tid + i * 256) * 8;
     if (idx < H) {
-      bf16x8 wv = load_bf16x8(w + idx);
       bf16x8 o;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        float ww = bf2f(wv[j]);
+        float ww = bf2f(wv[i][j]);
         if constexpr (GEMMA) ww += 1.f;
         o[j] = f2bf(v[i][j] * rstd * ww);
       }
