@@ -84,8 +84,9 @@ class LLMEngine:
         # fraction and the ranks agree on the smallest resulting block count
         self.hbm_budget = hbm_budget
         if num_blocks is None:
-            num_blocks = PagedKVCache.auto_num_blocks(cfg, model.sh.hkv, self.device, kv_fraction,
-                                                      hbm_budget=hbm_budget)
+            num_blocks = PagedKVCache.auto_num_blocks(
+                cfg, model.sh.hkv, self.device, kv_fraction, hbm_budget=hbm_budget,
+                weight_bytes=model.weight_bytes() if hbm_budget is not None else None)
         # lockstep (SPMD) TP/EP ranks must schedule identically: every rank
         # sizes its cache from the same (smallest) block count
         num_blocks = model.pc.agree_min(num_blocks)

@@ -65,18 +65,22 @@ class PagedKVCache:
     @staticmethod
     def auto_num_blocks(cfg: ModelConfig, hkv_local: int, device, kv_fraction: float = 0.85,
                         reserve_bytes: int = 8 << 30, max_blocks: int | None = None,
-                        hbm_budget: float | None = None) -> int:
+                        hbm_budget: float | None = None, weight_bytes: int | None = None) -> int:
         """KV blocks for an engine on ``device``: ``kv_fraction`` of the HBM free beyond
         ``reserve_bytes`` (activations, GEMM workspaces, graphs) - or, with ``hbm_budget``
         (engine groups sharing a GPU, llm.server --serve ...:mem=F), what is left of
-        hbm_budget x the GPU's total HBM after this process's own allocations (weights) and
-        the reserve, whatever the other groups on the GPU hold or start in what order."""
+        hbm_budget x the GPU's total HBM after the group's weights (``weight_bytes``; this
+        process's allocations when not given) and the reserve, whatever the other groups on the
+        GPU - in other processes or in this one - hold or start in what order."""
         dev = torch.device(device)
         if dev.type == "cuda":
+            # blocks the caching allocator holds but no tensor uses are free HBM here: release
+            # them so that neither the free figure nor this process's own share counts them
+            torch.cuda.empty_cache()
             free, total = torch.cuda.mem_get_info(dev)
             budget = int(max(0, free - reserve_bytes) * kv_fraction)
             if hbm_budget is not None:
-                mine = torch.cuda.memory_reserved(dev)
+                mine = torch.cuda.memory_reserved(dev) if weight_bytes is None else weight_bytes
                 budget = min(budget, int(hbm_budget * total) - mine - reserve_bytes)
                 budget = max(budget, 0)
         else:
