@@ -17,7 +17,7 @@ from .attention import (KV_BLOCK, DecodeWorkspace, decode_partitioning, paged_de
                         paged_decode_ref, prefill_attention, prefill_attention_ref, prefill_tiles)
 from .gemm import (fused_glu_ok, glu_linear, linear, linear_residual, mfma_gemm, norm_glu,
                    norm_linear, residual_fusable, w4_glu_ok)
-from .moe import fused_moe, fused_moe_ref
+from .moe import fused_moe, fused_moe_ref, router_logits
 from .norm import PendingNorm, rmsnorm, rmsnorm_ref
 from .rope import build_rope_cache, kv_write_v, kv_write_v_ref, rope_kv_, rope_kv_ref
 from .sampling import sample, sample_ref
@@ -25,7 +25,7 @@ from .sampling import sample, sample_ref
 __all__ = [
     "on_gpu", "reference_mode", "linear", "norm_linear", "glu_linear", "norm_glu", "w4_glu_ok",
     "fused_glu_ok",
-    "mfma_gemm", "linear_residual", "residual_fusable", "PendingNorm", "fused_moe",
+    "mfma_gemm", "linear_residual", "residual_fusable", "PendingNorm", "fused_moe", "router_logits",
     "fused_moe_ref", "act_glu", "act_glu_ref", "KV_BLOCK", "DecodeWorkspace",
     "decode_partitioning", "paged_decode_attention", "paged_decode_attention_rope",
     "paged_decode_ref", "prefill_attention", "prefill_attention_ref", "prefill_tiles",

@@ -76,6 +76,22 @@ def make_workspace(tokens: int, hidden: int, inter: int, e_local: int, top_k: in
     return torch.empty(n, dtype=torch.uint8, device=device)
 
 
+def router_logits(x: torch.Tensor, w_router: torch.Tensor) -> torch.Tensor:
+    """Router logits x [T, H] . w_router [E, H]^T -> [T, E] (contiguous), on the skinny HIP
+    GEMM transposed: the E router rows are the kernel's few activation rows and the T tokens
+    its streamed weight rows, so x is read once and no library GEMM runs in the MoE layer
+    (ref llm_server/llm_server.py:403: the suggestions model).  Shapes the skinny kernel does
+    not take (T not a multiple of its row block, E > 8) go to F.linear."""
+    from . import gemm as G
+
+    T, H = x.shape
+    E = w_router.shape[0]
+    if (on_gpu(x) and x.is_contiguous() and w_router.is_contiguous() and E <= 8
+            and G.skinny_supports(3, E, T, H, w_router.stride(0))):
+        return G.skinny_linear(w_router, x, variant=3).t().contiguous()
+    return F.linear(x, w_router)
+
+
 def fused_moe(x: torch.Tensor, router_logits: torch.Tensor, w_gu: torch.Tensor,
               w_dn: torch.Tensor, top_k: int, act: str = "silu", num_experts: int | None = None,
               e_off: int = 0, workspace: torch.Tensor | None = None,
@@ -135,7 +151,3 @@ def fused_moe(x: torch.Tensor, router_logits: torch.Tensor, w_gu: torch.Tensor,
                       cnt.numel() if cnt is not None else 0, st), "moe")
     return out
 
-
-def router_logits(x: torch.Tensor, router_w: torch.Tensor) -> torch.Tensor:
-    """bf16 router logits (the kernel up-converts)."""
-    return F.linear(x, router_w)

@@ -173,7 +173,9 @@ def ep_combine(back: torch.Tensor, dst_row: torch.Tensor, w: torch.Tensor, T: in
 def route(x: torch.Tensor, router_w: torch.Tensor, top_k: int):
     """(expert ids [T, k], weights [T, k] fp32): top-k of the bf16 router logits,
     softmax over the selected k, ties to the lower id (the fused kernel's rule)."""
-    return route_ref(F.linear(x, router_w), top_k)
+    from ..ops.moe import router_logits
+
+    return route_ref(router_logits(x, router_w), top_k)
 
 
 def _one_hot_logits(expert_ids: torch.Tensor, num_experts: int, dtype) -> torch.Tensor:

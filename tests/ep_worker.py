@@ -26,7 +26,12 @@ def main():
     x_all = torch.randn(world * T, H, generator=g).to(torch.bfloat16).cuda()
     el = E // world
     x = x_all[rank * T:(rank + 1) * T].contiguous()
-    ref = ops.fused_moe_ref(x_all, torch.nn.functional.linear(x_all, router), gu, dn, k)
+    # the reference routes on the logits each rank computes for its rows (ops.router_logits)
+    def logits_by_rank(xa, t):
+        return torch.cat([ops.router_logits(xa[r * t:(r + 1) * t].contiguous(), router)
+                          for r in range(world)])
+
+    ref = ops.fused_moe_ref(x_all, logits_by_rank(x_all, T), gu, dn, k)
     ref = ref[rank * T:(rank + 1) * T].float()
     gl, dl = gu[rank * el:(rank + 1) * el].contiguous(), dn[rank * el:(rank + 1) * el].contiguous()
     for form in ("exact", "static", "cap"):
@@ -70,7 +75,7 @@ def main():
     # capacity form runs without a host sync and matches the reference
     T3 = 4096
     x3_all = torch.randn(world * T3, H, generator=g).to(torch.bfloat16).cuda()
-    ref3 = ops.fused_moe_ref(x3_all, torch.nn.functional.linear(x3_all, router), gu, dn, k)
+    ref3 = ops.fused_moe_ref(x3_all, logits_by_rank(x3_all, T3), gu, dn, k)
     ref3 = ref3[rank * T3:(rank + 1) * T3].float()
     ovf = EpOverflow("cuda")
     y3 = ep_moe_forward(x3_all[rank * T3:(rank + 1) * T3].contiguous(), router, gl, dl, k,

@@ -819,3 +819,27 @@ def test_linear_residual(hipk, M, N, K):
     y = ops.linear_residual(x, w, res)
     assert y.data_ptr() == res.data_ptr()
     _close(y, ref, 3e-2, 2e-2, "linear_residual")
+
+
+@pytest.mark.parametrize("T", [32, 1024, 8192, 1000])
+def test_router_logits_on_skinny_kernel_match_fp32(hipk, T):
+    """MoE router logits through the transposed skinny HIP GEMM (ops.router_logits): the
+    8 router rows as the activation rows, the T tokens as the streamed rows; T = 1000 is not a
+    multiple of the kernel's row block and takes F.linear."""
+    from drtc_amd.ops import moe as M
+    g = torch.Generator(device="cuda").manual_seed(T)
+    x = torch.randn(T, 4096, device="cuda", dtype=torch.bfloat16, generator=g)
+    wr = torch.randn(8, 4096, device="cuda", dtype=torch.bfloat16, generator=g) * 0.02
+    lib = []
+    real = M.F.linear
+    M.F.linear = lambda *a, **k: lib.append(1) or real(*a, **k)
+    try:
+        got = M.router_logits(x, wr)
+    finally:
+        M.F.linear = real
+    assert bool(lib) == (T % 16 != 0)  # the library GEMM only where the HIP kernel cannot
+    torch.cuda.synchronize()
+    ref = x.float() @ wr.float().t()
+    assert got.shape == (T, 8) and got.is_contiguous() and got.dtype == torch.bfloat16
+    err = (got.float() - ref).abs().max().item()
+    assert err <= 1.5e-2 * ref.abs().max().item(), err
