@@ -60,6 +60,7 @@ def main():
     (Hq, Hkv, D), mixes = GEOMS[sys.argv[2] if len(sys.argv) > 2 else "llama8b"]
     cases = [(n, B, (lambda lo=lo, hi=hi: rng.randint(lo, hi))) for n, B, (lo, hi) in mixes] if mixes else [
         ("B1024 ctx150-200", 1024, lambda: rng.randint(150, 200)),
+        ("B1024 ctx150-450", 1024, lambda: rng.randint(150, 450)),  # a suggestions wave mid-decode
         ("B512 ctx150-200", 512, lambda: rng.randint(150, 200)),
         ("B256 ctx600-1400", 256, lambda: rng.randint(600, 1400)),
         ("B64 ctx1500-2000", 64, lambda: rng.randint(1500, 2000)),
