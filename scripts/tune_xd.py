@@ -70,7 +70,8 @@ def main() -> None:
     ap.add_argument("--ms", default=",".join(map(str, BUCKETS)))
     ap.add_argument("--min-gain", type=float, default=0.03)
     ap.add_argument("--out", default="gpurun_out/xd_tuned.json")
-    ap.add_argument("--gemms", default="qkv,o,gate_up,down", help="projections to tune")
+    ap.add_argument("--gemms", default="qkv,o,gate_up,down",
+                    help="projections to tune (lm_head too: profiles/r5ak)")
     ap.add_argument("--nt-any", action="store_true",
                     help="non-temporal forms among the candidates at every M, not only where "
                          "the batch fits one row tile")
@@ -89,8 +90,8 @@ def main() -> None:
     for spec in a.configs.split(","):
         model, tp = spec.split(":")
         for name, (N, K) in projection_shapes(model, int(tp)).items():
-            if name == "lm_head" or name not in a.gemms.split(","):
-                continue  # lm_head: 256 x 256 library tiles win at vocabulary widths
+            if name not in a.gemms.split(","):
+                continue
             wbytes = N * K * 2
             ncopy = max(2, min(10, -(-512 * 2**20 // wbytes)))
             ws = [(torch.randn(N, K, device=dev, generator=g) * 0.02).to(torch.bfloat16)
