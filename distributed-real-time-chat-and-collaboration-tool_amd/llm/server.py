@@ -40,7 +40,7 @@ from concurrent import futures
 
 import grpc
 
-from ..protos import LLM_SERVICE, add_servicer
+from ..protos import LLM_SERVICE, SERVER_QUEUE_OPTS, add_servicer
 from ..utils.config import parse_with_config
 from ..utils.logging_utils import setup_logging
 from .backends import ScriptedBackend
@@ -226,7 +226,7 @@ def serve(backend, port: int = 50055, workers: int = 64, bind: str = "[::]", par
     """Thread-pool gRPC server of the four RPCs over ``backend`` (SO_REUSEPORT off: a second
     server on a taken port fails instead of silently sharing it)."""
     server = grpc.server(futures.ThreadPoolExecutor(max_workers=workers),
-                         options=[("grpc.so_reuseport", 0)])
+                         options=[("grpc.so_reuseport", 0)] + SERVER_QUEUE_OPTS)
     add_servicer(server, LLM_SERVICE, LLMServicer(backend, params))
     if server.add_insecure_port(f"{bind}:{port}") == 0:
         raise RuntimeError(f"cannot bind port {port}")
@@ -256,7 +256,7 @@ class AioServer:
         asyncio.set_event_loop(self.loop)
 
         async def start():
-            srv = grpc.aio.server()
+            srv = grpc.aio.server(options=SERVER_QUEUE_OPTS)
             add_servicer(srv, LLM_SERVICE, AsyncLLMServicer(backend, params))
             if srv.add_insecure_port(f"{bind}:{port}") == 0:
                 raise RuntimeError(f"cannot bind port {port}")

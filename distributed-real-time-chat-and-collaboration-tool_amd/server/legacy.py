@@ -29,7 +29,7 @@ from concurrent import futures
 
 import grpc
 
-from ..protos import CHAT_SERVICE, add_servicer, chat_pb
+from ..protos import CHAT_SERVICE, SERVER_QUEUE_OPTS, add_servicer, chat_pb
 from ..utils import auth, pickle_compat
 from ..utils.config import parse_with_config
 from ..utils.logging_utils import setup_logging
@@ -606,7 +606,7 @@ class LegacyChatServer:
 
 def serve(port: int = 50050, data_dir: str = "server_data", block: bool = True, **kw):
     srv = LegacyChatServer(data_dir=data_dir, port=port, **kw)
-    server = grpc.server(futures.ThreadPoolExecutor(max_workers=32))
+    server = grpc.server(futures.ThreadPoolExecutor(max_workers=32), options=SERVER_QUEUE_OPTS)
     add_servicer(server, CHAT_SERVICE, srv)
     if server.add_insecure_port(f"[::]:{port}") == 0:
         raise RuntimeError(f"cannot bind {port}")

@@ -16,7 +16,7 @@ from concurrent import futures
 
 import grpc
 
-from ..protos import RAFT_SERVICE, RAFT_SNAPSHOT_SERVICE, add_servicer
+from ..protos import RAFT_SERVICE, RAFT_SNAPSHOT_SERVICE, SERVER_QUEUE_OPTS, add_servicer
 from ..raft.core import RaftConfig
 from ..utils.config import parse_with_config
 from ..utils.logging_utils import setup_logging
@@ -30,7 +30,7 @@ SERVER_OPTS = [
     ("grpc.max_receive_message_length", 50 * 1024 * 1024),
     ("grpc.keepalive_time_ms", 10000),
     ("grpc.keepalive_timeout_ms", 5000),
-]
+] + SERVER_QUEUE_OPTS
 
 
 def parse_peers(s: str | None) -> dict:

@@ -17,6 +17,7 @@ Reports one JSON line: requests/s, generated tokens/s, p50/p99 latency.
   python scripts/service_bench.py --backend scripted --mode raft --requests 200
 """
 import argparse
+import collections
 import json
 import multiprocessing as mp
 import os
@@ -112,7 +113,7 @@ def run_load(target, n_requests: int, threads: int, seed: int, ready=None, go=No
                 one(stub)
             except (grpc.RpcError, AssertionError) as e:
                 with lock:
-                    errors.append(repr(e)[:200])
+                    errors.append(f"{repr(e)[:400]} (at {time.time() - t_start:.1f} s)")
                 continue
             with lock:
                 lat.append(time.perf_counter() - t)
@@ -305,6 +306,8 @@ def main():
             "backend": args.backend, "frontend": args.frontend, "model": args.model if args.backend != "scripted" else None,
             "client_procs": args.client_procs,
             "requests": len(lat), "errors": len(errors), "concurrency": args.concurrency, "seconds": round(dt, 3),
+            "error_kinds": dict(collections.Counter(e.split(" (at ")[0] for e in errors).most_common(5)),
+            "error_times_s": sorted(float(e.rsplit("(at ", 1)[1][:-3]) for e in errors)[:20],
             "requests_per_s": round(len(lat) / dt, 2),
             "gen_tokens_per_s": round(gen_tokens / dt, 1) if gen_tokens else None,
             "steady_requests_per_s": round(steady, 2) if steady else None,

@@ -111,6 +111,44 @@ def test_llm_service_fallbacks_on_backend_error():
         srv.stop(0)
 
 
+def test_llm_service_takes_a_burst_of_concurrent_calls():
+    """1,200 smart-reply RPCs started together (a client wave over a 1,024-slot engine) all
+    complete: the server's pending-call queue is sized above grpc-core's default of 1,000,
+    which CANCELs the excess of such a burst (protos.SERVER_QUEUE_OPTS)."""
+    from drtc_amd.llm.backends import ScriptedBackend
+
+    n = 1200
+    port = free_port()
+    srv = serve_llm(ScriptedBackend(delay=0.05), port=port, bind="127.0.0.1", workers=n + 8)
+    chans = [grpc.insecure_channel(f"127.0.0.1:{port}", options=[("grpc.use_local_subchannel_pool", 1)])
+             for _ in range(16)]
+    try:
+        for ch in chans:
+            grpc.channel_ready_future(ch).result(timeout=30)
+        stubs = [make_stub(ch, LLM_SERVICE) for ch in chans]
+        msgs = [llm_pb.Message(sender="a", content="x")]
+        go, errors, ok = threading.Event(), [], []
+
+        def one(k):
+            go.wait()
+            try:
+                r = stubs[k % len(stubs)].GetSmartReply(
+                    llm_pb.SmartReplyRequest(recent_messages=msgs), timeout=60)
+                ok.append(len(r.suggestions))
+            except grpc.RpcError as e:
+                errors.append(e.code())
+
+        ths = [threading.Thread(target=one, args=(k,)) for k in range(n)]
+        [t.start() for t in ths]
+        go.set()
+        [t.join() for t in ths]
+        assert not errors, set(errors)
+        assert len(ok) == n and set(ok) == {3}
+    finally:
+        [ch.close() for ch in chans]
+        srv.stop(0)
+
+
 def test_ask_ai_retries_with_backoff():
     """GetLLMAnswer retries failures and empty answers with exponential backoff
     (ref llm_server.py:164-208) and stops retrying when the deadline is near."""
