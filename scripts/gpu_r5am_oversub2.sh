@@ -1,10 +1,11 @@
 #!/bin/bash
 # Round 5: two consecutive direct-service runs at 1,280 closed-loop clients over the 1,024-slot
 # engine (the error kinds reported), against the headline engine run on the same box.
+# (r5an: the same after the servers' pending-call queue fix.)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export HSA_ENABLE_IPC_MODE_LEGACY=0
-O=gpurun_out/r5am; mkdir -p $O
+O=gpurun_out/${R5_OUT:-r5am}; mkdir -p $O
 timeout -k 10 400 python -u bench.py --steps 6 --warmup 2 > $O/engine.json 2> $O/engine.err || { tail -5 $O/engine.err; exit 1; }
 python3 -c "import json;d=json.load(open('$O/engine.json'));print('engine', d['value'])"
 for r in 1 2; do
