@@ -29,3 +29,41 @@ def hipk():
     from drtc_amd.ops._ext import hipk as _h
 
     return _h()
+
+
+def pytest_sessionfinish(session, exitstatus):
+    """Leave no thread running into interpreter finalization: a daemon thread that is inside
+    native code (HIP / torch / gRPC) when CPython finalizes is ended with pthread_exit, whose
+    forced unwind through C++ frames aborts the process ("terminate called without an active
+    exception") after every test passed.  Join what the tests left (engine loops, server
+    handlers still returning) and drain the GPU while the runtime is intact."""
+    import gc
+    import threading
+    import time
+
+    main = threading.main_thread()
+    deadline = time.time() + 30
+    for t in threading.enumerate():
+        if t is not main and t.is_alive():
+            t.join(timeout=max(0.1, deadline - time.time()))
+    gc.collect()
+    try:
+        import torch
+
+        if torch.cuda.is_initialized():
+            torch.cuda.synchronize()
+    except Exception:
+        pass
+
+
+def pytest_unconfigure(config):
+    """DRTC_TEST_THREADS=1: list the threads still alive when the session ends (a native
+    thread left running is what aborts an interpreter at exit)."""
+    import os
+    import sys
+    import threading
+
+    if os.environ.get("DRTC_TEST_THREADS") == "1":
+        for t in threading.enumerate():
+            print(f"[threads at exit] {t.name} daemon={t.daemon} alive={t.is_alive()}",
+                  file=sys.stderr, flush=True)

@@ -27,8 +27,9 @@ def test_llm_service_on_gpu_through_raft_cluster(hipk, tmp_path):
         f.max_new_tokens = 8
     port = free_port()
     srv = serve_llm(backend, port=port, bind="127.0.0.1", params=fp)
+    ch = grpc.insecure_channel(f"127.0.0.1:{port}")
     try:
-        s = make_stub(grpc.insecure_channel(f"127.0.0.1:{port}"), LLM_SERVICE)
+        s = make_stub(ch, LLM_SERVICE)
         msgs = [llm_pb.Message(sender="alice", content="ship it friday?"),
                 llm_pb.Message(sender="bob", content="after review")]
         outs = []
@@ -49,7 +50,8 @@ def test_llm_service_on_gpu_through_raft_cluster(hipk, tmp_path):
             r = st.GetLLMAnswer(raft_pb.LLMRequest(token=tok, query="status?"))
             assert r.success
     finally:
-        srv.stop(0)
+        ch.close()
+        srv.stop(0).wait(10)
         backend.close()
 
 
@@ -77,8 +79,9 @@ def test_llm_server_serves_two_models_side_by_side_on_one_gpu(hipk):
         f.max_new_tokens = 6
     port = free_port()
     srv = S.serve(router, port=port, bind="127.0.0.1", params=fp)
+    ch = grpc.insecure_channel(f"127.0.0.1:{port}")
     try:
-        stub = make_stub(grpc.insecure_channel(f"127.0.0.1:{port}"), LLM_SERVICE)
+        stub = make_stub(ch, LLM_SERVICE)
         msgs = [llm_pb.Message(sender="a", content="lunch tomorrow?")]
         s0 = dict(smart.engine.stats), dict(summ.engine.stats)
         r = stub.GetSmartReply(llm_pb.SmartReplyRequest(request_id="1", recent_messages=msgs),
@@ -93,5 +96,6 @@ def test_llm_server_serves_two_models_side_by_side_on_one_gpu(hipk):
         assert s2[1].get("prefill_steps", 0) > s1[1].get("prefill_steps", 0)
         assert s2[0].get("prefill_steps", 0) == s1[0].get("prefill_steps", 0)
     finally:
-        srv.stop(0)
+        ch.close()
+        srv.stop(0).wait(10)
         router.close()
