@@ -51,7 +51,9 @@ GEOMS = {
     "gemma": ((8, 1, 256), [("B1024 ctx150-200", 1024, (150, 200)), ("B256 ctx150-200", 256, (150, 200)),
                             ("B256 ctx600-1400", 256, (600, 1400))]),
     "mixtral": ((32, 8, 128), [("B256 ctx175-270", 256, (175, 270)), ("B64 ctx175-270", 64, (175, 270))]),
-    "llama70b": ((64, 8, 128), [("B256 ctx136-286", 256, (136, 286)), ("B64 ctx136-286", 64, (136, 286))]),
+    "llama70b": ((64, 8, 128), [("B256 ctx136-286", 256, (136, 286)),
+                                ("B256 ctx136-436", 256, (136, 436)),  # mid-decode of the ask wave
+                                ("B64 ctx136-286", 64, (136, 286))]),
 }
 
 
