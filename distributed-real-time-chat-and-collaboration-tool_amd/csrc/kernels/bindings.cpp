@@ -83,11 +83,12 @@ PYBIND11_MODULE(_hipk, m) {
   m.def("moe", [](u64 out, u64 x, u64 logits, u64 w_gu, u64 w_dn, int T, int H, int I, int E,
                   int k, int e_off, int e_local, int act, u64 ws, int64_t ws_bytes, int variant,
                   int gu_form, int dn_form, u64 slab, int64_t slab_bytes, u64 counters,
-                  int n_counters, u64 st) {
+                  int n_counters, int logit_ts, int logit_es, u64 st) {
     return drtc::launch_moe(P<void>(out), P<const void>(x), P<const void>(logits),
                             P<const void>(w_gu), P<const void>(w_dn), T, H, I, E, k, e_off,
                             e_local, act, P<void>(ws), ws_bytes, variant, gu_form, dn_form,
-                            P<void>(slab), slab_bytes, P<int>(counters), n_counters, S(st));
+                            P<void>(slab), slab_bytes, P<int>(counters), n_counters, logit_ts,
+                            logit_es, S(st));
   });
   // gemm_w4 (ops.gemm.mfma_gemm): variant 7 + schedule bits (7 per-tile, 9 temporal stores,
   // 15 persistent, 31 persistent with the per-XCD K rotation)

@@ -57,7 +57,8 @@ int launch_sample(int* out_tokens, const void* logits, int B, int V, int ld,
 int launch_moe(void* out, const void* x, const void* router_logits, const void* w_gu,
                const void* w_dn, int T, int H, int I, int E, int k, int e_off, int e_local,
                int act, void* workspace, int64_t ws_bytes, int variant, int gu_form, int dn_form,
-               void* slab, int64_t slab_bytes, int* counters, int n_counters, hipStream_t st);
+               void* slab, int64_t slab_bytes, int* counters, int n_counters, int logit_ts,
+               int logit_es, hipStream_t st);
 int64_t moe_workspace_bytes(int T, int H, int I, int e_local, int k);
 // Expert-parallel dispatch / combine with a static per-destination capacity (moe_ep.hip).
 int launch_ep_plan(const int* topi, int P, int e_local, int world, int cap, int* dst_row,

@@ -34,20 +34,22 @@ __global__ __launch_bounds__(1024) void moe_align_kernel(
     int* __restrict__ inv_pos, float* __restrict__ topk_w,
     int* __restrict__ tile_expert, int* __restrict__ tile_row0, int* __restrict__ tile_rows,
     int* __restrict__ n_tiles, int* __restrict__ local_range, int max_tiles, int e_off,
-    int e_local, int bm) {
+    int e_local, int bm, int lts, int les) {
   __shared__ int cnt[256], off[257], fill[256], toff[257];
   const int tid = threadIdx.x;
   for (int e = tid; e < 256; e += 1024) { cnt[e] = 0; fill[e] = 0; }
   __syncthreads();
   for (int t = tid; t < T; t += 1024) {
-    const bf16_t* lr = logits + (int64_t)t * E;
+    // logit (t, e) at t * lts + e * les: [T, E] rows, or the router GEMM's [E, T] output read
+    // in place (lts = 1: consecutive threads read consecutive tokens of one expert row)
+    const bf16_t* lr = logits + (int64_t)t * lts;
     // sorted top-8 list kept in registers (fully unrolled: no scratch)
     float v[kMoeMaxK];
     int id[kMoeMaxK];
 #pragma unroll
     for (int j = 0; j < kMoeMaxK; ++j) { v[j] = -INFINITY; id[j] = 0x7fffffff; }
     for (int e = 0; e < E; ++e) {
-      float x = bf2f(lr[e]);
+      float x = bf2f(lr[(int64_t)e * les]);
       int xi = e;
 #pragma unroll
       for (int j = 0; j < kMoeMaxK; ++j) {
@@ -446,8 +448,10 @@ static void moe_xd_form(int form, int& mt, int& nf, int& sk) {
 int launch_moe(void* out, const void* x, const void* router_logits, const void* w_gu,
                const void* w_dn, int T, int H, int I, int E, int k, int e_off, int e_local,
                int act, void* workspace, int64_t ws_bytes, int variant, int gu_form, int dn_form,
-               void* slab, int64_t slab_bytes, int* counters, int n_counters, hipStream_t st) {
+               void* slab, int64_t slab_bytes, int* counters, int n_counters, int logit_ts,
+               int logit_es, hipStream_t st) {
   if (T == 0) return 0;
+  if (!((logit_ts == E && logit_es == 1) || (logit_ts == 1 && logit_es >= T))) return -1;
   if (E > 256 || k > kMoeMaxK || k < 1 || k > E || H % 128 != 0 || I % 64 != 0 || H % kBK != 0 ||
       e_off < 0 || e_local < 1 || e_off + e_local > E)
     return -1;
@@ -514,7 +518,7 @@ int launch_moe(void* out, const void* x, const void* router_logits, const void* 
   if (o > ws_bytes) return -2;
   hipLaunchKernelGGL(moe_align_kernel, dim3(1), dim3(1024), 0, st, (const bf16_t*)router_logits, T,
                      E, k, sorted_tok, sorted_w, inv_pos, topk_w, t_e, t_r0, t_n, n_tiles, local_range,
-                     max_tiles, e_off, e_local, bm);
+                     max_tiles, e_off, e_local, bm, logit_ts, logit_es);
   const dim3 g_gu((I / 64) * max_tiles), g_dn((H / 128) * max_tiles);
   if (variant == 3) {
     int mt, nf, sk, e;

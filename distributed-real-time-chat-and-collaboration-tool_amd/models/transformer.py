@@ -324,7 +324,8 @@ class TransformerLM:
             all_gather_into_tensor(out, y.contiguous(), group=pc.ep_group)
             return out
         if ops.on_gpu(x):
-            out = ops.fused_moe(x, ops.router_logits(x, L["router"]), L["gate_up"], L["down"],
+            logits = ops.router_logits(x, L["router"], contiguous=False)  # [E, T] read in place
+            out = ops.fused_moe(x, logits, L["gate_up"], L["down"],
                                 cfg.experts_per_token, cfg.act, cfg.num_experts,
                                 sh.expert_offset, workspace=self.moe_ws)
             if self.pc.ep_size > 1:
@@ -497,9 +498,10 @@ class TransformerLM:
                 # experts TP-sharded over the intermediate dim: every rank needs
                 # every token, partial outputs are reduce-scattered
                 xg = pc.all_gather_rows(x.materialize())
-                part = ops.fused_moe(xg, ops.router_logits(xg, L["router"]), L["gate_up"],
-                                     L["down"], cfg.experts_per_token, cfg.act, cfg.num_experts,
-                                     self.sh.expert_offset, workspace=self.moe_ws) \
+                part = ops.fused_moe(xg, ops.router_logits(xg, L["router"], contiguous=False),
+                                     L["gate_up"], L["down"], cfg.experts_per_token, cfg.act,
+                                     cfg.num_experts, self.sh.expert_offset,
+                                     workspace=self.moe_ws) \
                     if ops.on_gpu(xg) else ops.fused_moe_ref(
                         xg, F.linear(xg, L["router"]), L["gate_up"], L["down"],
                         cfg.experts_per_token, cfg.act, self.sh.expert_offset)

@@ -76,19 +76,27 @@ def make_workspace(tokens: int, hidden: int, inter: int, e_local: int, top_k: in
     return torch.empty(n, dtype=torch.uint8, device=device)
 
 
-def router_logits(x: torch.Tensor, w_router: torch.Tensor) -> torch.Tensor:
-    """Router logits x [T, H] . w_router [E, H]^T -> [T, E] (contiguous), on the skinny HIP
-    GEMM transposed: the E router rows are the kernel's few activation rows and the T tokens
-    its streamed weight rows, so x is read once and no library GEMM runs in the MoE layer
-    (ref llm_server/llm_server.py:403: the suggestions model).  Shapes the skinny kernel does
-    not take (T not a multiple of its row block, E > 8) go to F.linear."""
+# fused_moe reads the router GEMM's [E, T] output in place (DRTC_ROUTER_VIEW=0: the
+# transposed copy of round 5's first router form, for A/B)
+ROUTER_VIEW = os.environ.get("DRTC_ROUTER_VIEW", "1") != "0"
+
+
+def router_logits(x: torch.Tensor, w_router: torch.Tensor, contiguous: bool = True) -> torch.Tensor:
+    """Router logits x [T, H] . w_router [E, H]^T -> [T, E], on the skinny HIP GEMM
+    transposed: the E router rows are the kernel's few activation rows and the T tokens its
+    streamed weight rows, so x is read once and no library GEMM runs in the MoE layer (ref
+    llm_server/llm_server.py:403: the suggestions model).  ``contiguous=False`` returns the
+    kernel's [E, T] output as a transposed [T, E] view (strides (1, T)), which ``fused_moe``
+    reads in place (no transpose copy per layer).  Shapes the skinny kernel does not take (T not
+    a multiple of its row block, E > 8) go to F.linear."""
     from . import gemm as G
 
     T, H = x.shape
     E = w_router.shape[0]
     if (on_gpu(x) and x.is_contiguous() and w_router.is_contiguous() and E <= 8
             and G.skinny_supports(3, E, T, H, w_router.stride(0))):
-        return G.skinny_linear(w_router, x, variant=3).t().contiguous()
+        y = G.skinny_linear(w_router, x, variant=3).t()
+        return y.contiguous() if contiguous or not ROUTER_VIEW else y
     return F.linear(x, w_router)
 
 
@@ -99,7 +107,8 @@ def fused_moe(x: torch.Tensor, router_logits: torch.Tensor, w_gu: torch.Tensor,
               gu_form: int | None = None, dn_form: int | None = None) -> torch.Tensor:
     """y[t] = sum_j w[t,j] * down_e(act(gate_e x_t) * up_e x_t) over the top-k experts.
 
-    x [T, H] bf16; router_logits [T, E] bf16; w_gu [E_local, 2I, H] ([gate | up]
+    x [T, H] bf16; router_logits [T, E] bf16, row-major or the transposed view of an [E, T]
+    tensor (``router_logits(..., contiguous=False)``); w_gu [E_local, 2I, H] ([gate | up]
     rows); w_dn [E_local, H, I].
     """
     if not on_gpu(x):
@@ -116,8 +125,9 @@ def fused_moe(x: torch.Tensor, router_logits: torch.Tensor, w_gu: torch.Tensor,
     e_local, two_i, h2 = w_gu.shape
     inter = two_i // 2
     assert x.dtype == torch.bfloat16 and x.is_contiguous()
-    assert router_logits.dtype == torch.bfloat16 and router_logits.is_contiguous()
-    assert router_logits.shape == (T, E) and h2 == H
+    assert router_logits.dtype == torch.bfloat16 and router_logits.shape == (T, E) and h2 == H
+    lts, les = router_logits.stride()
+    assert (lts, les) == (E, 1) or (lts == 1 and les >= T), router_logits.stride()
     assert w_gu.is_contiguous() and w_dn.is_contiguous() and w_dn.shape == (e_local, H, inter)
     assert E <= 256 and 1 <= top_k <= min(8, E) and H % 128 == 0 and inter % 64 == 0
     if out is None:
@@ -148,6 +158,6 @@ def fused_moe(x: torch.Tensor, router_logits: torch.Tensor, w_gu: torch.Tensor,
                       slab.data_ptr() if slab is not None else 0,
                       slab.numel() * 4 if slab is not None else 0,
                       cnt.data_ptr() if cnt is not None else 0,
-                      cnt.numel() if cnt is not None else 0, st), "moe")
+                      cnt.numel() if cnt is not None else 0, lts, les, st), "moe")
     return out
 

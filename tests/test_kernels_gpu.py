@@ -619,6 +619,32 @@ def test_fused_moe_chunked_and_graph(hipk):
     _close(out, ops.fused_moe_ref(x[64:128], lg[64:128], wgu, wdn, k), 3e-2, 3e-2, "graph")
 
 
+@pytest.mark.parametrize("variant", [3, 0])
+def test_fused_moe_reads_transposed_router_logits(hipk, variant):
+    """fused_moe on the router GEMM's [E, T] output read in place (the transposed [T, E] view of
+    ops.router_logits(contiguous=False), no transpose copy per layer) equals the row-major
+    logits bitwise, over several MOE_CHUNK chunks too; the router -> MoE chain matches fp32."""
+    from drtc_amd.ops import gemm as G
+    from drtc_amd.ops import moe as moe_ops
+
+    G.gemm_workspace(torch.device(DEV))
+    T, H, I, E, k = moe_ops.MOE_CHUNK + 320, 1024, 512, 8, 2
+    x, lg, wgu, wdn = _moe_inputs(T, H, I, E, seed=21)
+    lt = lg.t().contiguous().t()  # [T, E] view of an [E, T] tensor: strides (1, T)
+    assert lt.stride() == (1, T)
+    forms = dict(gu_form=241, dn_form=241) if variant == 3 else {}
+    a = ops.fused_moe(x, lg, wgu, wdn, k, variant=variant, **forms)
+    b = ops.fused_moe(x, lt, wgu, wdn, k, variant=variant, **forms)
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)
+    wr = (torch.randn(E, H, device=DEV) * 0.05).to(torch.bfloat16)
+    view = moe_ops.router_logits(x, wr, contiguous=False)
+    assert view.stride() == (1, T) and torch.equal(view, moe_ops.router_logits(x, wr))
+    y = ops.fused_moe(x, view, wgu, wdn, k, variant=variant, **forms)
+    _close(y, ops.fused_moe_ref(x, view, wgu, wdn, k), 3e-2, 3e-2, "router view -> moe")
+    G.check_splitk_fault()
+
+
 @pytest.mark.parametrize("M,N,K", [(64, 512, 256), (256, 1280, 1024), (1, 4096, 512)])
 def test_tuned_linear(hipk, M, N, K):
     """Tuned hipBLASLt GEMM (csrc/kernels/gemm_lt.cpp): the measured-best
