@@ -854,7 +854,7 @@ int launch_paged_decode_rope(void* out, float* part_o, float* part_ml, const voi
                              const int* block_tables, int bt_stride, const int* context_lens,
                              int B, int Hq, int Hkv, int D, float scale, int max_parts,
                              int blocks_per_part, const int* positions, const int64_t* slots,
-                             const float* cos_sin, hipStream_t st) {
+                             const float* cos_sin, int max_wgs, hipStream_t st) {
   if (B == 0) return 0;
   if (Hkv <= 0 || Hq % Hkv != 0 || Hq / Hkv > 16 || D > 128) return -1;
   if (!positions || !slots || !cos_sin || q_stride < (Hq + 2 * Hkv) * D) return -1;
@@ -869,7 +869,11 @@ int launch_paged_decode_rope(void* out, float* part_o, float* part_ml, const voi
   }
   const float sl2 = scale * kLog2e;
   const int items = B * Hkv * max_parts;
-  const dim3 pgrid(std::max(1, std::min((items + 3) / 4, 2 * n_cu))), pblock(256);
+  // max_wgs > 0 caps the persistent grid (the kernel strides over its items by the grid's
+  // wave count, so any grid size covers every item): attention on part of the chip
+  int wgs = std::min((items + 3) / 4, 2 * n_cu);
+  if (max_wgs > 0) wgs = std::min(wgs, max_wgs);
+  const dim3 pgrid(std::max(1, wgs)), pblock(256);
   const DecodeRope r{positions, slots, cos_sin, (bf16_t*)k_cache, (bf16_t*)v_cache};
   switch (D) {
     case 64:

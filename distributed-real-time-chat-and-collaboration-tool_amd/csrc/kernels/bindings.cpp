@@ -64,12 +64,13 @@ PYBIND11_MODULE(_hipk, m) {
         [](u64 out, u64 part_o, u64 part_ml, u64 qkv, int q_stride, u64 k_cache, u64 v_cache,
            u64 block_tables, int bt_stride, u64 context_lens, int B, int Hq, int Hkv, int D,
            float scale, int max_parts, int blocks_per_part, u64 positions, u64 slots,
-           u64 cos_sin, u64 st) {
+           u64 cos_sin, int max_wgs, u64 st) {
           return drtc::launch_paged_decode_rope(
               P<void>(out), P<float>(part_o), P<float>(part_ml), P<const void>(qkv), q_stride,
               P<void>(k_cache), P<void>(v_cache), P<const int>(block_tables), bt_stride,
               P<const int>(context_lens), B, Hq, Hkv, D, scale, max_parts, blocks_per_part,
-              P<const int>(positions), P<const int64_t>(slots), P<const float>(cos_sin), S(st));
+              P<const int>(positions), P<const int64_t>(slots), P<const float>(cos_sin), max_wgs,
+              S(st));
         });
   m.def("prefill_attn",
         [](u64 out, int out_stride, u64 qkv, int qkv_stride, int Hq, int Hkv,

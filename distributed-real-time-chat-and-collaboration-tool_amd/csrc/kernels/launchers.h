@@ -33,7 +33,7 @@ int launch_paged_decode_rope(void* out, float* part_o, float* part_ml, const voi
                              const int* block_tables, int bt_stride, const int* context_lens,
                              int B, int Hq, int Hkv, int D, float scale, int max_parts,
                              int blocks_per_part, const int* positions, const int64_t* slots,
-                             const float* cos_sin, hipStream_t st);
+                             const float* cos_sin, int max_wgs, hipStream_t st);
 int launch_paged_decode(void* out, float* part_o, float* part_ml, int* counters, const void* q,
                         int q_stride, const void* k_cache, const void* v_cache,
                         const int* block_tables, int bt_stride,

@@ -469,13 +469,14 @@ int launch_moe(void* out, const void* x, const void* router_logits, const void* 
     // (128 outputs) for gate_up where I allows; down with split-K 2 while the grid is below
     // ~2 rounds of CUs; non-temporal weights where an expert's rows fit one tile (each
     // weight byte is read by one workgroup)
-    if (gu_form == 0) {
+    const bool gu_auto = gu_form == 0;  // an explicitly requested form runs as given
+    if (gu_auto) {
       for (int f : rows_e >= 96 ? std::initializer_list<int>{281, 241} :
                                   std::initializer_list<int>{141})
         if (moe_xd_ok(f, I, H, true)) { gu_form = f; break; }
     }
     const int mt0 = (gu_form % 1000) / 100, bm0 = 128 * mt0;
-    if (gu_form && gu_form < 1000 && rows_e <= bm0) gu_form += 1000;
+    if (gu_auto && gu_form && gu_form < 1000 && rows_e <= bm0) gu_form += 1000;
     if (dn_form == 0 && gu_form) {
       const int64_t max_t = (P + bm0 - 1) / bm0 + e_local;
       for (int f : mt0 == 2 ? std::initializer_list<int>{282, 281, 242, 241} :

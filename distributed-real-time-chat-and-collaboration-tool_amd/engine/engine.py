@@ -22,12 +22,14 @@ token bookkeeping).
 """
 from __future__ import annotations
 
+import atexit
 import collections
 import itertools
 import math
 import os
 import threading
 import time
+import weakref
 
 import numpy as np
 import torch
@@ -86,7 +88,8 @@ class LLMEngine:
         if num_blocks is None:
             num_blocks = PagedKVCache.auto_num_blocks(
                 cfg, model.sh.hkv, self.device, kv_fraction, hbm_budget=hbm_budget,
-                weight_bytes=model.weight_bytes() if hbm_budget is not None else None)
+                weight_bytes=model.weight_bytes() if hbm_budget is not None else None,
+                min_blocks=self.max_blocks)
         # lockstep (SPMD) TP/EP ranks must schedule identically: every rank
         # sizes its cache from the same (smallest) block count
         num_blocks = model.pc.agree_min(num_blocks)
@@ -148,10 +151,18 @@ class LLMEngine:
         self.admit_gap_s = float(os.environ.get("DRTC_ADMIT_GAP_MS", "3")) / 1000.0
         self.admit_max_delay_s = float(os.environ.get("DRTC_ADMIT_MAX_MS", "100")) / 1000.0
         self._last_arrival = 0.0
-        self._steps = 0  # scheduler steps (health checks every HEALTH_EVERY)
+        self._steps = 0  # scheduler steps (split-K fault polls every HEALTH_EVERY)
+        self._fault_watch = None
+        if self.device.type == "cuda":
+            from ..ops import gemm as _gemm
+
+            self._fault_watch = _gemm.SplitKWatch(self.device)
+        self.closed = False
 
     # ------------------------------------------------------------ API
     def add_request(self, req: Request) -> Request:
+        if self.closed:
+            raise RuntimeError("engine is shut down")
         n = len(req.prompt_ids)
         if n == 0:
             raise ValueError("empty prompt")
@@ -228,8 +239,9 @@ class LLMEngine:
             self.runner.capture_all(up_to)
         self.check_health()
 
-    # steps between two split-K fault checks while serving (each is one device sync)
-    HEALTH_EVERY = int(os.environ.get("DRTC_HEALTH_EVERY", "512"))
+    # steps between two split-K fault polls while serving (ops.gemm.SplitKWatch: an async copy
+    # of the fault words per poll, no device sync; 0 disables)
+    HEALTH_EVERY = int(os.environ.get("DRTC_HEALTH_EVERY", "1"))
 
     def check_health(self) -> None:
         """Raise ops.gemm.SplitKFault if a split-K GEMM combine on this engine's device timed
@@ -238,6 +250,38 @@ class LLMEngine:
             from ..ops import gemm as _gemm
 
             _gemm.check_splitk_fault(self.device)
+
+    def shutdown(self, reason: str = "error: shutdown") -> list[Request]:
+        """Stop serving, in order: read the in-flight (pipelined) decode step, finish every
+        queued and running request with ``reason`` (their waiters return at once), release
+        their batch slots and KV blocks, and wait until the device has finished every kernel
+        this engine issued.  Call it from the thread that drives the engine, or after that
+        thread has stopped (EngineLoop.stop).  Returns the requests it finished."""
+        if self.closed:
+            return []
+        self.closed = True
+        if self._inflight is not None:
+            try:
+                self._process_inflight()
+            except Exception:  # a failing device: still fail the requests below
+                self._inflight = None
+        with self.lock:
+            # (finished "zombies" still hold their slots: they are in ``running`` too)
+            pending = list(self.waiting) + list(self.running)
+            self.waiting.clear()
+            self._waiting_tokens = 0
+            self._aborts = []
+            for r in sorted(self.running, key=lambda r: -r.slot):
+                self._release_slot(r)
+            self._zombies = []
+        done = []
+        for r in pending:
+            if r.state != RequestState.FINISHED:
+                r.mark_finished(reason)
+                done.append(r)
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+        return done
 
     def generate(self, prompts: list[list[int]], params: SamplingParams | list) -> list[Request]:
         if isinstance(params, SamplingParams):
@@ -304,8 +348,9 @@ class LLMEngine:
         request, KV-cache occupancy and queue depths per step."""
         M = METRICS
         self._steps += 1
-        if self.HEALTH_EVERY > 0 and self._steps % self.HEALTH_EVERY == 0:
-            self.check_health()
+        if (self._fault_watch is not None and self.HEALTH_EVERY > 0
+                and self._steps % self.HEALTH_EVERY == 0):
+            self._fault_watch.poll()
         if done:
             M.observe_many("engine.ttft_s", [r.ttft for r in done])
             M.observe_many("engine.e2e_s", [r.finish_time - r.arrival_time for r in done])
@@ -827,6 +872,7 @@ class EngineLoop:
 
     def start(self) -> "EngineLoop":
         self.thread.start()
+        _LIVE_LOOPS.add(self)
         return self
 
     def submit(self, req: Request) -> Request:
@@ -881,7 +927,33 @@ class EngineLoop:
             for r in pending:
                 r.mark_finished("error")
 
-    def stop(self) -> None:
+    def stop(self, timeout: float = 10.0) -> bool:
+        """Ordered stop: end the loop at its next step boundary, join the thread, then shut
+        the engine down (drain the in-flight step, fail what is still queued or running with
+        "error: shutdown" so blocked callers return, wait for the device).  Returns whether the
+        thread ended within ``timeout``; idempotent."""
         self._stop.set()
         self._wake.set()
-        self.thread.join(timeout=10)
+        if self.thread.is_alive() and self.thread is not threading.current_thread():
+            self.thread.join(timeout=timeout)
+        ended = not self.thread.is_alive()
+        if ended:
+            try:
+                self.engine.shutdown()
+            except Exception:  # a dead device: nothing left to drain
+                pass
+        _LIVE_LOOPS.discard(self)
+        return ended
+
+
+# every started EngineLoop of the process: stopped in order at interpreter exit, while the
+# runtime is intact - a daemon engine thread still inside HIP / torch native code when CPython
+# finalizes is ended by a forced unwind through C++ frames and the process aborts
+# ("terminate called without an active exception"); atexit runs before that
+_LIVE_LOOPS: "weakref.WeakSet[EngineLoop]" = weakref.WeakSet()
+
+
+@atexit.register
+def _stop_live_loops() -> None:
+    for loop in list(_LIVE_LOOPS):
+        loop.stop(timeout=30.0)

@@ -65,7 +65,8 @@ class PagedKVCache:
     @staticmethod
     def auto_num_blocks(cfg: ModelConfig, hkv_local: int, device, kv_fraction: float = 0.85,
                         reserve_bytes: int = 8 << 30, max_blocks: int | None = None,
-                        hbm_budget: float | None = None, weight_bytes: int | None = None) -> int:
+                        hbm_budget: float | None = None, weight_bytes: int | None = None,
+                        min_blocks: int = 0) -> int:
         """KV blocks for an engine on ``device``: ``kv_fraction`` of the HBM free beyond
         ``reserve_bytes`` (activations, GEMM workspaces, graphs) - or, with ``hbm_budget``
         (engine groups sharing a GPU, llm.server --serve ...:mem=F), what is left of
@@ -81,8 +82,15 @@ class PagedKVCache:
             budget = int(max(0, free - reserve_bytes) * kv_fraction)
             if hbm_budget is not None:
                 mine = torch.cuda.memory_reserved(dev) if weight_bytes is None else weight_bytes
-                budget = min(budget, int(hbm_budget * total) - mine - reserve_bytes)
-                budget = max(budget, 0)
+                left = int(hbm_budget * total) - mine - reserve_bytes
+                if blocks_for_budget(cfg, hkv_local, cfg.num_layers, max(left, 0)) < min_blocks:
+                    # ``min_blocks``: the cache of one max_model_len sequence
+                    raise ValueError(
+                        f"{cfg.name}: an HBM budget of {hbm_budget:.2f} x {total / 1e9:.0f} GB "
+                        f"on {dev} leaves {left / 1e9:.1f} GB for the KV cache after "
+                        f"{mine / 1e9:.1f} GB of weights and the {reserve_bytes / 1e9:.0f} GB "
+                        f"reserve: less than one {min_blocks}-block sequence needs")
+                budget = min(budget, max(left, 0))
         else:
             budget = 256 << 20
         n = blocks_for_budget(cfg, hkv_local, cfg.num_layers, budget)

@@ -246,8 +246,10 @@ class WorkerPool:
             if kind == "ready":
                 self.healthy[rank] = True
                 self.last_hb[rank] = time.monotonic()
-        threading.Thread(target=self._collect, daemon=True).start()
-        threading.Thread(target=self._monitor, daemon=True).start()
+        self._threads = [threading.Thread(target=self._collect, daemon=True, name="pool-collect"),
+                         threading.Thread(target=self._monitor, daemon=True, name="pool-monitor")]
+        for t in self._threads:
+            t.start()
 
     def _spawn(self, w: int) -> None:
         self.inqs[w] = self._ctx.Queue()
@@ -386,15 +388,35 @@ class WorkerPool:
                     for w in range(len(self.procs))]
 
     def close(self):
+        """Ordered stop: no more evictions / respawns, each replica drains its engine and
+        exits (killed after 10 s), every request still waiting here fails with "error:
+        shutdown", and the collector / monitor threads are joined.  Idempotent."""
+        if self._closed and not any(p is not None and p.is_alive() for p in self.procs):
+            return
         self._closed = True
         for w, q in enumerate(self.inqs):
             if q is not None and self.procs[w] is not None and self.procs[w].is_alive():
-                q.put(None)
+                try:
+                    q.put(None)
+                except (OSError, ValueError):
+                    pass
         for p in self.procs:
             if p is not None:
                 p.join(timeout=10)
                 if p.is_alive():
                     p.kill()
+                    p.join(timeout=5)
+        failed = []
+        with self._lock:
+            for ev, slot, _ in self.futures.values():
+                if not slot:
+                    slot.append(([], "error: shutdown"))
+                    failed.append(ev)
+        for ev in failed:
+            ev.set()
+        for t in getattr(self, "_threads", ()):
+            if t is not threading.current_thread():
+                t.join(timeout=5)
 
 
 class ReplicaRouter:

@@ -195,10 +195,12 @@ def build_feature_backends(args, specs: list[str]):
         groups.setdefault((model, tuple(devices) if devices else None, tp, mem), []).append(feat)
     need_default = len(seen) < len(FEATURES)
     gpu_free = args.backend == "scripted"  # scripted stand-ins hold no GPU memory
-    placement = [(f"{'+'.join(fs)}={m}", _group_devices(list(d) if d else None, tp,
-                                                         1 if tp > 1 else
-                                                         (len(d) if d else args.gpus)), mem)
-                 for (m, d, tp, mem), fs in groups.items() if not (gpu_free or m == "scripted")]
+    # one rule for the GPUs of a --serve group, used by both the placement check and the build:
+    # the named GPUs, else GPU 0 (tp1: one replica) or GPUs 0 .. tp-1 (a TP group)
+    group_devs = {key: _group_devices(list(key[1]) if key[1] else None, key[2], 1)
+                  for key in groups}
+    placement = [(f"{'+'.join(fs)}={key[0]}", group_devs[key], key[3])
+                 for key, fs in groups.items() if not (gpu_free or key[0] == "scripted")]
     if need_default and not (gpu_free or args.model == "scripted"):
         placement.append((f"default={args.model}", _group_devices(None, args.tp, args.gpus),
                           getattr(args, "hbm_budget", None)))
@@ -210,9 +212,10 @@ def build_feature_backends(args, specs: list[str]):
         if key not in made:
             sub = argparse.Namespace(**vars(args))
             sub.model, sub.tp, sub.hbm_budget = model, tp, mem
-            sub.gpus = len(devices) if devices and tp == 1 else (1 if tp == 1 else args.gpus)
+            devs = group_devs[key]
+            sub.gpus = len(devs) if tp == 1 else args.gpus
             sub.max_batch = args.max_batch or default_max_batch(model, tp)
-            made[key] = build_backend(sub, devices=devices)
+            made[key] = build_backend(sub, devices=devs if (devices or tp == 1) else None)
         by_feature[feat] = made[key]
     default = None
     if need_default:
@@ -290,7 +293,19 @@ def serve_aio(backend, port: int = 50055, bind: str = "[::]", params=None) -> Ai
     return AioServer(backend, port, bind, params)
 
 
+def _stop_once(stop: threading.Event) -> None:
+    """SIGTERM: start the ordered shutdown; further SIGTERMs are ignored (CPython restores
+    the default - terminate - action for Python-level handlers during finalization, so a
+    repeated SIGTERM from a supervisor would otherwise kill the exiting process)."""
+    stop.set()
+    signal.signal(signal.SIGTERM, signal.SIG_IGN)
+
+
 def main(argv=None):
+    # installed first: a SIGTERM while the engines load still ends the service in order
+    stop = threading.Event()
+    signal.signal(signal.SIGINT, lambda *a: stop.set())
+    signal.signal(signal.SIGTERM, lambda *a: _stop_once(stop))
     ap = argparse.ArgumentParser(description="drtc_amd LLM service (on-GPU inference)")
     ap.add_argument("--port", type=int, default=50055)
     ap.add_argument("--backend", choices=("engine", "scripted"), default="engine")
@@ -340,11 +355,22 @@ def main(argv=None):
               else serve(backend, args.port, workers))
     log.info("LLM server on port %d (backend=%s model=%s gpus=%d tp=%d)", args.port, args.backend,
              args.model, args.gpus, args.tp)
-    stop = threading.Event()
-    signal.signal(signal.SIGINT, lambda *a: stop.set())
-    signal.signal(signal.SIGTERM, lambda *a: stop.set())
     stop.wait()
-    server.stop(1.0)
+    shutdown(server, backend)
+
+
+def shutdown(server, backend, grace: float = 1.0) -> None:
+    """Ordered stop of the service (SIGTERM / SIGINT): stop accepting RPCs (in-flight ones get
+    ``grace`` seconds), stop the engine groups - loop threads joined, in-flight steps drained,
+    unfinished requests failed so their handlers return the canned fallback, worker processes
+    joined, devices synchronized - then wait for the RPC server to finish."""
+    log.info("LLM server shutting down")
+    done = server.stop(grace)
+    close = getattr(backend, "close", None)
+    if close is not None:
+        close()
+    if done is not None:
+        done.wait(grace + 10)
 
 
 if __name__ == "__main__":

@@ -52,6 +52,17 @@ from .config import ModelConfig
 _EP_DECODE_A2A = os.environ.get("DRTC_EP_DECODE", "a2a") == "a2a"
 _EP_PREFILL = os.environ.get("DRTC_EP_PREFILL", "cap")
 
+# Two-stream micro-batched decode: the step's rows in two halves, one per
+# stream inside the captured graph, with each half's paged attention (HBM-bound) ordered to
+# run beside the other half's projections (per-CU operand-ingest bound).  DRTC_DECODE_MICRO=2
+# enables it for decode batches of at least DECODE_MICRO_MIN_B rows (dense TP=1 models);
+# DRTC_DECODE_MICRO_WGS caps the attention's persistent grid (0: two workgroups per CU);
+# DRTC_DECODE_MICRO_PINGPONG=0 drops the cross-stream attention ordering (two free chains).
+DECODE_MICRO = int(os.environ.get("DRTC_DECODE_MICRO", "0"))
+DECODE_MICRO_MIN_B = int(os.environ.get("DRTC_DECODE_MICRO_MIN_B", "512"))
+DECODE_MICRO_WGS = int(os.environ.get("DRTC_DECODE_MICRO_WGS", "0"))
+DECODE_MICRO_PINGPONG = os.environ.get("DRTC_DECODE_MICRO_PINGPONG", "1") != "0"
+
 
 @dataclass
 class PrefillMeta:
@@ -133,6 +144,9 @@ class TransformerLM:
                                                   cfg.experts_per_token, self.device)
         self.ep_overflow = None
         self._ep_cap_used = False
+        self._side_stream = None   # micro-batched decode: second stream + its split-K workspace
+        self._side_ws = None
+        self._micro_metas: dict = {}
         if cfg.is_moe and self.pc.ep_size > 1:
             from ..parallel.expert_parallel import EpOverflow
             self.ep_overflow = EpOverflow(self.device)
@@ -538,9 +552,97 @@ class TransformerLM:
                 return o, False, True  # reduced by the next norm (fused all-reduce + add + norm)
             return o, False
 
+        if self.decode_micro_ok(B):
+            return self._forward_decode_micro(ids, meta, kv_caches, attn_out)
         self._ep_begin()
         x = self._layers(self._embed(ids), attn, decode=True)
         return self._ep_end(self._logits(x))
+
+    # ------------------------------------------------------------ micro-batched decode
+    def decode_micro_ok(self, B: int) -> bool:
+        """Whether a decode step of B rows runs as two micro-batches on two streams."""
+        return (DECODE_MICRO >= 2 and B >= DECODE_MICRO_MIN_B and B % 2 == 0
+                and self.device.type == "cuda" and self.pc.tp_size == 1
+                and self.pc.ep_size == 1 and not self.cfg.is_moe and self.cfg.head_dim <= 128)
+
+    def _micro_meta(self, meta: DecodeMeta, lo: int, hi: int) -> DecodeMeta:
+        """Rows [lo, hi) of a decode step's metadata (views of its persistent buffers) with
+        the attention partitioning and workspace of a batch of hi - lo rows; cached per
+        (buffer, range) so a graph capture reuses what the eager warm-up built."""
+        key = (meta.positions.data_ptr(), meta.block_tables.data_ptr(), lo, hi)
+        m = self._micro_metas.get(key)
+        if m is None:
+            n, sh = hi - lo, self.sh
+            bt = meta.block_tables[lo:hi]
+            bpp, parts = ops.decode_partitioning(n, sh.hkv, bt.shape[1], D=self.cfg.head_dim)
+            ws = ops.DecodeWorkspace(n, sh.hq, self.cfg.head_dim, parts, self.device)
+            m = DecodeMeta(positions=meta.positions[lo:hi], slots=meta.slots[lo:hi],
+                           block_tables=bt, context_lens=meta.context_lens[lo:hi],
+                           blocks_per_part=bpp, workspace=ws)
+            self._micro_metas[key] = m
+        return m
+
+    def _forward_decode_micro(self, ids: torch.Tensor, meta: DecodeMeta, kv_caches,
+                              attn_out: torch.Tensor | None) -> torch.Tensor:
+        """forward_decode on two half-batches, one per stream: the caller's (current) stream
+        runs rows [0, B/2), a side stream - forked from it and joined back, so the whole step
+        stays one capturable graph - rows [B/2, B) with a private split-K workspace.  With
+        ping-pong ordering half A's layer-i attention waits for half B's layer-(i-1)
+        attention and B's waits for A's, so the two attentions never run together and each
+        overlaps the other half's projections.  Same per-row math as forward_decode (each
+        row's GEMMs, norms and attention see only that row), logits on all B rows at once."""
+        cfg, sh = self.cfg, self.sh
+        D = cfg.head_dim
+        B = ids.shape[0]
+        h = B // 2
+        if self._side_stream is None:  # created by the eager warm-up, before any capture
+            self._side_stream = torch.cuda.Stream(self.device)
+            self._side_ws = ops.gemm.new_gemm_workspace(self.device)
+        main = torch.cuda.current_stream(self.device)
+        streams = (main, self._side_stream)
+        wss = (None, self._side_ws)
+        rows = ((0, h), (h, B))
+        metas = [self._micro_meta(meta, lo, hi) for lo, hi in rows]
+        outs = [attn_out[lo:hi] if attn_out is not None else None for lo, hi in rows]
+        hidden = self._embed(ids)
+        streams[1].wait_stream(main)
+        xs = [ops.PendingNorm(hidden[lo:hi], None, self.layers[0]["ln_in"], cfg.rms_eps,
+                              cfg.gemma_norm) for lo, hi in rows]
+        ev_attn: list = [None, None]
+        n = len(self.layers)
+        for i, L in enumerate(self.layers):
+            kc, vc = kv_caches[i]
+            nxt = self.layers[i + 1]["ln_in"] if i + 1 < n else self.final_norm
+            for j in (0, 1):
+                with torch.cuda.stream(streams[j]), ops.gemm.private_workspace(wss[j]):
+                    x, m = xs[j], metas[j]
+                    qkv = ops.norm_linear(x, L["qkv"])
+                    if DECODE_MICRO_PINGPONG and ev_attn[1 - j] is not None:
+                        streams[j].wait_event(ev_attn[1 - j])
+                    a = ops.paged_decode_attention_rope(
+                        qkv, m.positions, m.slots, self.cos_sin, sh.hq, sh.hkv, D, kc, vc,
+                        m.block_tables, m.context_lens, cfg.attn_scale, out=outs[j],
+                        blocks_per_part=m.blocks_per_part, workspace=m.workspace,
+                        max_wgs=DECODE_MICRO_WGS)
+                    if DECODE_MICRO_PINGPONG:
+                        ev = torch.cuda.Event()
+                        ev.record(streams[j])
+                        ev_attn[j] = ev
+                    o = ops.linear(a.view(a.shape[0], sh.hq * D), L["o"])
+                    x = ops.PendingNorm(o, x.stream(), L["ln_post"], cfg.rms_eps, cfg.gemma_norm)
+                    mo, added, *_ = self._mlp(L, x, decode=True)
+                    xs[j] = ops.PendingNorm(mo, None if added else x.stream(), nxt, cfg.rms_eps,
+                                            cfg.gemma_norm)
+        finals = []
+        for j in (0, 1):
+            with torch.cuda.stream(streams[j]), ops.gemm.private_workspace(wss[j]):
+                finals.append(xs[j].materialize())
+        main.wait_stream(streams[1])
+        # every tensor the side stream read or wrote is still referenced here, and the main
+        # stream has joined it: later main-stream reuse of that memory is ordered after it
+        x = torch.cat(finals)
+        del finals, xs, hidden
+        return self._logits(x)
 
     # ------------------------------------------------------------ reference
     def forward_reference(self, ids_list: list[list[int]]) -> list[torch.Tensor]:

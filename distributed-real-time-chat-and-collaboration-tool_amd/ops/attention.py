@@ -257,12 +257,15 @@ def paged_decode_attention_rope(qkv: torch.Tensor, positions: torch.Tensor, slot
                                 block_tables: torch.Tensor, context_lens: torch.Tensor,
                                 scale: float, out: torch.Tensor | None = None,
                                 blocks_per_part: int | None = None,
-                                workspace: DecodeWorkspace | None = None) -> torch.Tensor:
+                                workspace: DecodeWorkspace | None = None,
+                                max_wgs: int = 0) -> torch.Tensor:
     """Decode-step attention from the raw QKV rows [B, (Hq + 2 Hkv) D]: rotate q / k of
     the step's token (position ``positions[b]`` = context_lens[b] - 1), write its k / v
     into the paged cache at ``slots[b]`` and attend over the whole context - the result
     of ``rope_kv_`` followed by ``paged_decode_attention``.  On the GPU the persistent
-    kernel (variant 3, D <= 128) does it in one launch; other shapes run the two ops."""
+    kernel (variant 3, D <= 128) does it in one launch; other shapes run the two ops.
+    ``max_wgs`` > 0 caps the persistent grid at that many 4-wave workgroups (attention on
+    part of the chip, beside another stream's GEMMs; 0: two per CU)."""
     from .rope import rope_kv_
 
     B = qkv.shape[0]
@@ -296,5 +299,5 @@ def paged_decode_attention_rope(qkv: torch.Tensor, positions: torch.Tensor, slot
                                    block_tables.stride(0), context_lens.data_ptr(), B, Hq, Hkv, D,
                                    float(scale), workspace.max_parts, blocks_per_part,
                                    positions.data_ptr(), slots.data_ptr(), cos_sin.data_ptr(),
-                                   stream_ptr(qkv)), "paged_decode_rope")
+                                   int(max_wgs), stream_ptr(qkv)), "paged_decode_rope")
     return out

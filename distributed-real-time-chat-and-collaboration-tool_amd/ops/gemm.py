@@ -426,13 +426,40 @@ WS_COUNTERS = 1 << 16
 _all_ws: list[tuple[torch.Tensor, torch.Tensor]] = []
 
 
+# per-thread override of the device workspace: GEMMs issued inside ``private_workspace(ws)``
+# (the second micro-batch stream of a decode step) use ``ws``
+_ws_local = threading.local()
+
+
+class private_workspace:
+    """Context manager: every split-K / medium-M GEMM issued by this thread inside it takes
+    ``ws`` (from ``new_gemm_workspace``) instead of the device's shared workspace - for GEMMs
+    that run concurrently with the shared workspace's users on another stream."""
+
+    def __init__(self, ws: tuple[torch.Tensor, torch.Tensor] | None):
+        self.ws = ws
+
+    def __enter__(self):
+        self.prev = getattr(_ws_local, "ws", None)
+        _ws_local.ws = self.ws
+        return self.ws
+
+    def __exit__(self, *exc):
+        _ws_local.ws = self.prev
+        return False
+
+
 def gemm_workspace(dev: torch.device) -> tuple[torch.Tensor, torch.Tensor]:
     """Split-K workspace of a device: fp32 slabs + per-tile arrival counters (zeroed once;
     the last arriver of each tile re-arms its counter; the LAST counter is the fault word,
     ``check_splitk_fault``).  One per device, shared by every GEMM on the engine's stream (and
     the medium-M kernel's partial slabs); a GEMM issued concurrently on another stream passes
-    its own (``ws=``).  Created before any graph capture (the engine's eager warm-up does)."""
+    its own (``ws=``, or ``private_workspace``).  Created before any graph capture (the
+    engine's eager warm-up does)."""
     key = dev.index if dev.index is not None else torch.cuda.current_device()
+    own = getattr(_ws_local, "ws", None)
+    if own is not None and own[0].device.index == key:
+        return own
     ws = _ws.get(key)
     if ws is None:
         with _ws_lock:
@@ -478,6 +505,57 @@ def check_splitk_fault(dev: torch.device | None = None) -> None:
             cnt.zero_()
             raise SplitKFault(f"split-K combine timed out on {cnt.device}: a GEMM result since "
                               "the last check is wrong (counters reset)")
+
+
+class SplitKWatch:
+    """Per-step split-K fault detection without a device sync, for one device.
+
+    ``poll()`` (the engine calls it after every step) enqueues, on the current stream, a copy of
+    every split-K workspace's fault word into pinned host memory and records an event; a later
+    poll reads those words once the event has completed.  A combine that timed out is therefore
+    reported one step after the step that ran it (two when the GPU runs a step behind the host),
+    instead of up to ``HEALTH_EVERY`` steps later with a blocking read.  On a fault the device's
+    counters are zeroed (the next GEMMs start clean) and SplitKFault is raised - or, with
+    ``raise_=False``, True is returned."""
+
+    def __init__(self, dev: torch.device):
+        dev = torch.device(dev)
+        if dev.type == "cuda" and dev.index is None:
+            dev = torch.device("cuda", torch.cuda.current_device())
+        self.dev = dev
+        self._host: torch.Tensor | None = None
+        self._ev = None
+        self._n = 0
+
+    def _counters(self) -> list[torch.Tensor]:
+        with _ws_lock:
+            return [cnt for _, cnt in _all_ws if cnt.device == self.dev]
+
+    def poll(self, raise_: bool = True) -> bool:
+        if self.dev.type != "cuda":
+            return False
+        if self._ev is not None and self._ev.query():
+            fault = bool(self._host[:self._n].any())
+            self._ev = None
+            if fault:
+                for cnt in self._counters():
+                    cnt.zero_()
+                if raise_:
+                    raise SplitKFault(f"split-K combine timed out on {self.dev}: a GEMM result "
+                                      "of the last steps is wrong (counters reset)")
+                return True
+        if self._ev is None:
+            cnts = self._counters()
+            if not cnts:
+                return False
+            if self._host is None or self._host.numel() < len(cnts):
+                self._host = torch.zeros(max(4, len(cnts)), dtype=torch.int32, pin_memory=True)
+            for i, cnt in enumerate(cnts):
+                self._host[i:i + 1].copy_(cnt[-1:], non_blocking=True)
+            self._n = len(cnts)
+            self._ev = torch.cuda.Event()
+            self._ev.record()
+        return False
 
 
 def set_splitk_spin_limit(limit: int) -> int:
@@ -839,7 +917,7 @@ def midm_gemm(x: torch.Tensor, w: torch.Tensor, epi: str = "store",
 __all__ = ["linear", "route", "norm_linear", "glu_linear", "norm_glu", "fused_glu_ok",
            "linear_residual",
            "residual_fusable", "w4_glu_ok", "w4_ok", "w4_shape_ok", "w4_group_m", "mfma_gemm",
-           "gemm_workspace", "new_gemm_workspace", "check_splitk_fault", "SplitKFault",
+           "gemm_workspace", "new_gemm_workspace", "private_workspace", "check_splitk_fault", "SplitKFault", "SplitKWatch",
            "set_splitk_spin_limit", "skinny_linear", "skinny_ok",
            "skinny_variant", "skinny_supports", "midm_gemm", "midm_supported", "midm_splits",
            "xd_gemm", "xd_supported", "xd_default_form", "tune", "save_entries", "load_table", "reset", "set_enabled", "table_path"]

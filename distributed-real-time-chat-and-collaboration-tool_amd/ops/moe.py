@@ -87,15 +87,22 @@ def router_logits(x: torch.Tensor, w_router: torch.Tensor, contiguous: bool = Tr
     streamed weight rows, so x is read once and no library GEMM runs in the MoE layer (ref
     llm_server/llm_server.py:403: the suggestions model).  ``contiguous=False`` returns the
     kernel's [E, T] output as a transposed [T, E] view (strides (1, T)), which ``fused_moe``
-    reads in place (no transpose copy per layer).  Shapes the skinny kernel does not take (T not
-    a multiple of its row block, E > 8) go to F.linear."""
+    reads in place (no transpose copy per layer).  A T that is not a multiple of the kernel's
+    16-row block is zero-padded up to one, so every batch size routes through the same kernel
+    and the same rounding (top-k choices on near-tied logits do not depend on T); E > 8 goes
+    to F.linear."""
     from . import gemm as G
 
     T, H = x.shape
     E = w_router.shape[0]
-    if (on_gpu(x) and x.is_contiguous() and w_router.is_contiguous() and E <= 8
-            and G.skinny_supports(3, E, T, H, w_router.stride(0))):
-        y = G.skinny_linear(w_router, x, variant=3).t()
+    Tp = -(-T // 16) * 16
+    if (on_gpu(x) and x.is_contiguous() and w_router.is_contiguous() and E <= 8 and T > 0
+            and G.skinny_supports(3, E, Tp, H, w_router.stride(0))):
+        if Tp != T:
+            xp = x.new_zeros((Tp, H))
+            xp[:T].copy_(x)
+            x = xp
+        y = G.skinny_linear(w_router, x, variant=3).t()[:T]
         return y.contiguous() if contiguous or not ROUTER_VIEW else y
     return F.linear(x, w_router)
 

@@ -86,15 +86,14 @@ def tp_worker(rank: int, world: int, port: int, model_name: str, engine_kw: dict
         if rank == 0:
             outq.put(("ready", 0, None))
     except BaseException as e:
-        if rank == 0:
-            outq.put(("fatal", 0, repr(e)))
+        outq.put(("fatal", rank, repr(e)))
         raise
     try:
         _serve_loop(rank, eng, pc, cpu, inq, outq)
-    except BaseException as e:
-        if rank == 0:
-            outq.put(("fatal", 0, repr(e)))
+    except BaseException as e:  # any rank: the front-end fails and ends the whole group
+        outq.put(("fatal", rank, repr(e)))
         raise
+    eng.shutdown()
     dist.barrier(group=cpu)
     dist.destroy_process_group()
 
@@ -153,9 +152,11 @@ class TPEngineGroup:
         ctx = mp.get_context("spawn")
         self.inq, self.outq = ctx.Queue(), ctx.Queue()
         port = _free_port()
+        # every rank reports a fatal error on outq (a split-K fault or an all-reduce flag
+        # timeout seen by any rank fails the group at once); only rank 0 reports results
         self.procs = [ctx.Process(target=tp_worker, daemon=True,
                                   args=(r, world, port, model_name, engine_kw,
-                                        self.inq if r == 0 else None, self.outq if r == 0 else None,
+                                        self.inq if r == 0 else None, self.outq,
                                         custom_allreduce, devices))
                       for r in range(world)]
         for p in self.procs:
@@ -169,18 +170,33 @@ class TPEngineGroup:
         self.error = None
         self._lock = threading.Lock()
         self._ids = itertools.count()
-        threading.Thread(target=self._collect, daemon=True).start()
+        self._closed = False
+        self._collector = threading.Thread(target=self._collect, daemon=True, name="tp-collect")
+        self._collector.start()
+
+    def _fail_all(self, reason: str) -> None:
+        with self._lock:
+            futs, self._futs = list(self._futs.values()), {}
+        for ev, slot in futs:
+            slot.append(([], reason))
+            ev.set()
 
     def _collect(self):
-        while True:
-            kind, rid, payload = self.outq.get()
+        while not self._closed:
+            try:
+                kind, rid, payload = self.outq.get(timeout=0.5)
+            except queue.Empty:
+                continue
+            except (EOFError, OSError):
+                return
             if kind == "fatal":  # the group died: fail every outstanding request
                 with self._lock:
-                    futs, self._futs = list(self._futs.values()), {}
                     self.error = payload
-                for ev, slot in futs:
-                    slot.append(([], f"error: TP group failed: {payload}"))
-                    ev.set()
+                self._fail_all(f"error: TP group failed: {payload}")
+                # the other ranks may sit in a collective with the failed one: end them all
+                for p in self.procs:
+                    if p.is_alive():
+                        p.kill()
                 continue
             with self._lock:
                 f = self._futs.pop(rid, None)
@@ -222,6 +238,20 @@ class TPEngineGroup:
         return out
 
     def close(self):
-        self.inq.put(None)
+        """Ordered stop: rank 0 broadcasts the stop, every rank drains its engine and leaves
+        the process group (killed after 30 s); waiting requests fail; the collector ends."""
+        if self._closed:
+            return
+        try:
+            self.inq.put(None)
+        except (OSError, ValueError):
+            pass
         for p in self.procs:
             p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+                p.join(timeout=5)
+        self._closed = True
+        self._fail_all("error: shutdown")
+        if self._collector is not threading.current_thread():
+            self._collector.join(timeout=5)

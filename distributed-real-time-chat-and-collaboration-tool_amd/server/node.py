@@ -43,7 +43,13 @@ def parse_peers(s: str | None) -> dict:
     return out
 
 
-def serve(cfg: NodeConfig, block: bool = True, bind: str = "[::]"):
+def serve(cfg: NodeConfig, block: bool = True, bind: str = "[::]",
+          stop: threading.Event | None = None):
+    """Run one node.  ``block``: serve until SIGINT / SIGTERM (or ``stop`` is set), then stop
+    in order and return; the handlers are installed before the node starts (main() installs
+    them even earlier, before argument-dependent start-up work)."""
+    if block and stop is None:
+        stop = _install_stop_handlers()
     node = ChatNode(cfg)
     server = grpc.server(futures.ThreadPoolExecutor(max_workers=cfg.grpc_workers), options=SERVER_OPTS)
     add_servicer(server, RAFT_SERVICE, node)
@@ -56,9 +62,6 @@ def serve(cfg: NodeConfig, block: bool = True, bind: str = "[::]"):
     log.info("raft chat node %d on port %d (peers %s)", cfg.node_id, cfg.port, cfg.peers)
     if not block:
         return node, server
-    stop = threading.Event()
-    signal.signal(signal.SIGINT, lambda *a: stop.set())
-    signal.signal(signal.SIGTERM, lambda *a: stop.set())
     while not stop.wait(2.0):
         i = node.rt.leader_info()
         with node.rt.state_lock:
@@ -67,12 +70,30 @@ def serve(cfg: NodeConfig, block: bool = True, bind: str = "[::]"):
         lead = f"leader {i['leader_id']}" if i["leader_id"] is not None else "no leader"
         log.info("node %d %s | term %d | log %d (commit %d) | %d users | %d channels | %d files | %s",
                  cfg.node_id, role, i["term"], i["log"], i["commit"], nu, nc, nf, lead)
-    server.stop(1.0)
+    # ordered stop: no new RPCs (in-flight ones get 1 s), then the Raft runtime (timer and
+    # persist threads joined, state flushed, log exported and closed, channels closed)
+    server.stop(1.0).wait(10)
     node.stop()
     return node, server
 
 
+def _install_stop_handlers() -> threading.Event:
+    stop = threading.Event()
+    signal.signal(signal.SIGINT, lambda *a: stop.set())
+    signal.signal(signal.SIGTERM, lambda *a: _stop_once(stop))
+    return stop
+
+
+def _stop_once(stop: threading.Event) -> None:
+    """SIGTERM: start the ordered shutdown; further SIGTERMs are ignored (CPython restores
+    the default - terminate - action for Python-level handlers during finalization, so a
+    repeated SIGTERM from a supervisor would otherwise kill the exiting process)."""
+    stop.set()
+    signal.signal(signal.SIGTERM, signal.SIG_IGN)
+
+
 def main(argv=None) -> None:
+    stop = _install_stop_handlers()  # a SIGTERM during start-up still ends the node in order
     ap = argparse.ArgumentParser(description="drtc_amd Raft chat node")
     ap.add_argument("--node-id", type=int, required=True)
     ap.add_argument("--port", type=int, required=True)
@@ -111,7 +132,7 @@ def main(argv=None) -> None:
                      snapshot_every=a.snapshot_every)
     print(f"\n{'=' * 60}\n  Raft Chat Node {a.node_id}\n  Port: {a.port}\n"
           f"  Features: Consensus + Full Chat Application + on-GPU AI\n{'=' * 60}\n", flush=True)
-    serve(cfg)
+    serve(cfg, stop=stop)
 
 
 if __name__ == "__main__":

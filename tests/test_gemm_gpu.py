@@ -500,3 +500,58 @@ def test_splitk_timeout_is_raised_and_next_gemm_is_correct(hipk, kind):
     w2 = torch.randn(4096, 1024, device="cuda", dtype=torch.bfloat16, generator=g) * 0.05
     _check(G.xd_gemm(x2, w2, form=242), _ref(x2, w2, "store", None))
     G.check_splitk_fault()
+
+
+def test_splitk_watch_reports_a_fault_without_a_sync(hipk):
+    """ops.gemm.SplitKWatch (the engine's per-step fault poll): the fault word is copied to
+    pinned memory asynchronously after each step and read by a later poll once the copy has
+    landed - a forced combine timeout is reported within a few polls, counters reset, and a
+    clean run never reports."""
+    g = torch.Generator(device="cuda").manual_seed(98)
+    x = torch.randn(512, 1024, device="cuda", dtype=torch.bfloat16, generator=g)
+    w = torch.randn(1024, 1024, device="cuda", dtype=torch.bfloat16, generator=g) * 0.05
+    ref = _ref(x, w, "store", None)
+    G.check_splitk_fault()
+    watch = G.SplitKWatch(torch.device("cuda"))
+    for _ in range(4):  # clean steps: nothing to report
+        _check(G.xd_gemm(x, w, form=242), ref)
+        assert watch.poll(raise_=False) is False
+        torch.cuda.synchronize()
+    assert watch.poll(raise_=False) is False
+    prev = G.set_splitk_spin_limit(-1)
+    try:
+        G.xd_gemm(x, w, form=242)
+    finally:
+        G.set_splitk_spin_limit(prev)
+    seen = False
+    for _ in range(4):  # the copy issued by one poll is read by the next
+        torch.cuda.synchronize()
+        if watch.poll(raise_=False):
+            seen = True
+            break
+    assert seen
+    G.check_splitk_fault()  # the watch reset the counters
+    _check(G.xd_gemm(x, w, form=242), ref)
+    with pytest.raises(G.SplitKFault):  # raising form
+        prev = G.set_splitk_spin_limit(-1)
+        try:
+            G.xd_gemm(x, w, form=242)
+        finally:
+            G.set_splitk_spin_limit(prev)
+        for _ in range(4):
+            torch.cuda.synchronize()
+            watch.poll()
+    G.check_splitk_fault()
+
+
+def test_hbm_budget_too_small_for_one_sequence_is_an_error(hipk):
+    """An engine group whose HBM budget cannot hold its weights plus one max_model_len sequence
+    of KV cache fails at start with the numbers, instead of starting with 2 blocks."""
+    from drtc_amd.engine import LLMEngine
+    from drtc_amd.models import LLAMA3_8B, TransformerLM
+
+    m = TransformerLM(LLAMA3_8B.replace(num_layers=2), "cuda", seed=0, full_then_shard=False)
+    with pytest.raises(ValueError, match="HBM budget"):
+        LLMEngine(m, max_batch=8, max_model_len=4096, hbm_budget=0.01, use_graphs=False)
+    eng = LLMEngine(m, max_batch=8, max_model_len=4096, hbm_budget=0.2, use_graphs=False)
+    assert eng.kv.num_blocks >= eng.max_blocks

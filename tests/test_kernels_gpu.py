@@ -847,11 +847,11 @@ def test_linear_residual(hipk, M, N, K):
     _close(y, ref, 3e-2, 2e-2, "linear_residual")
 
 
-@pytest.mark.parametrize("T", [32, 1024, 8192, 1000])
+@pytest.mark.parametrize("T", [32, 1024, 8192, 1000, 1, 8])
 def test_router_logits_on_skinny_kernel_match_fp32(hipk, T):
     """MoE router logits through the transposed skinny HIP GEMM (ops.router_logits): the
-    8 router rows as the activation rows, the T tokens as the streamed rows; T = 1000 is not a
-    multiple of the kernel's row block and takes F.linear."""
+    8 router rows as the activation rows, the T tokens as the streamed rows; T = 1000 / 1 / 8
+    are not multiples of the kernel's row block and are zero-padded (never F.linear)."""
     from drtc_amd.ops import moe as M
     g = torch.Generator(device="cuda").manual_seed(T)
     x = torch.randn(T, 4096, device="cuda", dtype=torch.bfloat16, generator=g)
@@ -863,9 +863,14 @@ def test_router_logits_on_skinny_kernel_match_fp32(hipk, T):
         got = M.router_logits(x, wr)
     finally:
         M.F.linear = real
-    assert bool(lib) == (T % 16 != 0)  # the library GEMM only where the HIP kernel cannot
+    assert not lib  # every T on the HIP kernel
     torch.cuda.synchronize()
     ref = x.float() @ wr.float().t()
     assert got.shape == (T, 8) and got.is_contiguous() and got.dtype == torch.bfloat16
     err = (got.float() - ref).abs().max().item()
     assert err <= 1.5e-2 * ref.abs().max().item(), err
+    # batch invariance: a token's logits do not depend on how many tokens share the call
+    sub = M.router_logits(x[: max(1, T // 3)].contiguous(), wr)
+    assert torch.equal(sub, got[: max(1, T // 3)])
+    view = M.router_logits(x, wr, contiguous=False)
+    assert view.shape == (T, 8) and view.stride(0) == 1 and torch.equal(view, got)

@@ -504,6 +504,28 @@ def test_serve_placement_needs_budgets_on_shared_gpus():
         S.build_feature_backends(args, ["smart=gemma-2b@0:mem=0.3"])
 
 
+def test_serve_group_without_gpus_is_placed_where_it_is_built(monkeypatch):
+    """A tp1 --serve group without @GPUS runs on GPU 0 (one replica): the placement check and
+    the build use that same rule, so it does not collide with groups on the other GPUs of a
+    --gpus 8 server."""
+    import argparse
+
+    from drtc_amd.llm import server as S
+
+    built = []
+    monkeypatch.setattr(S, "build_backend",
+                        lambda sub, devices=None: built.append((sub.model, sub.gpus, devices))
+                        or object())
+    args = argparse.Namespace(backend="engine", model="llama-3-8b", tp=1, gpus=8, max_batch=0,
+                              max_model_len=512, no_graphs=True, custom_allreduce=False,
+                              in_process=True, hbm_budget=None)
+    S.build_feature_backends(args, ["smart=gemma-2b", "summary=llama-3-8b@1",
+                                    "answer=llama-3-8b@2", "suggest=mixtral-8x7b@3"])
+    assert ("gemma-2b", 1, [0]) in built and ("llama-3-8b", 1, [1]) in built
+    with pytest.raises(ValueError, match="GPU 0 is shared"):  # and still checked
+        S.build_feature_backends(args, ["smart=gemma-2b", "summary=llama-3-8b@0"])
+
+
 def test_llm_server_serves_features_from_separate_backends():
     """``llm.server --serve FEATURE=MODEL...``: one service address, one engine group per
     feature (scripted stand-ins here); the feature spec grammar and its errors."""
