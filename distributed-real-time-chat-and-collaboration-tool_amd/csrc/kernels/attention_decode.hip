@@ -26,6 +26,18 @@
 #include "common.h"
 #include "launchers.h"
 
+namespace {
+// s_waitcnt vmcnt(0): every vector-memory load of this wave has landed.  Used right after the
+// first K/V block of a register double-buffered block loop is issued (see the persistent
+// kernel): without it the waitcnt pass merges the loop's entry edge (that block still in
+// flight) with the iterations that issue no next-block loads and guards the block's first
+// QK MFMA with vmcnt(0) / a small vmcnt(n) on EVERY iteration - which waits for the next
+// block's loads as well, so no block ever streams while another is computed.
+__device__ __forceinline__ void vm_wait_all() {
+  __builtin_amdgcn_s_waitcnt((0x7 << 4) | (0xF << 8));
+}
+}  // namespace
+
 namespace drtc {
 
 constexpr int kBS = 32;  // tokens per KV-cache block (fixed by the layout)
@@ -115,6 +127,7 @@ __global__ __launch_bounds__(256, D >= 256 ? 1 : 2) void paged_decode_kernel(
     load_kv_block<D>(cur, k_cache + (phys * Hkv + h) * blk_elems,
                      v_cache + (phys * Hkv + h) * blk_elems, lane);
   }
+  vm_wait_all();  // the first block lands before the loop (vm_wait_all)
   for (; blk < blk_end; blk += 4) {
     const int nb = blk + 4;
     if (nb < blk_end) {  // register double-buffer: next block in flight
@@ -326,6 +339,7 @@ __global__ __launch_bounds__(256, D >= 256 ? 1 : 2) void paged_decode_wave_kerne
     load_kv_block<D>(cur, k_cache + (ph * Hkv + h) * blk_elems,
                      v_cache + (ph * Hkv + h) * blk_elems, lane);
   }
+  vm_wait_all();  // the first block lands before the loop (vm_wait_all)
   for (int blk = blk_begin; blk < blk_end; ++blk) {
     const bool more = blk + 1 < blk_end;
     if (more) {
@@ -584,6 +598,10 @@ __global__ __launch_bounds__(256, D >= 256 ? 1 : 2) void paged_decode_persist_ke
   int bt_reg = load_bt(A, chunk);
   KVRegs<D> cur, nxt;
   load_blk(cur, A, __builtin_amdgcn_readlane(bt_reg, 0), A.begin);
+  // the first block lands before the loop (vm_wait_all: here the merge left a vmcnt(5..2)
+  // in front of every block's QK MFMAs, i.e. a wait for 19 of the 24 next-block loads just
+  // issued; removing it: kernel -1 %, decode pass -0.2 %, profiles/r6c)
+  vm_wait_all();
   while (true) {
     f32x4 o[NT];
 #pragma unroll

@@ -5,7 +5,7 @@ grid capped at G workgroups (4 waves each): how many CUs does the HBM-bound atte
 
 Llama-3-8B heads (Hq 32, Hkv 8, D 128), contexts 150-200 tokens (the smart-reply decode),
 B = 1024 and 512 (a micro-batch half).  Prints one JSON line per (B, G): us per call and the
-K+V bytes read per second."""
+K+V bytes read per second.  argv[1]: comma-separated caps (default: the sweep below)."""
 import json
 import math
 import random
@@ -18,6 +18,8 @@ from drtc_amd import ops  # noqa: E402
 
 
 def main():
+    caps = [int(c) for c in (sys.argv[1] if len(sys.argv) > 1 else
+                             "0,512,384,256,192,160,128,96,64,32").split(",")]
     dev = torch.device("cuda")
     Hq, Hkv, D, bs = 32, 8, 128, ops.KV_BLOCK
     rng = random.Random(0)
@@ -47,7 +49,7 @@ def main():
         ws = ops.DecodeWorkspace(B, Hq, D, parts, dev)
         kv_bytes = sum(c - 1 for c in ctxs) * Hkv * D * 2 * 2
         ref = None
-        for G in (0, 512, 384, 256, 192, 160, 128, 96, 64, 32):
+        for G in caps:
             def fn():
                 ops.paged_decode_attention_rope(qkv, pos, slots, cos_sin, Hq, Hkv, D, kc, vc, bt,
                                                 ctx, D ** -0.5, out=out, blocks_per_part=bpp,

@@ -100,6 +100,81 @@ __global__ __launch_bounds__(256) void gather_kernel(const u32x4* __restrict__ s
   sink[blockIdx.x * 256 + threadIdx.x] = acc.x ^ acc.y ^ acc.z ^ acc.w;
 }
 
+// the decode attention's exact per-lane addressing: one 16 KiB item = an 8 KiB K block
+// ([32 tok][128 D]: instruction s of lanes (t, g) reads token t's dims 32 s + 8 g .. + 8, for
+// tokens 0-15 and 16-31) and an 8 KiB V block (8 groups x [128 D][4 tok]: 8-B loads of 16
+// rows per group), registers only; DEPTH items in flight per wave (1 = the kernel today: the
+// next item's loads issued while the current one is consumed)
+struct KV16 {
+  u32x4 k[8];
+  unsigned long long v[16];
+};
+
+template <int DEPTH>
+__global__ __launch_bounds__(256, 2) void attnkv_kernel(const u32x4* __restrict__ src,
+                                                        const int* __restrict__ order,
+                                                        int n_items, unsigned* __restrict__ sink) {
+  const int lane = threadIdx.x & 63, t = lane & 15, g = lane >> 4;
+  const int W = gridDim.x * 4;
+  unsigned acc = 0;
+  auto load = [&](KV16& r, int it) {
+    const char* kb = reinterpret_cast<const char*>(src) + (long)order[it] * 16384;
+    const char* vb = kb + 8192;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      r.k[s] = *reinterpret_cast<const u32x4*>(kb + t * 256 + 64 * s + 16 * g);
+      r.k[4 + s] = *reinterpret_cast<const u32x4*>(kb + (16 + t) * 256 + 64 * s + 16 * g);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      r.v[i] = *reinterpret_cast<const unsigned long long*>(vb + g * 1024 + (16 * i + t) * 8);
+      r.v[8 + i] = *reinterpret_cast<const unsigned long long*>(vb + (4 + g) * 1024 + (16 * i + t) * 8);
+    }
+  };
+  auto fold = [&](const KV16& r) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc ^= r.k[j].x ^ r.k[j].w;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) acc ^= (unsigned)r.v[j];
+  };
+  KV16 buf[DEPTH + 1];
+  int it = blockIdx.x * 4 + (threadIdx.x >> 6);
+#pragma unroll
+  for (int d = 0; d < DEPTH; ++d)
+    if (it + d * W < n_items) load(buf[d], it + d * W);
+  for (; it < n_items; it += W) {
+    const int nx = it + DEPTH * W;
+    if (nx < n_items) load(buf[DEPTH], nx);
+    fold(buf[0]);
+#pragma unroll
+    for (int d = 0; d < DEPTH; ++d) buf[d] = buf[d + 1];
+  }
+  sink[blockIdx.x * 256 + threadIdx.x] = acc;
+}
+
+template <int DEPTH>
+void attnkv(const u32x4* buf, const int* order, int n_items, unsigned* sink, int G) {
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  hipLaunchKernelGGL((attnkv_kernel<DEPTH>), dim3(G), dim3(256), 0, 0, buf, order, n_items, sink);
+  CK(hipDeviceSynchronize());
+  const int reps = 5;
+  CK(hipEventRecord(e0));
+  for (int r = 0; r < reps; ++r)
+    hipLaunchKernelGGL((attnkv_kernel<DEPTH>), dim3(G), dim3(256), 0, 0, buf, order, n_items, sink);
+  CK(hipEventRecord(e1));
+  CK(hipEventSynchronize(e1));
+  float ms = 0;
+  CK(hipEventElapsedTime(&ms, e0, e1));
+  const double tbs = (double)n_items * 16384 * reps / (ms * 1e-3) / 1e12;
+  std::printf("{\"probe\": \"attn_kv_addressing\", \"items_in_flight_per_wave\": %d, \"wgs\": %d, "
+              "\"TBs\": %.3f}\n", DEPTH, G, tbs);
+  std::fflush(stdout);
+  CK(hipEventDestroy(e0));
+  CK(hipEventDestroy(e1));
+}
+
 template <int U, bool NT>
 void sweep(const u32x4* buf, long n16, unsigned* sink, unsigned* where, int G) {
   const long per = (n16 / G) / (256L * U) * (256L * U);
@@ -177,6 +252,16 @@ int main() {
   CK(hipMemcpy(d_order, order.data(), n_items * sizeof(int), hipMemcpyHostToDevice));
   for (int G : {64, 96, 128, 192, 256, 384, 512, 1024}) gather<false>(buf, d_order, n_items, sink, G);
   for (int G : {128, 256, 512}) gather<true>(buf, d_order, n_items, sink, G);
+  CK(hipFree(d_order));
+  // the attention's K / V addressing over random 16 KiB items (K block + V block)
+  const int n_kv = (int)(bytes / 16384);
+  std::vector<int> ord16(n_kv);
+  std::iota(ord16.begin(), ord16.end(), 0);
+  std::shuffle(ord16.begin(), ord16.end(), std::mt19937(2));
+  CK(hipMalloc(&d_order, n_kv * sizeof(int)));
+  CK(hipMemcpy(d_order, ord16.data(), n_kv * sizeof(int), hipMemcpyHostToDevice));
+  for (int G : {256, 512}) attnkv<1>(buf, d_order, n_kv, sink, G);
+  for (int G : {256, 512}) attnkv<2>(buf, d_order, n_kv, sink, G);
   CK(hipFree(d_order));
   CK(hipFree(buf));
   CK(hipFree(sink));
