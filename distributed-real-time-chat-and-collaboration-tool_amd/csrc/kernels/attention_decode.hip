@@ -26,6 +26,8 @@
 #include "common.h"
 #include "launchers.h"
 
+typedef __attribute__((address_space(3))) void* ad_lds_ptr;
+
 namespace {
 // s_waitcnt vmcnt(0): every vector-memory load of this wave has landed.  Used right after the
 // first K/V block of a register double-buffered block loop is issued (see the persistent
@@ -518,6 +520,40 @@ DRTC_DEVICE void rope_frags(bf16x8* f, const float* __restrict__ cos_sin, int po
   }
 }
 
+// One LDS-DMA wave-instruction of one dword per lane: 256 contiguous bytes land at the LDS byte
+// address `dst` (M0 saved and restored).  Counts in vmcnt like any vector load.
+DRTC_DEVICE void dma_dword_lds(unsigned dst, unsigned voff, __amdgpu_buffer_rsrc_t rsrc) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\t"
+               "buffer_load_dword %2, %3, %4 offen lds\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "s"(dst), "v"(voff), "s"(rsrc), "s"(0u)
+               : "memory");
+}
+
+// rope_frags with the position's cos | sin row read from LDS (the staged row of the item)
+template <int D>
+DRTC_DEVICE void rope_frags_lds(bf16x8* f, const float* cs_row, int g) {
+  constexpr int KS = D / 32;
+  const float* cs = cs_row + 8 * g;
+#pragma unroll
+  for (int s = 0; s < KS / 2; ++s) {
+    const f32x4 ca = *reinterpret_cast<const f32x4*>(cs + 32 * s);
+    const f32x4 cb = *reinterpret_cast<const f32x4*>(cs + 32 * s + 4);
+    const f32x4 sa = *reinterpret_cast<const f32x4*>(cs + D / 2 + 32 * s);
+    const f32x4 sb = *reinterpret_cast<const f32x4*>(cs + D / 2 + 32 * s + 4);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float c = j < 4 ? ca[j] : cb[j - 4];
+      const float sn = j < 4 ? sa[j] : sb[j - 4];
+      const float a = bf2f(f[s][j]), b = bf2f(f[s + KS / 2][j]);
+      f[s][j] = f2bf(a * c - b * sn);
+      f[s + KS / 2][j] = f2bf(b * c + a * sn);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
 template <int D, bool ROPE>
 __global__ __launch_bounds__(256, D >= 256 ? 1 : 2) void paged_decode_persist_kernel(
     bf16_t* __restrict__ out, float* __restrict__ part_o,
@@ -538,13 +574,18 @@ __global__ __launch_bounds__(256, D >= 256 ? 1 : 2) void paged_decode_persist_ke
 
   struct Item {
     int it, b, h, ctx, begin, end, nparts, pos;  // pos: the step token's position (ROPE)
+    int64_t slot;                                // its KV-cache slot (ROPE)
   };
   // first item >= it (stride W) with work; padded sequences get their zeros
   auto next_item = [&](int it) -> Item {
     for (; it < n_items; it += W) {
       const int p = it / BH, bh = it - p * BH;
       const int b = bh / Hkv, h = bh - b * Hkv;
-      const int ctx = __builtin_amdgcn_readfirstlane(context_lens[b]);
+      // the sequence's three words in one round trip (issued together, then used)
+      const int ctx_l = context_lens[b];
+      const int pos_l = ROPE ? rope.positions[b] : 0;
+      const int64_t slot_l = ROPE ? rope.slots[b] : 0;
+      const int ctx = __builtin_amdgcn_readfirstlane(ctx_l);
       if (ctx <= 0) {
         if (p == 0) {
           bf16x8 z;
@@ -559,12 +600,40 @@ __global__ __launch_bounds__(256, D >= 256 ? 1 : 2) void paged_decode_persist_ke
       const int nparts = (nblk + blocks_per_part - 1) / blocks_per_part;
       if (p >= nparts) continue;
       const int begin = p * blocks_per_part;
-      // ROPE: the position is read here, one item ahead of its use (the rotation at the
-      // item's start then waits for the cos / sin rows only)
-      const int pos = ROPE ? __builtin_amdgcn_readfirstlane(rope.positions[b]) : 0;
-      return Item{it, b, h, ctx, begin, min(nblk, begin + blocks_per_part), nparts, pos};
+      // ROPE: the position and slot are read here, one item ahead of their use
+      const int pos = ROPE ? __builtin_amdgcn_readfirstlane(pos_l) : 0;
+      const int64_t slot = ROPE ? (int64_t)__builtin_amdgcn_readfirstlane((int)slot_l) |
+                                      ((int64_t)__builtin_amdgcn_readfirstlane(
+                                           (int)(slot_l >> 32)) << 32)
+                                : 0;
+      return Item{it, b, h, ctx, begin, min(nblk, begin + blocks_per_part), nparts, pos, slot};
     }
-    return Item{n_items, 0, 0, 0, 0, 0, 0, 0};
+    return Item{n_items, 0, 0, 0, 0, 0, 0, 0, 0};
+  };
+  // ROPE, D = 128 (STAGE): the step token's k and v rows (256 B each, QKV GEMM output) and its
+  // cos | sin row (512 B) are staged into this wave's 1 KiB LDS slot by LDS-DMA when the item
+  // is chosen - one item ahead, beside the current item's block stream, holding no registers -
+  // so starting an item (q rotation, the step token's score, v row and cache write) reads LDS
+  // instead of waiting on three memory round trips.  Slot: [0, 256) k row, [256, 512) v row,
+  // [512, 1024) cos | sin.
+  constexpr bool STAGE = ROPE && D == 128;
+  __shared__ __attribute__((aligned(16))) char rope_lds[STAGE ? 4 * 1024 : 16];
+  char* const slot_lds = rope_lds + (STAGE ? 1024 * wave_id_uniform() : 0);
+  const unsigned slot_dst =
+      __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(ad_lds_ptr)slot_lds);
+  const __amdgpu_buffer_rsrc_t rsrc_q =
+      __builtin_amdgcn_make_buffer_rsrc((void*)q, (short)0, 0x7FFFFFFF, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsrc_cs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)rope.cos_sin, (short)0, 0x7FFFFFFF, 0x00020000);
+  auto stage_rope = [&](const Item& X) {
+    if constexpr (STAGE) {
+      const unsigned row = (unsigned)X.b * (unsigned)q_stride * 2u + (unsigned)lane * 4u;
+      dma_dword_lds(slot_dst, row + (unsigned)((Hq + X.h) * D) * 2u, rsrc_q);
+      dma_dword_lds(slot_dst + 256, row + (unsigned)((Hq + Hkv + X.h) * D) * 2u, rsrc_q);
+      const unsigned cs = (unsigned)X.pos * (unsigned)(D * 4) + (unsigned)lane * 4u;
+      dma_dword_lds(slot_dst + 512, cs, rsrc_cs);
+      dma_dword_lds(slot_dst + 768, cs + 256u, rsrc_cs);
+    }
   };
   auto load_q = [&](bf16x8* qf, const Item& A) {
     const bf16_t* qrow = q + (int64_t)A.b * q_stride + (int64_t)(A.h * G + col) * D;
@@ -585,19 +654,23 @@ __global__ __launch_bounds__(256, D >= 256 ? 1 : 2) void paged_decode_persist_ke
                        v_cache + (phys * Hkv + A.h) * blk_elems, lane, cached(A) - blk * kBS);
   };
   auto rope_q = [&](bf16x8* qf, const Item& A) {
-    if constexpr (ROPE)
+    if constexpr (STAGE)
+      rope_frags_lds<D>(qf, reinterpret_cast<const float*>(slot_lds + 512), g);
+    else if constexpr (ROPE)
       rope_frags<D>(qf, rope.cos_sin, A.pos, g);
   };
 
   Item A = next_item(blockIdx.x * 4 + wave_id_uniform());
   if (A.it >= n_items) return;
   bf16x8 qf[KS], qn[KS];
+  stage_rope(A);
   load_q(qf, A);
-  rope_q(qf, A);
   int chunk = A.begin;  // block-table slice [chunk, chunk + 64) of item A in bt_reg
   int bt_reg = load_bt(A, chunk);
   KVRegs<D> cur, nxt;
   load_blk(cur, A, __builtin_amdgcn_readlane(bt_reg, 0), A.begin);
+  if constexpr (STAGE) vm_wait_all();  // the first item's staged rows
+  rope_q(qf, A);
   // the first block lands before the loop (vm_wait_all: here the merge left a vmcnt(5..2)
   // in front of every block's QK MFMAs, i.e. a wait for 19 of the 24 next-block loads just
   // issued; removing it: kernel -1 %, decode pass -0.2 %, profiles/r6c)
@@ -612,12 +685,17 @@ __global__ __launch_bounds__(256, D >= 256 ? 1 : 2) void paged_decode_persist_ke
         // the partition holding the step's token: it opens the online softmax (m = its
         // score, p = 1 counted once in lane group 0, o = its v row), before the next
         // item's loads are issued (fewest live registers)
-        const bf16_t* kn = q + (int64_t)A.b * q_stride + (int64_t)(Hq + A.h) * D;
-        const bf16_t* vn = kn + (int64_t)Hkv * D;
+        const bf16_t* kn = STAGE ? reinterpret_cast<const bf16_t*>(slot_lds)
+                                 : q + (int64_t)A.b * q_stride + (int64_t)(Hq + A.h) * D;
+        const bf16_t* vn = STAGE ? reinterpret_cast<const bf16_t*>(slot_lds + 256)
+                                 : kn + (int64_t)Hkv * D;
         bf16x8 kf[KS];
 #pragma unroll
         for (int s = 0; s < KS; ++s) kf[s] = load_bf16x8(kn + 32 * s + 8 * g);
-        rope_frags<D>(kf, rope.cos_sin, A.pos, g);
+        if constexpr (STAGE)
+          rope_frags_lds<D>(kf, reinterpret_cast<const float*>(slot_lds + 512), g);
+        else
+          rope_frags<D>(kf, rope.cos_sin, A.pos, g);
         float dot = 0.f;
 #pragma unroll
         for (int s = 0; s < KS; ++s)
@@ -627,7 +705,7 @@ __global__ __launch_bounds__(256, D >= 256 ? 1 : 2) void paged_decode_persist_ke
         dot += __shfl_xor(dot, 32, 64);
         m = dot * scale_log2e;
         lsum = g == 0 ? 1.f : 0.f;
-        const int64_t slot = rope.slots[A.b];
+        const int64_t slot = A.slot;
         const bool writer = col == 0 && slot >= 0;  // lanes 0 / 16 / 32 / 48
         const int64_t cblk = slot / kBS, off = slot - cblk * kBS;
         if (writer) {
@@ -653,6 +731,12 @@ __global__ __launch_bounds__(256, D >= 256 ? 1 : 2) void paged_decode_persist_ke
     const bool have_next = Bn.it < n_items;
     int bt_n = 0;
     if (have_next) {
+      if constexpr (STAGE) {
+        // this item's slot reads (q rotation, step token) have returned before the DMA
+        // that overwrites the slot is issued
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+        stage_rope(Bn);
+      }
       load_q(qn, Bn);
       bt_n = load_bt(Bn, Bn.begin);
     }
