@@ -575,11 +575,22 @@ __global__ __launch_bounds__(256, D >= 256 ? 1 : 2) void paged_decode_persist_ke
   struct Item {
     int it, b, h, ctx, begin, end, nparts, pos;  // pos: the step token's position (ROPE)
     int64_t slot;                                // its KV-cache slot (ROPE)
+    int p;                                       // its partition
+  };
+  // Wave w takes logical items w, w + W, w + 2W, ... (W = the grid's waves).  Every odd full
+  // round is mirrored (logical item k W + j is work item k W + W - 1 - j): with the engine's
+  // slots ordered by context length (LLMEngine._sort_slots) a wave then takes one long and
+  // one short sequence per pair of rounds, so the slowest wave carries ~2-6 % more blocks
+  // than the mean instead of ~10-12 % (chat contexts of 4-8 blocks, 4 items per wave).
+  auto phys = [&](int it) -> int {
+    const int k = it / W, j = it - k * W;
+    return ((k & 1) && (k + 1) * W <= n_items) ? k * W + (W - 1 - j) : it;
   };
   // first item >= it (stride W) with work; padded sequences get their zeros
   auto next_item = [&](int it) -> Item {
     for (; it < n_items; it += W) {
-      const int p = it / BH, bh = it - p * BH;
+      const int ip = phys(it);
+      const int p = ip / BH, bh = ip - p * BH;
       const int b = bh / Hkv, h = bh - b * Hkv;
       // the sequence's three words in one round trip (issued together, then used)
       const int ctx_l = context_lens[b];
@@ -606,9 +617,10 @@ __global__ __launch_bounds__(256, D >= 256 ? 1 : 2) void paged_decode_persist_ke
                                       ((int64_t)__builtin_amdgcn_readfirstlane(
                                            (int)(slot_l >> 32)) << 32)
                                 : 0;
-      return Item{it, b, h, ctx, begin, min(nblk, begin + blocks_per_part), nparts, pos, slot};
+      return Item{it, b, h, ctx, begin, min(nblk, begin + blocks_per_part), nparts, pos, slot,
+                  p};
     }
-    return Item{n_items, 0, 0, 0, 0, 0, 0, 0, 0};
+    return Item{n_items, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   };
   // ROPE, D = 128 (STAGE): the step token's k and v rows (256 B each, QKV GEMM output) and its
   // cos | sin row (512 B) are staged into this wave's 1 KiB LDS slot by LDS-DMA when the item
@@ -681,7 +693,7 @@ __global__ __launch_bounds__(256, D >= 256 ? 1 : 2) void paged_decode_persist_ke
     for (int i = 0; i < NT; ++i) o[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
     float m = kNegBig, lsum = 0.f;
     if constexpr (ROPE) {
-      if (A.it / BH == A.nparts - 1) {
+      if (A.p == A.nparts - 1) {
         // the partition holding the step's token: it opens the online softmax (m = its
         // score, p = 1 counted once in lane group 0, o = its v row), before the next
         // item's loads are issued (fewest live registers)
@@ -803,7 +815,7 @@ __global__ __launch_bounds__(256, D >= 256 ? 1 : 2) void paged_decode_persist_ke
     lsum += __shfl_xor(lsum, 32, 64);
     if (col < G) {
       const int hq = A.h * G + col;
-      const int p = A.it / BH;
+      const int p = A.p;
       if (A.nparts == 1) {
         const float inv = 1.f / lsum;
         bf16_t* orow = out + ((int64_t)A.b * Hq + hq) * D + 4 * g;

@@ -745,9 +745,38 @@ class LLMEngine:
                 return done  # the next step() admits and prefills
         with self.lock:
             self._ensure_blocks()
+            self._sort_slots()
         if self.running:
             self._inflight = self._launch_decode(pipelined=False)
         return done
+
+    # decode batches of at least this many rows keep their slots ordered by context length
+    # (DRTC_SORT_SLOTS=0 disables): the persistent decode attention deals its (sequence,
+    # kv head) items to waves round-robin with every odd round mirrored, so ordered slots give
+    # each wave a balanced share of cache blocks (attention_decode.hip ``phys``)
+    SORT_SLOTS_MIN = int(os.environ.get("DRTC_SORT_SLOTS", "256"))
+
+    def _sort_slots(self) -> None:
+        """Reorder the running slots by context length, longest first.  Only between steps
+        with nothing in flight (a non-pipelined decode launch stages every input from the
+        host); pipelined steps keep the order, since every context grows by one per step."""
+        n = len(self.running)
+        if self.SORT_SLOTS_MIN <= 0 or n < self.SORT_SLOTS_MIN or self._inflight is not None:
+            return
+        ctx = self.ctx[:n]
+        if np.all(ctx[:-1] >= ctx[1:]):
+            return
+        order = np.argsort(-ctx, kind="stable")
+        for arr in (self.bt, self.ctx, self.last, self.temp, self.topk, self.topp, self.gen,
+                    self.max_new, self.eos_stop, self.nblk):
+            arr[:n] = arr[:n][order]
+        new_of = np.empty(n, dtype=np.int64)
+        new_of[order] = np.arange(n)
+        self.stop_ids = {int(new_of[s_]): v for s_, v in self.stop_ids.items()}
+        self.running = [self.running[i] for i in order.tolist()]
+        for s_, r in enumerate(self.running):
+            r.slot = s_
+        self.stats["slot_sorts"] += 1
 
     def _process_inflight(self) -> list[Request]:
         step, self._inflight = self._inflight, None

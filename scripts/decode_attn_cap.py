@@ -5,7 +5,8 @@ grid capped at G workgroups (4 waves each): how many CUs does the HBM-bound atte
 
 Llama-3-8B heads (Hq 32, Hkv 8, D 128), contexts 150-200 tokens (the smart-reply decode),
 B = 1024 and 512 (a micro-batch half).  Prints one JSON line per (B, G): us per call and the
-K+V bytes read per second.  argv[1]: comma-separated caps (default: the sweep below)."""
+K+V bytes read per second.  argv[1]: comma-separated caps (default: the sweep below);
+argv[2]: context orders, "random" and / or "sorted" (longest first, as the engine's slots)."""
 import json
 import math
 import random
@@ -24,8 +25,11 @@ def main():
     Hq, Hkv, D, bs = 32, 8, 128, ops.KV_BLOCK
     rng = random.Random(0)
     cos_sin = ops.build_rope_cache(4096, D, 500000.0, None, dev)
-    for B in (1024, 512):
+    orders = sys.argv[2].split(",") if len(sys.argv) > 2 else ["random"]
+    for B, order in [(b, o) for b in (1024, 512) for o in orders]:
         ctxs = [rng.randint(150, 200) for _ in range(B)]
+        if order == "sorted":  # the engine's slot order (LLMEngine._sort_slots)
+            ctxs.sort(reverse=True)
         maxb = max(math.ceil(c / bs) for c in ctxs)
         nb = sum(math.ceil(c / bs) for c in ctxs) + 1
         kc = torch.randn(nb, Hkv, bs, D, device=dev, dtype=torch.bfloat16)
@@ -75,7 +79,7 @@ def main():
                 e1.synchronize()
                 ts.append(e0.elapsed_time(e1) * 1e3 / 20)
             us = sorted(ts)[len(ts) // 2]
-            print(json.dumps({"B": B, "max_wgs": G, "us": round(us, 2),
+            print(json.dumps({"B": B, "order": order, "max_wgs": G, "us": round(us, 2),
                               "kv_TBs": round(kv_bytes / us / 1e6, 3), "same_as_full": same}),
                   flush=True)
 

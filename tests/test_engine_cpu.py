@@ -107,6 +107,43 @@ def test_pipelined_decode_matches_synchronous():
     assert st_pipe["decode_steps_pipelined"] > 0 and st_sync["decode_steps_pipelined"] == 0
 
 
+def test_sorted_slots_match_unsorted(monkeypatch):
+    """Slots reordered by context length before non-pipelined decode launches
+    (LLMEngine._sort_slots, for the balanced attention item order) leave every greedy output
+    unchanged - with stop-token finishes, staggered lengths, block growth, pipelined steps and
+    mid-run admissions - and the order holds: longest context first."""
+    from drtc_amd.engine import Request
+
+    m = TransformerLM(TINY_LLAMA, "cpu", seed=6)
+    prompts = [list(range(1, 5 + 11 * ((3 * i) % 7))) for i in range(7)]
+
+    def run(sort_min: int):
+        monkeypatch.setattr(LLMEngine, "SORT_SLOTS_MIN", sort_min)
+        eng = LLMEngine(m, max_batch=8, max_model_len=256, num_blocks=96, use_graphs=False)
+        probe = eng.generate([prompts[1]], SamplingParams.greedy(5, ignore_eos=True))[0]
+        stop_tok = probe.output_ids[2]
+        params = [SamplingParams(max_new_tokens=10 + 4 * i, temperature=0.0, top_k=0, top_p=1.0,
+                                 stop_token_ids=(stop_tok,) if i == 1 else ())
+                  for i in range(7)]
+        reqs = [eng.add_request(Request(list(p), prm)) for p, prm in zip(prompts[:5], params[:5])]
+        orders = []
+        for _ in range(5):
+            eng.step()
+            n = len(eng.running)
+            orders.append(list(eng.ctx[:n]))
+        reqs += [eng.add_request(Request(list(p), prm)) for p, prm in zip(prompts[5:], params[5:])]
+        while eng.has_work():
+            eng.step()
+        assert eng.alloc.num_used == 0 and not eng.running
+        return [(r.output_ids, r.finish_reason) for r in reqs], eng.stats, orders
+
+    plain, st_plain, _ = run(0)
+    srt, st_srt, orders = run(1)
+    assert srt == plain
+    assert st_srt["slot_sorts"] > 0 and st_plain.get("slot_sorts", 0) == 0
+    assert any(o == sorted(o, reverse=True) and len(set(o)) > 1 for o in orders)
+
+
 @pytest.mark.parametrize("cfg", [TINY_LLAMA, TINY_MIXTRAL], ids=lambda c: c.name)
 def test_mixed_steps_match_prefill_first(cfg):
     """Mixed scheduling (late prompts prefilled inside decode steps under a
