@@ -42,6 +42,8 @@ PYBIND11_MODULE(_hipk, m) {
                                 block_size, write_v, S(st));
   });
   m.def("set_rope_variant", [](int v) { drtc::set_rope_variant(v); });
+  m.def("w4_set_krot", [](int k) { drtc::w4_set_krot(k); });
+  m.def("w4_krot", []() { return drtc::w4_krot(); });
   m.def("kv_write_v", [](u64 v_cache, u64 qkv, int qkv_stride, u64 seg_tok, u64 seg_len,
                          u64 seg_blk, int nseg, int Hq, int Hkv, int D, int block_size,
                          u64 st) {

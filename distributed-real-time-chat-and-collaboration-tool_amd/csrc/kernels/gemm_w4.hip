@@ -75,6 +75,7 @@ struct W4Params {
   int up_off;
   int group_m;
   int xk;  // K-slice-by-XCD tile order (split-K forms; see gemm_w4_kernel)
+  int krot;  // V & 16: distinct K start offsets over the 8 XCD labels (8: one per XCD)
   int* err;        // split-K fault word: the workspace's last counter, outside every ticket
                    // range; read and cleared by the host
   int spin_limit;  // bound of the parallel combine's arrival poll (< 0: test hook, always fault)
@@ -617,7 +618,8 @@ __global__ __launch_bounds__(kW4Threads, 1) void gemm_w4_kernel(W4Params p) {
   // each XCD label b % 8 starts at its own eighth of K, so the eight XCDs reach their tile
   // seams (the epilogue's store burst, 4 MiB per XCD) at different times while the 32
   // workgroups of one XCD still stream the same K tile through its L2 in lockstep.
-  const int kst = (V & 16) ? ((orig & 7) * nk) >> 3 : 0;
+  // (p.krot < 8 gives XCD labels b % 8 in groups of 8 / krot one offset: w4_set_krot)
+  const int kst = (V & 16) ? ((((orig & 7) * p.krot) >> 3) * nk) / p.krot : 0;
   const unsigned k0b = (unsigned)kst * 128u, k1b = (unsigned)(kst + 1 < nk ? kst + 1 : 0) * 128u;
   // ---- prologue: tiles 0 and 1 into stages 0 and 1
 #pragma unroll
@@ -759,6 +761,10 @@ int w4_cfg() {
 
 }  // namespace
 
+static int g_w4_krot = 8;
+void w4_set_krot(int k) { g_w4_krot = (k == 1 || k == 2 || k == 4) ? k : 8; }
+int w4_krot() { return g_w4_krot; }
+
 int w4_num_cus() {
   static int n = [] {
     int dev = 0, cus = 0;
@@ -809,6 +815,7 @@ int launch_gemm_w4(void* c, const void* a, const void* b, const void* r, int M, 
   p.kt_split = K / 64 / splitk;
   p.up_off = up_off;
   p.group_m = group_m;
+  p.krot = g_w4_krot;
   if (xk) {
     const int64_t tiles = (int64_t)p.tiles_m * p.tiles_n;
     if ((v & 8) || 8 % splitk || (tiles * splitk) % 8 || tiles % (8 / splitk)) return -1;

@@ -117,6 +117,8 @@ int launch_skinny_norm_gemm(void* y, void* h_out, const void* x, const void* res
 // up, N = up_off).  v = schedule bits (0 per-tile, 2 temporal stores, 8 persistent, 24
 // persistent + per-XCD K rotation); splitk > 1 (per-tile form) needs slab + counters (zeroed
 // once): 256 KiB of slab per tile and slice.
+void w4_set_krot(int k);
+int w4_krot();
 int launch_gemm_w4(void* c, const void* a, const void* b, const void* r, int M, int N, int K,
                    int lda, int ldb, int ldc, int ldr, int epi, int up_off, int splitk,
                    int group_m, void* slab, int64_t slab_bytes, int* counters, int n_counters,

@@ -69,17 +69,28 @@ def main():
             else:
                 fns[arm] = lambda form=form: G.xd_gemm(x, nxt(), a.epi, out=out, form=form)
         else:
-            # "vV" or "vV:splitk:group_m" (group_m < 0: K-slice-by-XCD tile order)
+            # "vV" or "vV:splitk:group_m[:kR]" (group_m < 0: K-slice-by-XCD tile order;
+            # kR: R distinct per-XCD K start offsets of the rotating variants, w4_set_krot)
             f = arm[1:].split(":")
             v = int(f[0])
             sk = int(f[1]) if len(f) > 1 else a.splitk
             gm = int(f[2]) if len(f) > 2 else a.group_m
+            kr = int(f[3][1:]) if len(f) > 3 else 8
             if a.epi == "residual":
                 fns[arm] = (lambda v=v, sk=sk, gm=gm: G.mfma_gemm(
                     x, nxt(), "residual", residual=res, out=res, variant=v, splitk=sk, group_m=gm))
             else:
                 fns[arm] = (lambda v=v, sk=sk, gm=gm: G.mfma_gemm(
                     x, nxt(), a.epi, out=out, variant=v, splitk=sk, group_m=gm))
+            from drtc_amd.ops._ext import hipk as _hk
+
+            def with_krot(f0=fns[arm], kr=kr):  # every call runs with this arm's K rotation
+                _hk().w4_set_krot(kr)
+                try:
+                    return f0()
+                finally:
+                    _hk().w4_set_krot(8)
+            fns[arm] = with_krot
     # correctness of every hand arm against an fp32 reference (one call each)
     ref = x.float() @ w.float().t()
     if a.epi == "residual":
