@@ -104,6 +104,15 @@ PYBIND11_MODULE(_hipk, m) {
                                 P<void>(slab), slab_bytes, P<int>(counters), n_counters,
                                 variant - 7, S(st));
   });
+  // gemm_w4 grouped persistent form (ops.gemm.mfma_gemm_grouped): per-group weights, device
+  // row offsets
+  m.def("gemm_grouped", [](u64 c, u64 a, u64 b, u64 grp, int n_grp, int max_rows, int N, int K,
+                           int lda, int ldb, int ldc, int64_t b_grp, int epi, int up_off,
+                           int group_m, u64 st) {
+    return drtc::launch_gemm_w4_grouped(P<void>(c), P<const void>(a), P<const void>(b),
+                                        P<const int>(grp), n_grp, max_rows, N, K, lda, ldb, ldc,
+                                        b_grp, epi, up_off, group_m, S(st));
+  });
   // gemm_xd (ops.gemm.xd_gemm): decode-shaped tiles, XCD-partitioned order, split-K 1..8
   m.def("gemm_xd", [](u64 c, u64 a, u64 b, u64 r, int M, int N, int K, int lda, int ldb, int ldc,
                       int ldr, int epi, int mt, int nf, int splitk, u64 slab, int64_t slab_bytes,

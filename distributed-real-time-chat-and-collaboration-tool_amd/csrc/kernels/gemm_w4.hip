@@ -79,7 +79,36 @@ struct W4Params {
   int* err;        // split-K fault word: the workspace's last counter, outside every ticket
                    // range; read and cleared by the host
   int spin_limit;  // bound of the parallel combine's arrival poll (< 0: test hook, always fault)
+  // V & 64, grouped form (persistent only): n_grp row groups of A / C, group g = rows
+  // [grp[g], grp[g + 1]) (device array, written by the producing kernel: no host sync), each
+  // multiplied by its own B at b + g * b_grp.  tiles_m is unused (the tile count is derived on
+  // the device); M bounds the rows the launcher sized the grid for.
+  const int* grp;
+  int n_grp;
+  int64_t b_grp;
 };
+
+// Position of one output tile: row tile tm, column tile tn; grouped form: rows [row0,
+// min(row0 + 256, mend)) and operand B b (the plain forms read 256 tm, M and p.b instead, so
+// their code is the same as before the grouped form existed: no spill of the 256 + 256
+// register budget).
+struct W4Pos {
+  int tm, tn;
+  int row0, mend;
+  const bf16_t* b;
+};
+template <int V>
+DRTC_DEVICE int w4_row0(const W4Pos& q) {
+  if constexpr ((V & 64) != 0) return q.row0; else return 256 * q.tm;
+}
+template <int V>
+DRTC_DEVICE int w4_mend(const W4Params& p, const W4Pos& q) {
+  if constexpr ((V & 64) != 0) return q.mend; else return p.M;
+}
+template <int V>
+DRTC_DEVICE const bf16_t* w4_bop(const W4Params& p, const W4Pos& q) {
+  if constexpr ((V & 64) != 0) return q.b; else return p.b;
+}
 
 template <int EPI>
 DRTC_DEVICE constexpr bool w4_glu() { return EPI == W4_SILU || EPI == W4_GELU; }
@@ -284,14 +313,14 @@ DRTC_DEVICE void w4_st8(bf16_t* p, bf16x4 v) {
 }
 
 template <int EPI, int V>
-DRTC_DEVICE void w4_epilogue(const W4Params& p, f32x4 (&acc)[8][8], int tm, int tn, int wm,
-                             int wn, int l16, int g, int slice) {
+DRTC_DEVICE void w4_epilogue(const W4Params& p, f32x4 (&acc)[8][8], int row0, int mend, int tn,
+                             int wm, int wn, int l16, int g, int slice) {
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int m = 256 * tm + 128 * wm + 16 * i + 4 * g + r;
-      if (m >= p.M) continue;
+      const int m = row0 + 128 * wm + 16 * i + 4 * g + r;
+      if (m >= mend) continue;
       bf16_t* crow = p.c + (int64_t)m * p.ldc;
       if constexpr (w4_glu<EPI>()) {
         const int n = 128 * tn + 64 * wn + 4 * l16;
@@ -319,18 +348,18 @@ DRTC_DEVICE void w4_epilogue(const W4Params& p, f32x4 (&acc)[8][8], int tm, int 
     for (int i = 0; i < 8; ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int m = min(256 * tm + 128 * wm + 16 * i + 4 * g + r, p.M - 1);
+        const int m = min(row0 + 128 * wm + 16 * i + 4 * g + r, mend - 1);
         rv[i][r] = *reinterpret_cast<const bf16x8*>(p.r + (int64_t)m * p.ldr + n);
       }
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int m = 256 * tm + 128 * wm + 16 * i + 4 * g + r;
+        const int m = row0 + 128 * wm + 16 * i + 4 * g + r;
         bf16x8 o;
 #pragma unroll
         for (int j = 0; j < 8; ++j) o[j] = f2bf(acc[i][j][r] + bf2f(rv[i][r][j]));
-        if (m >= p.M) continue;
+        if (m >= mend) continue;
         w4_st16<V>(p.c + (int64_t)m * p.ldc + n, o);
       }
   }
@@ -497,23 +526,68 @@ DRTC_DEVICE void w4_splitk_par(const W4Params& p, f32x4 (&acc)[8][8], int tile, 
   }
 }
 
-// Tile coordinates of tile-order index tt (row-grouped: group_m row tiles sweep the columns).
-DRTC_DEVICE void w4_tile_of(const W4Params& p, int tt, int& tm, int& tn) {
-  const int gsize = p.group_m * p.tiles_n;
-  const int first_m = (tt / gsize) * p.group_m;
-  const int gm = min(p.tiles_m - first_m, p.group_m);
+// Tile coordinates of tile-order index tt within a tiles_m x tiles_n grid (row-grouped:
+// group_m row tiles sweep the columns).
+DRTC_DEVICE void w4_tile_mn(int tiles_m, int tiles_n, int group_m, int tt, int& tm, int& tn) {
+  const int gsize = group_m * tiles_n;
+  const int first_m = (tt / gsize) * group_m;
+  const int gm = min(tiles_m - first_m, group_m);
   tm = first_m + (tt % gsize) % gm;
   tn = (tt % gsize) / gm;
 }
+DRTC_DEVICE void w4_tile_of(const W4Params& p, int tt, int& tm, int& tn) {
+  w4_tile_mn(p.tiles_m, p.tiles_n, p.group_m, tt, tm, tn);
+}
+
+// Tiles of the launch: tiles_m x tiles_n, or (grouped) the sum over the row groups.
+template <int V>
+DRTC_DEVICE int w4_ntiles(const W4Params& p) {
+  if constexpr ((V & 64) != 0) {
+    int n = 0;
+    for (int e = 0; e < p.n_grp; ++e) n += (p.grp[e + 1] - p.grp[e] + 255) >> 8;
+    return n * p.tiles_n;
+  } else {
+    return p.tiles_m * p.tiles_n;
+  }
+}
+
+// Position of tile-order index tt (grouped: the groups' tiles one after another, each group
+// in the row-grouped order of its own row tiles).
+template <int V>
+DRTC_DEVICE W4Pos w4_pos_of(const W4Params& p, int tt) {
+  W4Pos q;
+  if constexpr ((V & 64) != 0) {
+    int base = 0;
+    for (int e = 0; e < p.n_grp; ++e) {
+      const int r0 = p.grp[e], r1 = p.grp[e + 1];
+      const int tme = (r1 - r0 + 255) >> 8, nt = tme * p.tiles_n;
+      if (tt < base + nt) {
+        w4_tile_mn(tme, p.tiles_n, p.group_m, tt - base, q.tm, q.tn);
+        q.row0 = r0 + 256 * q.tm;
+        q.mend = r1;
+        q.b = p.b + (int64_t)e * p.b_grp;
+        return q;
+      }
+      base += nt;
+    }
+    q.tm = 0; q.tn = 0; q.row0 = 0; q.mend = 0; q.b = p.b;  // unreachable (tt < w4_ntiles)
+    return q;
+  } else {
+    w4_tile_of(p, tt, q.tm, q.tn);
+    return q;
+  }
+}
 
 // DMA plan of tile (tm, tn) for this wave (operand bases, per-lane source offsets).
-template <int EPI>
-DRTC_DEVICE void w4_plan(W4Dma& d, const W4Params& p, int tm, int tn, int wv, int lane,
+template <int EPI, int V>
+DRTC_DEVICE void w4_plan(W4Dma& d, const W4Params& p, const W4Pos& q, int wv, int lane,
                          int k_base, unsigned lds0) {
   const int r8 = lane >> 3;
+  const int tn = q.tn;
   const int chunk = (lane & 7) ^ ((4 * wv + (lane >> 4)) & 7);  // logical chunk of this lane
-  const int rows_a = min(256, p.M - 256 * tm);
-  const bf16_t* abase = p.a + (int64_t)(256 * tm) * p.lda + k_base;
+  const int row0 = w4_row0<V>(q);
+  const int rows_a = min(256, w4_mend<V>(p, q) - row0);
+  const bf16_t* abase = p.a + (int64_t)row0 * p.lda + k_base;
   d.na = (unsigned)(rows_a * p.lda * 2 - k_base * 2);
   d.ra = __builtin_amdgcn_make_buffer_rsrc((void*)abase, (short)0, (int)d.na, 0x00020000);
   // tile-independent lane offsets: rows past the tile's valid rows fall outside `na`
@@ -530,13 +604,13 @@ DRTC_DEVICE void w4_plan(W4Dma& d, const W4Params& p, int tm, int tn, int wv, in
   const bf16_t* bbase;
   int brow;
   if constexpr (w4_glu<EPI>()) {
-    bbase = p.b + (int64_t)(128 * tn) * p.ldb + k_base;
+    bbase = w4_bop<V>(p, q) + (int64_t)(128 * tn) * p.ldb + k_base;
     brow = 4 * wv + (r8 & 3) + (r8 >= 4 ? p.up_off : 0);
 #pragma unroll
     for (int s = 0; s < 8; ++s)
       d.sb[s] = (unsigned)((64 * (s >> 2) + 16 * (s & 3)) * p.ldb * 2);
   } else {
-    bbase = p.b + (int64_t)(256 * tn) * p.ldb + k_base;
+    bbase = w4_bop<V>(p, q) + (int64_t)(256 * tn) * p.ldb + k_base;
     brow = 8 * wv + r8;
 #pragma unroll
     for (int s = 0; s < 8; ++s) d.sb[s] = (unsigned)(32 * s * p.ldb * 2);
@@ -584,9 +658,14 @@ __global__ __launch_bounds__(kW4Threads, 1) void gemm_w4_kernel(W4Params p) {
     slice = xcd % p.splitk;
     tt = (xcd / p.splitk) * per + (orig >> 3);
   }
-  const int ntiles = p.tiles_m * p.tiles_n;
-  int tm, tn;
-  w4_tile_of(p, tt, tm, tn);
+  const int ntiles = w4_ntiles<V>(p);
+  if constexpr ((V & 64) != 0) {
+    // grouped: the grid is sized for the most tiles the rows can make (whole workgroups leave
+    // before any DMA when the groups' actual tiles are fewer)
+    if (tt >= ntiles) return;
+  }
+  W4Pos q = w4_pos_of<V>(p, tt);
+  const int tm = q.tm, tn = q.tn;
 
   const int lane = threadIdx.x & 63;
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -597,7 +676,7 @@ __global__ __launch_bounds__(kW4Threads, 1) void gemm_w4_kernel(W4Params p) {
   // ---- DMA plan
   W4Dma d;
   const unsigned lds0 = (unsigned)(uintptr_t)(w4_lds_ptr)w4_lds;
-  w4_plan<EPI>(d, p, tm, tn, wv, lane, k_base, lds0);
+  w4_plan<EPI, V>(d, p, q, wv, lane, k_base, lds0);
   // fragment read offsets (bytes within a stage): row 128 w + l16 (+ 16 per fragment), the
   // 16-B chunk 4 h + g stored at chunk ^ ((row >> 1) & 7)
   const int fx = (l16 >> 1) & 7;
@@ -655,10 +734,10 @@ __global__ __launch_bounds__(kW4Threads, 1) void gemm_w4_kernel(W4Params p) {
     for (;;) {
       const int tnext = tt + nwg;
       const bool more = tnext < ntiles;
-      int tm2 = tm, tn2 = tn;
-      if (more) w4_tile_of(p, tnext, tm2, tn2);
+      W4Pos q2 = q;
+      if (more) q2 = w4_pos_of<V>(p, tnext);
       W4Dma dn;
-      w4_plan<EPI>(dn, p, tm2, tn2, wv, lane, 0, lds0);
+      w4_plan<EPI, V>(dn, p, q2, wv, lane, 0, lds0);
       // K step t + 2 of this tile, or step t + 2 - nk of the next one; the very last tile
       // re-stages its final K tile (valid bytes, never read) as the plain form does.  Step 0
       // starts the accumulators from 0 (MFMA with a zero C operand: no separate zeroing of the
@@ -687,13 +766,13 @@ __global__ __launch_bounds__(kW4Threads, 1) void gemm_w4_kernel(W4Params p) {
       // spilled, and its reload's vmcnt(0) would wait for the next tile's DMA
       int ln;
       asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
-      w4_epilogue<EPI, V>(p, acc, tm, tn, wm, wn, ln & 15, ln >> 4, 0);
+      w4_epilogue<EPI, V>(p, acc, w4_row0<V>(q), w4_mend<V>(p, q), q.tn, wm, wn, ln & 15,
+                          ln >> 4, 0);
       if (!more) break;
-      seam = kSeamOk && 256 * tm + 256 <= p.M;
+      seam = kSeamOk && w4_row0<V>(q) + 256 <= w4_mend<V>(p, q);
       par ^= nk & 1;
       tt = tnext;
-      tm = tm2;
-      tn = tn2;
+      q = q2;
       d = dn;
     }
     return;
@@ -717,7 +796,7 @@ __global__ __launch_bounds__(kW4Threads, 1) void gemm_w4_kernel(W4Params p) {
     __syncthreads();
     if (!w4_splitk(p, acc, tm * p.tiles_n + tn, slice, w4_lds)) return;
   }
-  w4_epilogue<EPI, V>(p, acc, tm, tn, wm, wn, l16, g, slice);
+  w4_epilogue<EPI, V>(p, acc, 256 * tm, p.M, tn, wm, wn, l16, g, slice);
 }
 
 template <int EPI, int V>
@@ -745,6 +824,13 @@ int w4_launch(const W4Params& p, int v, hipStream_t st) {
     case 56: return w4_launch_v<EPI, 56>(p, st);
     default: return -1;
   }
+}
+
+// grouped persistent form (V & 64 on the default schedule 56): store and gated epilogues
+template <int EPI>
+int w4_launch_grouped(const W4Params& p, int nwg, hipStream_t st) {
+  hipLaunchKernelGGL((gemm_w4_kernel<EPI, 120>), dim3(nwg), dim3(kW4Threads), kW4Lds, st, p);
+  return (int)hipGetLastError();
 }
 
 template <int EPI, int V>
@@ -843,13 +929,59 @@ int launch_gemm_w4(void* c, const void* a, const void* b, const void* r, int M, 
   }
 }
 
+// Grouped persistent GEMM: for g < n_grp, C[r] = epi(A[r] . B_g^T) over the rows r in
+// [grp[g], grp[g + 1]) with B_g = b + g * b_grp elements (the experts of a MoE layer over
+// expert-ordered rows).  grp is a DEVICE array (n_grp + 1 non-decreasing row offsets, the last
+// <= max_rows): the routing kernel writes it and the launch reads it with no host sync, so the
+// layer stays hipGraph-capturable.  The grid is min(CUs, tiles of max_rows rows spread over
+// n_grp groups); workgroups past the actual tile count leave at once.
+int launch_gemm_w4_grouped(void* c, const void* a, const void* b, const int* grp, int n_grp,
+                           int max_rows, int N, int K, int lda, int ldb, int ldc, int64_t b_grp,
+                           int epi, int up_off, int group_m, hipStream_t st) {
+  const bool glu = epi == W4_SILU || epi == W4_GELU;
+  if (epi != W4_STORE && !glu) return -1;
+  if (grp == nullptr || n_grp < 1 || max_rows < 1 || K % 64 || K / 64 < 2) return -1;
+  if (glu ? (N % 128 || up_off != N) : (N % 256)) return -1;
+  if (lda % 8 || ldb % 8 || (glu ? ldc % 4 : ldc % 8)) return -1;
+  if ((uintptr_t)a % 16 || (uintptr_t)b % 16 || (uintptr_t)c % (glu ? 8 : 16)) return -1;
+  if ((int64_t)256 * lda * 2 >= (1ll << 31)) return -1;
+  if ((int64_t)(glu ? up_off + 128 : 256) * ldb * 2 >= (1ll << 31)) return -1;
+  W4Params p{};
+  p.c = (bf16_t*)c;
+  p.a = (const bf16_t*)a;
+  p.b = (const bf16_t*)b;
+  p.M = max_rows; p.N = N; p.K = K;
+  p.lda = lda; p.ldb = ldb; p.ldc = ldc;
+  p.tiles_m = (max_rows + 255) / 256;
+  p.tiles_n = glu ? N / 128 : N / 256;
+  p.splitk = 1;
+  p.kt_split = K / 64;
+  p.up_off = up_off;
+  p.group_m = group_m < 1 ? 8 : group_m;
+  p.krot = g_w4_krot;
+  p.grp = grp;
+  p.n_grp = n_grp;
+  p.b_grp = b_grp;
+  // the most row tiles n_grp groups of max_rows rows in total can make
+  const int64_t tiles = (int64_t)(p.tiles_m + n_grp - 1) * p.tiles_n;
+  int nwg = (int)(tiles < w4_num_cus() ? tiles : w4_num_cus());
+  nwg -= nwg & 7;  // whole XCD rounds (the per-XCD K rotation); surplus workgroups leave at once
+  if (nwg < 8) nwg = 8;
+  switch (epi) {
+    case W4_STORE: return w4_launch_grouped<W4_STORE>(p, nwg, st);
+    case W4_SILU: return w4_launch_grouped<W4_SILU>(p, nwg, st);
+    default: return w4_launch_grouped<W4_GELU>(p, nwg, st);
+  }
+}
+
 int64_t gemm_w4_workspace_bytes(int64_t M, int64_t N, int splitk) {
   // fp32 split-K slabs: 256 KiB per 256 x 256 tile and slice
   return splitk > 1 ? ((M + 255) / 256) * (N / 256) * splitk * 64ll * kW4Threads * 16 : 0;
 }
 
 int configure_gemm_w4() {
-  return w4_cfg<W4_STORE>() | w4_cfg<W4_RESIDUAL>() | w4_cfg<W4_SILU>() | w4_cfg<W4_GELU>();
+  return w4_cfg<W4_STORE>() | w4_cfg<W4_RESIDUAL>() | w4_cfg<W4_SILU>() | w4_cfg<W4_GELU>() |
+         w4_cfg_one<W4_STORE, 120>() | w4_cfg_one<W4_SILU, 120>() | w4_cfg_one<W4_GELU, 120>();
 }
 
 }  // namespace drtc

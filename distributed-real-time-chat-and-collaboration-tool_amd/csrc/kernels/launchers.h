@@ -53,7 +53,9 @@ int launch_sample(int* out_tokens, const void* logits, int B, int V, int ld,
 
 // variant 0 / 1 / 2: the moe.hip grouped GEMMs; 3: gemm_xd grouped mode with xd forms gu_form
 // (gated gate_up) / dn_form (down), 0 = by rows per expert; slab / counters: the split-K
-// workspace of the gemm_xd forms (may be null: no split-K); -1: by rows per expert
+// workspace of the gemm_xd forms (may be null: no split-K); 4: rows gathered into expert order,
+// then gemm_w4's grouped persistent form (prefill-sized rows per expert); -1: by rows per
+// expert
 int launch_moe(void* out, const void* x, const void* router_logits, const void* w_gu,
                const void* w_dn, int T, int H, int I, int E, int k, int e_off, int e_local,
                int act, void* workspace, int64_t ws_bytes, int variant, int gu_form, int dn_form,
@@ -123,6 +125,12 @@ int launch_gemm_w4(void* c, const void* a, const void* b, const void* r, int M, 
                    int lda, int ldb, int ldc, int ldr, int epi, int up_off, int splitk,
                    int group_m, void* slab, int64_t slab_bytes, int* counters, int n_counters,
                    int v, hipStream_t st);
+// Grouped persistent form: rows [grp[g], grp[g + 1]) of a / c (grp: n_grp + 1 row offsets in
+// DEVICE memory) times weight b + g * b_grp; epi 0 store or 2/3 gated; max_rows >= grp[n_grp]
+// sizes the grid.
+int launch_gemm_w4_grouped(void* c, const void* a, const void* b, const int* grp, int n_grp,
+                           int max_rows, int N, int K, int lda, int ldb, int ldc, int64_t b_grp,
+                           int epi, int up_off, int group_m, hipStream_t st);
 int64_t gemm_w4_workspace_bytes(int64_t M, int64_t N, int splitk);
 int configure_gemm_w4();
 

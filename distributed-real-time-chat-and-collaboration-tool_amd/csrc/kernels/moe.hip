@@ -26,6 +26,7 @@ namespace drtc {
 
 constexpr int kMoeBM = 128;   // rows per tile
 constexpr int kMoeMaxK = 8;   // top-k bound
+constexpr int kMoeW4Rows = 1024;  // auto variant 4 from this many rows per expert
 
 // ---------------------------------------------------------------- align
 __global__ __launch_bounds__(1024) void moe_align_kernel(
@@ -34,7 +35,7 @@ __global__ __launch_bounds__(1024) void moe_align_kernel(
     int* __restrict__ inv_pos, float* __restrict__ topk_w,
     int* __restrict__ tile_expert, int* __restrict__ tile_row0, int* __restrict__ tile_rows,
     int* __restrict__ n_tiles, int* __restrict__ local_range, int max_tiles, int e_off,
-    int e_local, int bm, int lts, int les) {
+    int e_local, int bm, int lts, int les, int* __restrict__ grp_off) {
   __shared__ int cnt[256], off[257], fill[256], toff[257];
   const int tid = threadIdx.x;
   for (int e = tid; e < 256; e += 1024) { cnt[e] = 0; fill[e] = 0; }
@@ -90,6 +91,8 @@ __global__ __launch_bounds__(1024) void moe_align_kernel(
     local_range[1] = off[e_off + e_local];
   }
   __syncthreads();
+  // variant 4: this rank's expert row groups in the sorted order (absolute positions)
+  if (grp_off != nullptr && tid <= e_local) grp_off[tid] = off[e_off + tid];
   for (int e = tid; e < E; e += 1024) {
     const int nt = toff[e + 1] - toff[e];
     for (int i = 0; i < nt; ++i) {
@@ -406,6 +409,21 @@ __global__ __launch_bounds__(PipeCfg<BM>::NT, 1) void moe_gemm_pipe_kernel(
     }
 }
 
+// Variant 4: the pairs' token rows copied into expert order, xs[p] = x[sorted_tok[p]] for this
+// rank's positions (16 B per lane; a row of H bf16 per workgroup pass).
+__global__ __launch_bounds__(256) void moe_gather_kernel(bf16_t* __restrict__ xs,
+                                                         const bf16_t* __restrict__ x,
+                                                         const int* __restrict__ sorted_tok,
+                                                         const int* __restrict__ local_range,
+                                                         int P, int H) {
+  const int lo = local_range[0], hi = local_range[1];
+  for (int p = lo + blockIdx.x; p < hi; p += gridDim.x) {
+    const bf16_t* src = x + (int64_t)sorted_tok[p] * H;
+    bf16_t* dst = xs + (int64_t)p * H;
+    for (int c = threadIdx.x * 8; c < H; c += 256 * 8) store_bf16x8(dst + c, load_bf16x8(src + c));
+  }
+}
+
 __global__ __launch_bounds__(256) void moe_combine_kernel(
     bf16_t* __restrict__ out, const bf16_t* __restrict__ zbuf, const float* __restrict__ topk_w,
     const int* __restrict__ inv_pos, const int* __restrict__ local_range, int T, int H, int k) {
@@ -462,8 +480,18 @@ int launch_moe(void* out, const void* x, const void* router_logits, const void* 
   // -1 = pick by rows per expert (scripts/moe_bench.py, Mixtral shapes)
   const int rows_e = P / e_local;
   const bool auto_v = variant < 0;
-  if (auto_v) variant = rows_e >= 96 ? 3 : 1;
-  if (variant > 3) return -1;
+  // variant 4 from ~1k rows per expert (Mixtral prefill chunks: gemm_w4's persistent 256 x 256
+  // tiles over expert-ordered rows, profiles/r6j), gemm_xd's grouped forms from ~a 96-row tile
+  if (auto_v) variant = rows_e >= kMoeW4Rows ? 4 : (rows_e >= 96 ? 3 : 1);
+  if (variant > 4) return -1;
+  // variant 4: the persistent GEMM's prologue stages two K tiles; the down reduction is I
+  if (variant == 4 && (H / 64 < 2 || I % 128 || I / 64 < 2 || H % 256)) {
+    if (!auto_v) return -1;
+    variant = 3;
+  }
+  // variant 4 with dn_form: down on a 256-row gemm_xd grouped form (the tile table's rows)
+  if (variant == 4 && dn_form && ((dn_form % 1000) / 100 != 2 || !moe_xd_ok(dn_form, H, I, false)))
+    return -1;
   if (variant == 3) {
     // 256-row tiles from ~1.5 tiles of rows per expert, else 128-row; 256 gated columns
     // (128 outputs) for gate_up where I allows; down with split-K 2 while the grid is below
@@ -499,7 +527,8 @@ int launch_moe(void* out, const void* x, const void* router_logits, const void* 
       variant = rows_e >= 96 ? 2 : 1;  // shapes the grouped gemm_xd forms do not take
     }
   }
-  const int bm = variant == 3 ? 128 * ((gu_form % 1000) / 100) : (variant == 2 ? 256 : 128);
+  const int bm = variant == 3 ? 128 * ((gu_form % 1000) / 100)
+                              : (variant == 2 || variant == 4 ? 256 : 128);
   const int max_tiles = (P + bm - 1) / bm + e_local;
   // workspace carve (all 256-B aligned)
   auto align = [](int64_t v) { return (v + 255) & ~int64_t(255); };
@@ -516,12 +545,35 @@ int launch_moe(void* out, const void* x, const void* router_logits, const void* 
   int* local_range = (int*)(p + o); o = align(o + 8);
   bf16_t* hbuf = (bf16_t*)(p + o); o = align(o + 2ll * P * I);
   bf16_t* zbuf = (bf16_t*)(p + o); o = align(o + 2ll * P * H);
+  int* grp_off = (int*)(p + o); o = align(o + 4ll * (e_local + 1));
   if (o > ws_bytes) return -2;
   hipLaunchKernelGGL(moe_align_kernel, dim3(1), dim3(1024), 0, st, (const bf16_t*)router_logits, T,
                      E, k, sorted_tok, sorted_w, inv_pos, topk_w, t_e, t_r0, t_n, n_tiles, local_range,
-                     max_tiles, e_off, e_local, bm, logit_ts, logit_es);
+                     max_tiles, e_off, e_local, bm, logit_ts, logit_es,
+                     variant == 4 ? grp_off : (int*)nullptr);
   const dim3 g_gu((I / 64) * max_tiles), g_dn((H / 128) * max_tiles);
-  if (variant == 3) {
+  if (variant == 4) {
+    // xs (expert-ordered token rows) lives in zbuf: gate_up consumes it before down writes Z
+    bf16_t* xs = zbuf;
+    hipLaunchKernelGGL(moe_gather_kernel, dim3(min(P, 8192)), dim3(256), 0, st, xs,
+                       (const bf16_t*)x, sorted_tok, local_range, P, H);
+    int e = launch_gemm_w4_grouped(hbuf, xs, w_gu, grp_off, e_local, P, I, H, H, H, I,
+                                   2ll * I * H, 2 + act, I, 4, st);
+    if (e) return e;
+    if (dn_form) {
+      // down on gemm_xd's grouped split-K forms over the 256-row tile table (few rows per
+      // expert: the persistent 256 x 256 down has H / 256 column tiles per expert only)
+      int mt, nf, sk;
+      moe_xd_form(dn_form, mt, nf, sk);
+      e = launch_gemm_xd_grouped(zbuf, hbuf, w_dn, P, H, I, I, I, H, 0, mt, nf, sk, max_tiles,
+                                 t_r0, t_n, t_e, n_tiles, nullptr, (int64_t)H * I, slab,
+                                 slab_bytes, counters, n_counters, st);
+    } else {
+      e = launch_gemm_w4_grouped(zbuf, hbuf, w_dn, grp_off, e_local, P, H, I, I, I, H,
+                                 (int64_t)H * I, 0, 0, 8, st);
+    }
+    if (e) return e;
+  } else if (variant == 3) {
     int mt, nf, sk, e;
     moe_xd_form(gu_form, mt, nf, sk);
     e = launch_gemm_xd_grouped(hbuf, x, w_gu, T, I, H, H, H, I, 2 + act, mt, nf, sk, max_tiles,
@@ -579,8 +631,9 @@ int64_t moe_workspace_bytes(int T, int H, int I, int e_local, int k) {
   auto align = [](int64_t v) { return (v + 255) & ~int64_t(255); };
   const int64_t P = (int64_t)T * k;
   const int64_t mt = (P + kMoeBM - 1) / kMoeBM + e_local;
+  // (tile tables sized for the 128-row tiles: the largest count of any variant)
   return 4 * align(4 * P) + 3 * align(4 * mt) + align(4) + align(8) + align(2 * P * I) +
-         align(2 * P * H);
+         align(2 * P * H) + align(4 * (e_local + 1));
 }
 
 }  // namespace drtc

@@ -604,6 +604,31 @@ def mfma_gemm(x: torch.Tensor, w: torch.Tensor, epi: str = "store",
     return out
 
 
+def mfma_gemm_grouped(x: torch.Tensor, w: torch.Tensor, grp: torch.Tensor, epi: str = "store",
+                      out: torch.Tensor | None = None, group_m: int = 0) -> torch.Tensor:
+    """Grouped persistent gemm_w4 (csrc/kernels/gemm_w4.hip, V & 64): for every group g,
+    out[r] = epi(x[r] @ w[g].T) over the rows r in [grp[g], grp[g + 1]).
+
+    x [R, K] bf16 (rows in group order); w [G, N, K] ("silu" / "gelu_tanh": [G, 2I, K] with
+    the gate rows first); grp int32 [G + 1] on the device, non-decreasing, grp[G] <= R -
+    read by the kernel, never by the host (a routing kernel writes it: no sync, graph-safe).
+    Rows outside [grp[0], grp[G]) of ``out`` are not written."""
+    R, K = x.shape
+    G_, n2, k2 = w.shape
+    glu = epi in ("silu", "gelu_tanh")
+    N = n2 // 2 if glu else n2
+    assert k2 == K and w.is_contiguous() and x.stride(1) == 1 and x.dtype == torch.bfloat16
+    assert grp.dtype == torch.int32 and grp.numel() == G_ + 1 and grp.device == x.device
+    if out is None:
+        out = torch.empty((R, N), dtype=x.dtype, device=x.device)
+    assert out.shape == (R, N) and out.stride(1) == 1
+    check(hipk().gemm_grouped(out.data_ptr(), x.data_ptr(), w.data_ptr(), grp.data_ptr(), G_,
+                              R, N, K, x.stride(0), K, out.stride(0), n2 * K, EPI[epi],
+                              N if glu else 0, group_m or (4 if glu else 8), stream_ptr(x)),
+          "gemm_grouped")
+    return out
+
+
 def tune(M: int, N: int, K: int, device, iters: int = 20, max_candidates: int = 12) -> dict:
     """Measure every hipBLASLt solution for y[M,N] = x[M,K] @ W[N,K]^T on random operands;
     returns {"algo", "us", "heuristic_us", "candidates"}."""
@@ -917,6 +942,7 @@ def midm_gemm(x: torch.Tensor, w: torch.Tensor, epi: str = "store",
 __all__ = ["linear", "route", "norm_linear", "glu_linear", "norm_glu", "fused_glu_ok",
            "linear_residual",
            "residual_fusable", "w4_glu_ok", "w4_ok", "w4_shape_ok", "w4_group_m", "mfma_gemm",
+           "mfma_gemm_grouped",
            "gemm_workspace", "new_gemm_workspace", "private_workspace", "check_splitk_fault", "SplitKFault", "SplitKWatch",
            "set_splitk_spin_limit", "skinny_linear", "skinny_ok",
            "skinny_variant", "skinny_supports", "midm_gemm", "midm_supported", "midm_splits",

@@ -23,12 +23,14 @@ from .activation import ACTS, act_glu_ref
 
 # Largest token chunk per kernel call: bounds the workspace (P = chunk * k
 # rows of [I] and [H] intermediates) while keeping >10k workgroups per GEMM.
-MOE_CHUNK = 8192
+MOE_CHUNK = int(os.environ.get("DRTC_MOE_CHUNK", "8192"))
 
 # Grouped-GEMM structure (csrc/kernels/moe.hip): 0 = 128-row two-barrier,
 # 1 = 128-row 3-stage pipeline, 2 = 256-row 3-stage pipeline, 3 = gemm_xd's grouped mode
 # (csrc/kernels/gemm_xd.hip: XCD-partitioned tiles, GLU epilogue, split-K, non-temporal
-# weights where an expert's rows fit one tile), -1 = by rows per expert.
+# weights where an expert's rows fit one tile), 4 = token rows gathered into expert order, then
+# gemm_w4's grouped persistent 256 x 256 form (csrc/kernels/gemm_w4.hip; prefill-sized rows per
+# expert), -1 = by rows per expert (4 from 1024 rows per expert, 3 from 96).
 MOE_GEMM_VARIANT = int(os.environ.get("DRTC_MOE_VARIANT", "-1"))
 # gemm_xd forms of variant 3 (mt * 100 + nf * 10 + splitk, + 1000 non-temporal; 0 = by rows
 # per expert, csrc/kernels/moe.hip launch_moe)

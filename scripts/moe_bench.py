@@ -40,7 +40,7 @@ def main():
         lg = torch.randn(T, E, device=dev, generator=g).to(torch.bfloat16)
         out = torch.empty_like(x)
         t_v = []
-        for v in (0, 1, 2, 3):
+        for v in (0, 1, 2, 3, 4):
             t_v.append(timeit(lambda: ops.fused_moe(x, lg, wgu, wdn, k, workspace=ws, out=out,
                                                     variant=v)))
         # variant 3 with explicit gemm_xd forms (gate_up / down)
@@ -49,6 +49,13 @@ def main():
             try:
                 forms[f"{gu}/{dn}"] = timeit(lambda: ops.fused_moe(
                     x, lg, wgu, wdn, k, workspace=ws, out=out, variant=3, gu_form=gu, dn_form=dn))
+            except RuntimeError:
+                pass
+        # variant 4 (gemm_w4 grouped gate_up) with down on a 256-row gemm_xd grouped form
+        for dn in (282, 1282, 281, 242):
+            try:
+                forms[f"v4/{dn}"] = timeit(lambda: ops.fused_moe(
+                    x, lg, wgu, wdn, k, workspace=ws, out=out, variant=4, dn_form=dn))
             except RuntimeError:
                 pass
         t_f = timeit(lambda: ops.fused_moe(x, lg, wgu, wdn, k, workspace=ws, out=out))

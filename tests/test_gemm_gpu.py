@@ -555,3 +555,54 @@ def test_hbm_budget_too_small_for_one_sequence_is_an_error(hipk):
         LLMEngine(m, max_batch=8, max_model_len=4096, hbm_budget=0.01, use_graphs=False)
     eng = LLMEngine(m, max_batch=8, max_model_len=4096, hbm_budget=0.2, use_graphs=False)
     assert eng.kv.num_blocks >= eng.max_blocks
+
+
+@pytest.mark.parametrize("epi", ["store", "silu", "gelu_tanh"])
+@pytest.mark.parametrize("sizes,N,K,r0", [
+    ((300, 0, 700, 256, 1), 512, 256, 7),   # an empty group, row tails, a one-row group
+    ((1024, 1024, 513), 1024, 1024, 0),
+    ((5,), 256, 128, 3),                    # one partial tile: surplus workgroups leave at once
+    ((2048, 1900, 2100, 2000, 1990, 2010, 2080, 1970), 256, 512, 0),  # MoE-like, 8 experts
+])
+def test_w4_grouped_matches_fp32(hipk, epi, sizes, N, K, r0):
+    """gemm_w4's grouped persistent form (the MoE prefill GEMM): every row group times its own
+    weight, device-side row offsets, rows outside the groups untouched."""
+    glu = epi != "store"
+    G_ = len(sizes)
+    g = torch.Generator(device="cuda").manual_seed(sum(sizes) + N)
+    offs = [r0]
+    for s in sizes:
+        offs.append(offs[-1] + s)
+    R = offs[-1] + 5
+    x = torch.randn(R, K, device="cuda", dtype=torch.bfloat16, generator=g)
+    w = torch.randn(G_, 2 * N if glu else N, K, device="cuda", dtype=torch.bfloat16,
+                    generator=g) * 0.05
+    grp = torch.tensor(offs, dtype=torch.int32, device="cuda")
+    out = torch.full((R, N), 7.0, device="cuda", dtype=torch.bfloat16)
+    G.mfma_gemm_grouped(x, w, grp, epi, out=out)
+    for e in range(G_):
+        a, b = offs[e], offs[e + 1]
+        if b > a:
+            _check(out[a:b], _ref(x[a:b], w[e], epi, None))
+    assert bool((out[:r0] == 7).all()) and bool((out[offs[-1]:] == 7).all())
+
+
+def test_w4_grouped_graph_replay_follows_device_offsets(hipk):
+    """The group offsets are read on the device at run time: a captured launch replays with
+    new offsets written into the same tensor (no host sync, no re-capture)."""
+    g = torch.Generator(device="cuda").manual_seed(3)
+    R, N, K = 1500, 512, 256
+    x = torch.randn(R, K, device="cuda", dtype=torch.bfloat16, generator=g)
+    w = torch.randn(3, N, K, device="cuda", dtype=torch.bfloat16, generator=g) * 0.05
+    grp = torch.tensor([0, 500, 1000, 1500], dtype=torch.int32, device="cuda")
+    out = torch.zeros(R, N, device="cuda", dtype=torch.bfloat16)
+    G.mfma_gemm_grouped(x, w, grp, "store", out=out)
+    torch.cuda.synchronize()
+    gr = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(gr):
+        G.mfma_gemm_grouped(x, w, grp, "store", out=out)
+    grp.copy_(torch.tensor([0, 100, 1400, 1500], dtype=torch.int32))
+    gr.replay()
+    torch.cuda.synchronize()
+    for e, (a, b) in enumerate([(0, 100), (100, 1400), (1400, 1500)]):
+        _check(out[a:b], _ref(x[a:b], w[e], "store", None))

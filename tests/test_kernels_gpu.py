@@ -582,6 +582,61 @@ def test_fused_moe_grouped_xd_forms(hipk, T, H, I, E, k, gu, dn, act):
     G.check_splitk_fault()
 
 
+@pytest.mark.parametrize("T,H,I,E,k,e_off,e_local", [
+    (4096, 1024, 512, 8, 2, 0, 8),       # ~1k rows per expert: the auto pick
+    (3000, 512, 384, 4, 2, 0, 4),        # row tails in every expert
+    (2500, 512, 256, 8, 2, 2, 3),        # expert-parallel slice (rows of other ranks skipped)
+    (700, 256, 128, 16, 4, 0, 16),       # small groups, empty experts likely
+])
+@pytest.mark.parametrize("act", ["silu", "gelu_tanh"])
+def test_fused_moe_dense_grouped_variant(hipk, T, H, I, E, k, e_off, e_local, act):
+    """MoE variant 4 (prefill): token rows gathered into expert order, then gemm_w4's grouped
+    persistent GEMMs over device-side expert row offsets, then the fixed-order combine -
+    against the fp32 reference, and hipGraph replay on new inputs."""
+    from drtc_amd.ops import moe as moe_ops
+
+    x, lg, wgu, wdn = _moe_inputs(T, H, I, E, seed=T + H)
+    wgu, wdn = wgu[e_off:e_off + e_local].contiguous(), wdn[e_off:e_off + e_local].contiguous()
+    y = ops.fused_moe(x, lg, wgu, wdn, k, act, num_experts=E, e_off=e_off, variant=4)
+    yr = ops.fused_moe_ref(x, lg, wgu, wdn, k, act, e_off=e_off)
+    _close(y, yr, 3e-2, 3e-2, "moe variant 4")
+    if e_off == 0 and e_local == E and T * k // E >= 1024:  # the auto pick at this size
+        assert torch.equal(ops.fused_moe(x, lg, wgu, wdn, k, act), y)
+    ws = moe_ops.make_workspace(T, H, I, e_local, k, DEV)
+    xs, ls = x.clone(), lg.clone()
+    out = torch.empty_like(xs)
+    ops.fused_moe(xs, ls, wgu, wdn, k, act, num_experts=E, e_off=e_off, workspace=ws, out=out,
+                  variant=4)
+    torch.cuda.synchronize()
+    gr = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(gr):
+        ops.fused_moe(xs, ls, wgu, wdn, k, act, num_experts=E, e_off=e_off, workspace=ws,
+                      out=out, variant=4)
+    x2, lg2, _, _ = _moe_inputs(T, H, I, E, seed=T + H + 1)
+    xs.copy_(x2)
+    ls.copy_(lg2)
+    gr.replay()
+    torch.cuda.synchronize()
+    _close(out, ops.fused_moe_ref(x2, lg2, wgu, wdn, k, act, e_off=e_off), 3e-2, 3e-2,
+           "moe variant 4 graph")
+
+
+@pytest.mark.parametrize("T,H,I,E,k,dn", [(1024, 1024, 512, 8, 2, 282), (600, 512, 384, 8, 2, 1282),
+                                           (900, 512, 512, 4, 2, 242)])
+def test_fused_moe_w4_gate_up_xd_down(hipk, T, H, I, E, k, dn):
+    """MoE variant 4 with dn_form: gemm_w4 grouped gate_up over expert-ordered rows, down on a
+    256-row gemm_xd grouped (split-K) form over the same routing's tile table."""
+    from drtc_amd.ops import gemm as G
+
+    G.gemm_workspace(torch.device(DEV))
+    x, lg, wgu, wdn = _moe_inputs(T, H, I, E, seed=T + dn)
+    y = ops.fused_moe(x, lg, wgu, wdn, k, variant=4, dn_form=dn)
+    _close(y, ops.fused_moe_ref(x, lg, wgu, wdn, k), 3e-2, 3e-2, f"moe v4/{dn}")
+    G.check_splitk_fault()
+    with pytest.raises(RuntimeError):
+        ops.fused_moe(x, lg, wgu, wdn, k, variant=4, dn_form=142)  # 128-row form: other table
+
+
 def test_fused_moe_expert_parallel_slices_sum(hipk):
     """EP: per-rank contributions (expert slices) sum to the full layer."""
     T, H, I, E, k = 200, 256, 128, 8, 2
