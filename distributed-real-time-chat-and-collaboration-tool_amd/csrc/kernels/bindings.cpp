@@ -44,6 +44,7 @@ PYBIND11_MODULE(_hipk, m) {
   m.def("set_rope_variant", [](int v) { drtc::set_rope_variant(v); });
   m.def("w4_set_krot", [](int k) { drtc::w4_set_krot(k); });
   m.def("w4_krot", []() { return drtc::w4_krot(); });
+  m.def("w4_set_grouped_rot", [](int r) { drtc::w4_set_grouped_rot(r); });
   m.def("kv_write_v", [](u64 v_cache, u64 qkv, int qkv_stride, u64 seg_tok, u64 seg_len,
                          u64 seg_blk, int nseg, int Hq, int Hkv, int D, int block_size,
                          u64 st) {
@@ -108,10 +109,10 @@ PYBIND11_MODULE(_hipk, m) {
   // row offsets
   m.def("gemm_grouped", [](u64 c, u64 a, u64 b, u64 grp, int n_grp, int max_rows, int N, int K,
                            int lda, int ldb, int ldc, int64_t b_grp, int epi, int up_off,
-                           int group_m, u64 st) {
+                           int group_m, int ksplit, int64_t c_split, u64 st) {
     return drtc::launch_gemm_w4_grouped(P<void>(c), P<const void>(a), P<const void>(b),
                                         P<const int>(grp), n_grp, max_rows, N, K, lda, ldb, ldc,
-                                        b_grp, epi, up_off, group_m, S(st));
+                                        b_grp, epi, up_off, group_m, ksplit, c_split, S(st));
   });
   // gemm_xd (ops.gemm.xd_gemm): decode-shaped tiles, XCD-partitioned order, split-K 1..8
   m.def("gemm_xd", [](u64 c, u64 a, u64 b, u64 r, int M, int N, int K, int lda, int ldb, int ldc,

@@ -83,9 +83,13 @@ struct W4Params {
   // [grp[g], grp[g + 1]) (device array, written by the producing kernel: no host sync), each
   // multiplied by its own B at b + g * b_grp.  tiles_m is unused (the tile count is derived on
   // the device); M bounds the rows the launcher sized the grid for.
+  // ksplit > 1: every group's K is cut into ksplit slices (kt_split K tiles each), slice s
+  // written to c + s * c_split (bf16 partial products, summed by the consumer)
   const int* grp;
   int n_grp;
   int64_t b_grp;
+  int ksplit;
+  int64_t c_split;
 };
 
 // Position of one output tile: row tile tm, column tile tn; grouped form: rows [row0,
@@ -96,6 +100,8 @@ struct W4Pos {
   int tm, tn;
   int row0, mend;
   const bf16_t* b;
+  int koff;  // grouped split-K: K element offset of the slice
+  bf16_t* c;  // grouped split-K: the slice's output
 };
 template <int V>
 DRTC_DEVICE int w4_row0(const W4Pos& q) {
@@ -108,6 +114,14 @@ DRTC_DEVICE int w4_mend(const W4Params& p, const W4Pos& q) {
 template <int V>
 DRTC_DEVICE const bf16_t* w4_bop(const W4Params& p, const W4Pos& q) {
   if constexpr ((V & 64) != 0) return q.b; else return p.b;
+}
+template <int V>
+DRTC_DEVICE int w4_koff(const W4Pos& q) {
+  if constexpr ((V & 64) != 0) return q.koff; else return 0;
+}
+template <int V>
+DRTC_DEVICE bf16_t* w4_cop(const W4Params& p, const W4Pos& q) {
+  if constexpr ((V & 64) != 0) return q.c; else return p.c;
 }
 
 template <int EPI>
@@ -313,15 +327,15 @@ DRTC_DEVICE void w4_st8(bf16_t* p, bf16x4 v) {
 }
 
 template <int EPI, int V>
-DRTC_DEVICE void w4_epilogue(const W4Params& p, f32x4 (&acc)[8][8], int row0, int mend, int tn,
-                             int wm, int wn, int l16, int g, int slice) {
+DRTC_DEVICE void w4_epilogue(const W4Params& p, bf16_t* cbase, f32x4 (&acc)[8][8], int row0,
+                             int mend, int tn, int wm, int wn, int l16, int g, int slice) {
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int m = row0 + 128 * wm + 16 * i + 4 * g + r;
       if (m >= mend) continue;
-      bf16_t* crow = p.c + (int64_t)m * p.ldc;
+      bf16_t* crow = cbase + (int64_t)m * p.ldc;
       if constexpr (w4_glu<EPI>()) {
         const int n = 128 * tn + 64 * wn + 4 * l16;
         bf16x4 o;
@@ -360,7 +374,7 @@ DRTC_DEVICE void w4_epilogue(const W4Params& p, f32x4 (&acc)[8][8], int row0, in
 #pragma unroll
         for (int j = 0; j < 8; ++j) o[j] = f2bf(acc[i][j][r] + bf2f(rv[i][r][j]));
         if (m >= mend) continue;
-        w4_st16<V>(p.c + (int64_t)m * p.ldc + n, o);
+        w4_st16<V>(cbase + (int64_t)m * p.ldc + n, o);
       }
   }
 }
@@ -545,7 +559,7 @@ DRTC_DEVICE int w4_ntiles(const W4Params& p) {
   if constexpr ((V & 64) != 0) {
     int n = 0;
     for (int e = 0; e < p.n_grp; ++e) n += (p.grp[e + 1] - p.grp[e] + 255) >> 8;
-    return n * p.tiles_n;
+    return n * p.tiles_n * p.ksplit;
   } else {
     return p.tiles_m * p.tiles_n;
   }
@@ -560,17 +574,21 @@ DRTC_DEVICE W4Pos w4_pos_of(const W4Params& p, int tt) {
     int base = 0;
     for (int e = 0; e < p.n_grp; ++e) {
       const int r0 = p.grp[e], r1 = p.grp[e + 1];
-      const int tme = (r1 - r0 + 255) >> 8, nt = tme * p.tiles_n;
+      const int tme = (r1 - r0 + 255) >> 8, ns = tme * p.tiles_n, nt = ns * p.ksplit;
       if (tt < base + nt) {
-        w4_tile_mn(tme, p.tiles_n, p.group_m, tt - base, q.tm, q.tn);
+        const int s = (tt - base) / ns;  // K slice
+        w4_tile_mn(tme, p.tiles_n, p.group_m, tt - base - s * ns, q.tm, q.tn);
         q.row0 = r0 + 256 * q.tm;
         q.mend = r1;
         q.b = p.b + (int64_t)e * p.b_grp;
+        q.koff = s * p.kt_split * 64;
+        q.c = p.c + (int64_t)s * p.c_split;
         return q;
       }
       base += nt;
     }
     q.tm = 0; q.tn = 0; q.row0 = 0; q.mend = 0; q.b = p.b;  // unreachable (tt < w4_ntiles)
+    q.koff = 0; q.c = p.c;
     return q;
   } else {
     w4_tile_of(p, tt, q.tm, q.tn);
@@ -581,7 +599,8 @@ DRTC_DEVICE W4Pos w4_pos_of(const W4Params& p, int tt) {
 // DMA plan of tile (tm, tn) for this wave (operand bases, per-lane source offsets).
 template <int EPI, int V>
 DRTC_DEVICE void w4_plan(W4Dma& d, const W4Params& p, const W4Pos& q, int wv, int lane,
-                         int k_base, unsigned lds0) {
+                         int k_base0, unsigned lds0) {
+  const int k_base = k_base0 + w4_koff<V>(q);
   const int r8 = lane >> 3;
   const int tn = q.tn;
   const int chunk = (lane & 7) ^ ((4 * wv + (lane >> 4)) & 7);  // logical chunk of this lane
@@ -766,8 +785,8 @@ __global__ __launch_bounds__(kW4Threads, 1) void gemm_w4_kernel(W4Params p) {
       // spilled, and its reload's vmcnt(0) would wait for the next tile's DMA
       int ln;
       asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(ln));
-      w4_epilogue<EPI, V>(p, acc, w4_row0<V>(q), w4_mend<V>(p, q), q.tn, wm, wn, ln & 15,
-                          ln >> 4, 0);
+      w4_epilogue<EPI, V>(p, w4_cop<V>(p, q), acc, w4_row0<V>(q), w4_mend<V>(p, q), q.tn, wm, wn,
+                          ln & 15, ln >> 4, 0);
       if (!more) break;
       seam = kSeamOk && w4_row0<V>(q) + 256 <= w4_mend<V>(p, q);
       par ^= nk & 1;
@@ -796,7 +815,7 @@ __global__ __launch_bounds__(kW4Threads, 1) void gemm_w4_kernel(W4Params p) {
     __syncthreads();
     if (!w4_splitk(p, acc, tm * p.tiles_n + tn, slice, w4_lds)) return;
   }
-  w4_epilogue<EPI, V>(p, acc, 256 * tm, p.M, tn, wm, wn, l16, g, slice);
+  w4_epilogue<EPI, V>(p, p.c, acc, 256 * tm, p.M, tn, wm, wn, l16, g, slice);
 }
 
 template <int EPI, int V>
@@ -826,10 +845,19 @@ int w4_launch(const W4Params& p, int v, hipStream_t st) {
   }
 }
 
-// grouped persistent form (V & 64 on the default schedule 56): store and gated epilogues
+// grouped persistent form (V & 64 on schedule 40: spread fragment reads, NO per-XCD K
+// rotation): store and gated epilogues.  The routing kernel places a pair's row within its
+// expert's group by an atomic ticket, so a row's tile - and with the rotation its workgroup's
+// K start - would vary run to run; without it every tile sums K in the same order and the
+// layer is deterministic.
+// (w4_set_grouped_rot(1): schedule 56 + 64, with the rotation - an A/B arm, not deterministic)
+static int g_w4_grouped_rot = 0;
 template <int EPI>
 int w4_launch_grouped(const W4Params& p, int nwg, hipStream_t st) {
-  hipLaunchKernelGGL((gemm_w4_kernel<EPI, 120>), dim3(nwg), dim3(kW4Threads), kW4Lds, st, p);
+  if (g_w4_grouped_rot)
+    hipLaunchKernelGGL((gemm_w4_kernel<EPI, 120>), dim3(nwg), dim3(kW4Threads), kW4Lds, st, p);
+  else
+    hipLaunchKernelGGL((gemm_w4_kernel<EPI, 104>), dim3(nwg), dim3(kW4Threads), kW4Lds, st, p);
   return (int)hipGetLastError();
 }
 
@@ -848,6 +876,7 @@ int w4_cfg() {
 }  // namespace
 
 static int g_w4_krot = 8;
+void w4_set_grouped_rot(int r) { g_w4_grouped_rot = r != 0; }
 void w4_set_krot(int k) { g_w4_krot = (k == 1 || k == 2 || k == 4) ? k : 8; }
 int w4_krot() { return g_w4_krot; }
 
@@ -937,10 +966,15 @@ int launch_gemm_w4(void* c, const void* a, const void* b, const void* r, int M, 
 // n_grp groups); workgroups past the actual tile count leave at once.
 int launch_gemm_w4_grouped(void* c, const void* a, const void* b, const int* grp, int n_grp,
                            int max_rows, int N, int K, int lda, int ldb, int ldc, int64_t b_grp,
-                           int epi, int up_off, int group_m, hipStream_t st) {
+                           int epi, int up_off, int group_m, int ksplit, int64_t c_split,
+                           hipStream_t st) {
   const bool glu = epi == W4_SILU || epi == W4_GELU;
   if (epi != W4_STORE && !glu) return -1;
-  if (grp == nullptr || n_grp < 1 || max_rows < 1 || K % 64 || K / 64 < 2) return -1;
+  if (ksplit < 1 || (glu && ksplit != 1)) return -1;  // a gated epilogue cannot be split
+  if (grp == nullptr || n_grp < 1 || max_rows < 1 || K % 64 || (K / 64) % ksplit ||
+      K / 64 / ksplit < 2)
+    return -1;
+  if (ksplit > 1 && (c_split % 8 || (int64_t)max_rows * ldc > c_split)) return -1;
   if (glu ? (N % 128 || up_off != N) : (N % 256)) return -1;
   if (lda % 8 || ldb % 8 || (glu ? ldc % 4 : ldc % 8)) return -1;
   if ((uintptr_t)a % 16 || (uintptr_t)b % 16 || (uintptr_t)c % (glu ? 8 : 16)) return -1;
@@ -955,17 +989,19 @@ int launch_gemm_w4_grouped(void* c, const void* a, const void* b, const int* grp
   p.tiles_m = (max_rows + 255) / 256;
   p.tiles_n = glu ? N / 128 : N / 256;
   p.splitk = 1;
-  p.kt_split = K / 64;
+  p.kt_split = K / 64 / ksplit;
   p.up_off = up_off;
   p.group_m = group_m < 1 ? 8 : group_m;
   p.krot = g_w4_krot;
   p.grp = grp;
   p.n_grp = n_grp;
   p.b_grp = b_grp;
+  p.ksplit = ksplit;
+  p.c_split = c_split;
   // the most row tiles n_grp groups of max_rows rows in total can make
-  const int64_t tiles = (int64_t)(p.tiles_m + n_grp - 1) * p.tiles_n;
+  const int64_t tiles = (int64_t)(p.tiles_m + n_grp - 1) * p.tiles_n * ksplit;
   int nwg = (int)(tiles < w4_num_cus() ? tiles : w4_num_cus());
-  nwg -= nwg & 7;  // whole XCD rounds (the per-XCD K rotation); surplus workgroups leave at once
+  nwg -= nwg & 7;  // whole XCD rounds; surplus workgroups leave at once
   if (nwg < 8) nwg = 8;
   switch (epi) {
     case W4_STORE: return w4_launch_grouped<W4_STORE>(p, nwg, st);
@@ -981,6 +1017,7 @@ int64_t gemm_w4_workspace_bytes(int64_t M, int64_t N, int splitk) {
 
 int configure_gemm_w4() {
   return w4_cfg<W4_STORE>() | w4_cfg<W4_RESIDUAL>() | w4_cfg<W4_SILU>() | w4_cfg<W4_GELU>() |
+         w4_cfg_one<W4_STORE, 104>() | w4_cfg_one<W4_SILU, 104>() | w4_cfg_one<W4_GELU, 104>() |
          w4_cfg_one<W4_STORE, 120>() | w4_cfg_one<W4_SILU, 120>() | w4_cfg_one<W4_GELU, 120>();
 }
 

@@ -120,6 +120,7 @@ int launch_skinny_norm_gemm(void* y, void* h_out, const void* x, const void* res
 // persistent + per-XCD K rotation); splitk > 1 (per-tile form) needs slab + counters (zeroed
 // once): 256 KiB of slab per tile and slice.
 void w4_set_krot(int k);
+void w4_set_grouped_rot(int r);
 int w4_krot();
 int launch_gemm_w4(void* c, const void* a, const void* b, const void* r, int M, int N, int K,
                    int lda, int ldb, int ldc, int ldr, int epi, int up_off, int splitk,
@@ -127,10 +128,12 @@ int launch_gemm_w4(void* c, const void* a, const void* b, const void* r, int M, 
                    int v, hipStream_t st);
 // Grouped persistent form: rows [grp[g], grp[g + 1]) of a / c (grp: n_grp + 1 row offsets in
 // DEVICE memory) times weight b + g * b_grp; epi 0 store or 2/3 gated; max_rows >= grp[n_grp]
-// sizes the grid.
+// sizes the grid.  ksplit > 1 (store only): K cut into ksplit slices, slice s written as bf16
+// partial products to c + s * c_split elements.
 int launch_gemm_w4_grouped(void* c, const void* a, const void* b, const int* grp, int n_grp,
                            int max_rows, int N, int K, int lda, int ldb, int ldc, int64_t b_grp,
-                           int epi, int up_off, int group_m, hipStream_t st);
+                           int epi, int up_off, int group_m, int ksplit, int64_t c_split,
+                           hipStream_t st);
 int64_t gemm_w4_workspace_bytes(int64_t M, int64_t N, int splitk);
 int configure_gemm_w4();
 

@@ -26,7 +26,8 @@ namespace drtc {
 
 constexpr int kMoeBM = 128;   // rows per tile
 constexpr int kMoeMaxK = 8;   // top-k bound
-constexpr int kMoeW4Rows = 1024;  // auto variant 4 from this many rows per expert
+constexpr int kMoeW4Rows = 256;  // auto variant 4 from this many rows per expert
+constexpr int kMoeW4SplitTiles = 256;  // variant 4: down split over K below this many tiles
 
 // ---------------------------------------------------------------- align
 __global__ __launch_bounds__(1024) void moe_align_kernel(
@@ -425,8 +426,9 @@ __global__ __launch_bounds__(256) void moe_gather_kernel(bf16_t* __restrict__ xs
 }
 
 __global__ __launch_bounds__(256) void moe_combine_kernel(
-    bf16_t* __restrict__ out, const bf16_t* __restrict__ zbuf, const float* __restrict__ topk_w,
-    const int* __restrict__ inv_pos, const int* __restrict__ local_range, int T, int H, int k) {
+    bf16_t* __restrict__ out, const bf16_t* __restrict__ zbuf, const bf16_t* __restrict__ zbuf2,
+    const float* __restrict__ topk_w, const int* __restrict__ inv_pos,
+    const int* __restrict__ local_range, int T, int H, int k) {
   const int t = blockIdx.x;
   const int lo = local_range[0], hi = local_range[1];
   for (int c = threadIdx.x * 8; c < H; c += 256 * 8) {
@@ -436,8 +438,14 @@ __global__ __launch_bounds__(256) void moe_combine_kernel(
       if (p < lo || p >= hi) continue;  // pair routed to another EP rank
       const float w = topk_w[t * k + j];
       const bf16x8 z = load_bf16x8(zbuf + (int64_t)p * H + c);
+      if (zbuf2 != nullptr) {  // down split over K: the two halves' partial products
+        const bf16x8 z2 = load_bf16x8(zbuf2 + (int64_t)p * H + c);
 #pragma unroll
-      for (int q = 0; q < 8; ++q) s[q] += w * bf2f(z[q]);
+        for (int q = 0; q < 8; ++q) s[q] += w * (bf2f(z[q]) + bf2f(z2[q]));
+      } else {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) s[q] += w * bf2f(z[q]);
+      }
     }
     bf16x8 o;
 #pragma unroll
@@ -480,8 +488,10 @@ int launch_moe(void* out, const void* x, const void* router_logits, const void* 
   // -1 = pick by rows per expert (scripts/moe_bench.py, Mixtral shapes)
   const int rows_e = P / e_local;
   const bool auto_v = variant < 0;
-  // variant 4 from ~1k rows per expert (Mixtral prefill chunks: gemm_w4's persistent 256 x 256
-  // tiles over expert-ordered rows, profiles/r6j), gemm_xd's grouped forms from ~a 96-row tile
+  // variant 4 from one 256-row tile per expert (gemm_w4's persistent 256 x 256 tiles over
+  // expert-ordered rows; Mixtral shapes, profiles/r6j: 770 / 917 / 1061 TF/s at T = 1024 /
+  // 2048 / 4096 against 703 / 841 / 1019 on variant 3), gemm_xd's grouped forms from ~a
+  // 96-row tile
   if (auto_v) variant = rows_e >= kMoeW4Rows ? 4 : (rows_e >= 96 ? 3 : 1);
   if (variant > 4) return -1;
   // variant 4: the persistent GEMM's prologue stages two K tiles; the down reduction is I
@@ -546,7 +556,13 @@ int launch_moe(void* out, const void* x, const void* router_logits, const void* 
   bf16_t* hbuf = (bf16_t*)(p + o); o = align(o + 2ll * P * I);
   bf16_t* zbuf = (bf16_t*)(p + o); o = align(o + 2ll * P * H);
   int* grp_off = (int*)(p + o); o = align(o + 4ll * (e_local + 1));
+  bf16_t* zbuf2 = (bf16_t*)(p + o); o = align(o + 2ll * P * H);  // (variant 4, split down)
   if (o > ws_bytes) return -2;
+  // variant 4: down split over K in two when its 256 x 256 tiles (rows spread evenly over the
+  // experts) would not fill the CUs once - one tile row per expert at Mixtral decode sizes
+  const int64_t dn_tiles = (int64_t)e_local * ((rows_e + 255) / 256) * (H / 256);
+  const bool dn_split = variant == 4 && dn_form == 0 && dn_tiles < kMoeW4SplitTiles &&
+                        (I / 64) % 2 == 0 && I / 128 >= 2;
   hipLaunchKernelGGL(moe_align_kernel, dim3(1), dim3(1024), 0, st, (const bf16_t*)router_logits, T,
                      E, k, sorted_tok, sorted_w, inv_pos, topk_w, t_e, t_r0, t_n, n_tiles, local_range,
                      max_tiles, e_off, e_local, bm, logit_ts, logit_es,
@@ -558,7 +574,7 @@ int launch_moe(void* out, const void* x, const void* router_logits, const void* 
     hipLaunchKernelGGL(moe_gather_kernel, dim3(min(P, 8192)), dim3(256), 0, st, xs,
                        (const bf16_t*)x, sorted_tok, local_range, P, H);
     int e = launch_gemm_w4_grouped(hbuf, xs, w_gu, grp_off, e_local, P, I, H, H, H, I,
-                                   2ll * I * H, 2 + act, I, 4, st);
+                                   2ll * I * H, 2 + act, I, 4, 1, 0, st);
     if (e) return e;
     if (dn_form) {
       // down on gemm_xd's grouped split-K forms over the 256-row tile table (few rows per
@@ -570,7 +586,8 @@ int launch_moe(void* out, const void* x, const void* router_logits, const void* 
                                  slab_bytes, counters, n_counters, st);
     } else {
       e = launch_gemm_w4_grouped(zbuf, hbuf, w_dn, grp_off, e_local, P, H, I, I, I, H,
-                                 (int64_t)H * I, 0, 0, 8, st);
+                                 (int64_t)H * I, 0, 0, 8, dn_split ? 2 : 1,
+                                 dn_split ? (int64_t)(zbuf2 - zbuf) : 0, st);
     }
     if (e) return e;
   } else if (variant == 3) {
@@ -609,8 +626,9 @@ int launch_moe(void* out, const void* x, const void* router_logits, const void* 
                        (const bf16_t*)hbuf, (const bf16_t*)w_dn, sorted_tok, t_e, t_r0, t_n,
                        n_tiles, I, H, I, H, max_tiles, 0);
   }
-  hipLaunchKernelGGL(moe_combine_kernel, dim3(T), dim3(256), 0, st, (bf16_t*)out, zbuf, topk_w,
-                     inv_pos, local_range, T, H, k);
+  hipLaunchKernelGGL(moe_combine_kernel, dim3(T), dim3(256), 0, st, (bf16_t*)out, zbuf,
+                     dn_split ? (const bf16_t*)zbuf2 : nullptr, topk_w, inv_pos, local_range, T, H,
+                     k);
   return (int)hipGetLastError();
 }
 
@@ -633,7 +651,7 @@ int64_t moe_workspace_bytes(int T, int H, int I, int e_local, int k) {
   const int64_t mt = (P + kMoeBM - 1) / kMoeBM + e_local;
   // (tile tables sized for the 128-row tiles: the largest count of any variant)
   return 4 * align(4 * P) + 3 * align(4 * mt) + align(4) + align(8) + align(2 * P * I) +
-         align(2 * P * H) + align(4 * (e_local + 1));
+         2 * align(2 * P * H) + align(4 * (e_local + 1));
 }
 
 }  // namespace drtc

@@ -605,26 +605,33 @@ def mfma_gemm(x: torch.Tensor, w: torch.Tensor, epi: str = "store",
 
 
 def mfma_gemm_grouped(x: torch.Tensor, w: torch.Tensor, grp: torch.Tensor, epi: str = "store",
-                      out: torch.Tensor | None = None, group_m: int = 0) -> torch.Tensor:
+                      out: torch.Tensor | None = None, group_m: int = 0,
+                      ksplit: int = 1) -> torch.Tensor:
     """Grouped persistent gemm_w4 (csrc/kernels/gemm_w4.hip, V & 64): for every group g,
     out[r] = epi(x[r] @ w[g].T) over the rows r in [grp[g], grp[g + 1]).
 
     x [R, K] bf16 (rows in group order); w [G, N, K] ("silu" / "gelu_tanh": [G, 2I, K] with
     the gate rows first); grp int32 [G + 1] on the device, non-decreasing, grp[G] <= R -
     read by the kernel, never by the host (a routing kernel writes it: no sync, graph-safe).
-    Rows outside [grp[0], grp[G]) of ``out`` are not written."""
+    Rows outside [grp[0], grp[G]) of ``out`` are not written.  ``ksplit`` > 1 ("store"): K is
+    cut into ksplit slices and out is [ksplit, R, N], slice s holding the bf16 partial product
+    over its K range (the consumer sums them; the MoE combine does)."""
     R, K = x.shape
     G_, n2, k2 = w.shape
     glu = epi in ("silu", "gelu_tanh")
     N = n2 // 2 if glu else n2
     assert k2 == K and w.is_contiguous() and x.stride(1) == 1 and x.dtype == torch.bfloat16
     assert grp.dtype == torch.int32 and grp.numel() == G_ + 1 and grp.device == x.device
+    shape = (ksplit, R, N) if ksplit > 1 else (R, N)
     if out is None:
-        out = torch.empty((R, N), dtype=x.dtype, device=x.device)
-    assert out.shape == (R, N) and out.stride(1) == 1
+        out = torch.empty(shape, dtype=x.dtype, device=x.device)
+    assert out.shape == shape and out.stride(-1) == 1
+    if ksplit > 1:
+        assert out.is_contiguous()
     check(hipk().gemm_grouped(out.data_ptr(), x.data_ptr(), w.data_ptr(), grp.data_ptr(), G_,
-                              R, N, K, x.stride(0), K, out.stride(0), n2 * K, EPI[epi],
-                              N if glu else 0, group_m or (4 if glu else 8), stream_ptr(x)),
+                              R, N, K, x.stride(0), K, out.stride(-2), n2 * K, EPI[epi],
+                              N if glu else 0, group_m or (4 if glu else 8), ksplit,
+                              R * N if ksplit > 1 else 0, stream_ptr(x)),
           "gemm_grouped")
     return out
 

@@ -21,16 +21,18 @@ import torch.nn.functional as F
 from ._ext import check, hipk, on_gpu, stream_ptr
 from .activation import ACTS, act_glu_ref
 
-# Largest token chunk per kernel call: bounds the workspace (P = chunk * k
-# rows of [I] and [H] intermediates) while keeping >10k workgroups per GEMM.
-MOE_CHUNK = int(os.environ.get("DRTC_MOE_CHUNK", "8192"))
+# Largest token chunk per kernel call: bounds the workspace (P = chunk * k rows of [I] and [H]
+# intermediates: 1.2 GB for Mixtral).  One Mixtral prefill step (~15k tokens) in one call:
+# 4k rows per expert on variant 4 (profiles/r6j: the 16k-token layer 8.94 ms in one chunk vs
+# 9.56 ms in two of 8192).
+MOE_CHUNK = int(os.environ.get("DRTC_MOE_CHUNK", "16384"))
 
 # Grouped-GEMM structure (csrc/kernels/moe.hip): 0 = 128-row two-barrier,
 # 1 = 128-row 3-stage pipeline, 2 = 256-row 3-stage pipeline, 3 = gemm_xd's grouped mode
 # (csrc/kernels/gemm_xd.hip: XCD-partitioned tiles, GLU epilogue, split-K, non-temporal
 # weights where an expert's rows fit one tile), 4 = token rows gathered into expert order, then
 # gemm_w4's grouped persistent 256 x 256 form (csrc/kernels/gemm_w4.hip; prefill-sized rows per
-# expert), -1 = by rows per expert (4 from 1024 rows per expert, 3 from 96).
+# expert), -1 = by rows per expert (4 from 256 rows per expert, 3 from 96).
 MOE_GEMM_VARIANT = int(os.environ.get("DRTC_MOE_VARIANT", "-1"))
 # gemm_xd forms of variant 3 (mt * 100 + nf * 10 + splitk, + 1000 non-temporal; 0 = by rows
 # per expert, csrc/kernels/moe.hip launch_moe)

@@ -60,7 +60,15 @@ def main():
                         group_m=G.w4_group_m(rows, I, H, glu=True))
             torch.matmul(he, wdn[e].t(), out=ye)
 
-    arms = {"fused_moe_v3": fused(3), "fused_moe_v4": fused(4), "dense_w4_x8": dense,
+    lib = __import__("drtc_amd.ops._ext", fromlist=["hipk"]).hipk()
+
+    def fused_rot():  # variant 4 with the per-XCD K rotation in the grouped GEMMs (A/B arm)
+        lib.w4_set_grouped_rot(1)
+        ops.fused_moe(x, lg, wgu, wdn, k, workspace=ws, out=out, variant=4)
+        lib.w4_set_grouped_rot(0)
+
+    arms = {"fused_moe_v3": fused(3), "fused_moe_v4": fused(4), "fused_moe_v4_rot": fused_rot,
+            "dense_w4_x8": dense,
             "dense_w4_gu_lib_down_x8": dense_lib_down}
     for f in arms.values():
         f()

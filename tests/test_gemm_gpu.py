@@ -587,6 +587,28 @@ def test_w4_grouped_matches_fp32(hipk, epi, sizes, N, K, r0):
     assert bool((out[:r0] == 7).all()) and bool((out[offs[-1]:] == 7).all())
 
 
+@pytest.mark.parametrize("ksplit", [2, 4])
+def test_w4_grouped_split_k_partials_sum_to_fp32(hipk, ksplit):
+    """Grouped form with K cut into slices (the MoE down at few rows per expert): the bf16
+    partial products of the slices sum to the fp32 product; a gated epilogue is refused."""
+    g = torch.Generator(device="cuda").manual_seed(11 + ksplit)
+    offs = [0, 300, 300, 812, 1000]
+    R, N, K = 1000, 512, 1024
+    x = torch.randn(R, K, device="cuda", dtype=torch.bfloat16, generator=g)
+    w = torch.randn(4, N, K, device="cuda", dtype=torch.bfloat16, generator=g) * 0.05
+    grp = torch.tensor(offs, dtype=torch.int32, device="cuda")
+    out = G.mfma_gemm_grouped(x, w, grp, "store", ksplit=ksplit)
+    assert out.shape == (ksplit, R, N)
+    tot = out.float().sum(0)
+    for e in range(4):
+        a, b = offs[e], offs[e + 1]
+        if b > a:
+            _check(tot[a:b], _ref(x[a:b], w[e], "store", None), tol=2e-2)
+    w2 = torch.randn(4, 2 * N, K, device="cuda", dtype=torch.bfloat16, generator=g)
+    with pytest.raises(RuntimeError):
+        G.mfma_gemm_grouped(x, w2, grp, "silu", ksplit=2)
+
+
 def test_w4_grouped_graph_replay_follows_device_offsets(hipk):
     """The group offsets are read on the device at run time: a captured launch replays with
     new offsets written into the same tensor (no host sync, no re-capture)."""
