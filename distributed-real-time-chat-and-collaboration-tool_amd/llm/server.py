@@ -326,9 +326,12 @@ def main(argv=None):
     ap.add_argument("--workers", type=int, default=None,
                     help="gRPC handler threads; each blocks on one generation (default: "
                          "max-batch x replicas + 16, so the engine batch can fill)")
-    ap.add_argument("--frontend", choices=("threads", "aio"), default="threads",
+    ap.add_argument("--frontend", choices=("threads", "aio"), default=None,
                     help="gRPC front-end: a handler thread per in-flight RPC, or grpc.aio "
-                         "coroutines on one event-loop thread")
+                         "coroutines on one event-loop thread (default: aio when the engines "
+                         "run in worker processes - 94.0-94.9 %% of the engine vs 92.5 %% with "
+                         "threads, 1,024 closed-loop clients, profiles/r6k, r6n - threads for "
+                         "--in-process, whose engine thread would share the GIL with the loop)")
     ap.add_argument("--serve", action="append", default=[],
                     metavar="FEATURE=MODEL[@GPUS][:tpN][:mem=F]",
                     help="host FEATURE (smart | summary | answer | suggest) on its own engine "
@@ -351,7 +354,8 @@ def main(argv=None):
             args.max_batch = default_max_batch(args.model, args.tp)
         backend = build_backend(args)
         workers = args.workers or args.max_batch * max(1, args.gpus) + 16
-    server = (serve_aio(backend, args.port) if args.frontend == "aio"
+    frontend = args.frontend or ("threads" if args.in_process else "aio")
+    server = (serve_aio(backend, args.port) if frontend == "aio"
               else serve(backend, args.port, workers))
     log.info("LLM server on port %d (backend=%s model=%s gpus=%d tp=%d)", args.port, args.backend,
              args.model, args.gpus, args.tp)

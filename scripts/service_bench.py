@@ -206,8 +206,9 @@ def main():
                     help="run the load clients in this many separate processes (0: threads here)")
     ap.add_argument("--model", default="llama-3-8b")
     ap.add_argument("--mode", choices=("direct", "raft"), default="direct")
-    ap.add_argument("--frontend", choices=("threads", "aio"), default="threads",
-                    help="LLM service front-end (llm/server.py --frontend)")
+    ap.add_argument("--frontend", choices=("threads", "aio"), default=None,
+                    help="LLM service front-end (llm/server.py --frontend; default as there: "
+                         "aio, threads for the in-process engine backend)")
     ap.add_argument("--in-process-nodes", action="store_true",
                     help="--mode raft: run the 3 Raft nodes in this process (default: one "
                          "process per node, as deployed)")
@@ -222,6 +223,8 @@ def main():
     fp = FeatureParams(ignore_eos=True)  # full 48-token budget per reply (random weights)
     port = free_port()
     backend, eng = build_backend(args)
+    if args.frontend is None:
+        args.frontend = "threads" if args.backend == "engine" else "aio"
     if args.frontend == "aio":
         llm_srv = serve_aio(backend, port=port, bind="127.0.0.1", params=fp)
     else:
