@@ -2,9 +2,9 @@
 // Static launch shapes (device-side tile table), so the whole MoE layer is
 // hipGraph-capturable - the decode step of Mixtral replays with no host sync.
 //
-//   moe_align_kernel      top-k over the router logits (+ softmax over the
-//                         selected logits), counting sort of the (token, slot)
-//                         pairs by expert, per-expert 128-row tile table.
+//   moe_route / offsets / scatter   top-k over the router logits (+ softmax over the
+//                         selected logits), stable counting sort of the (token, slot)
+//                         pairs by expert, per-expert row-tile table.
 //   moe_gate_up_kernel    grouped GEMM  H[p] = act(X[tok(p)] . Wg[e]^T) * (X[tok(p)] . Wu[e]^T)
 //                         with the gate|up activation fused in the epilogue: a
 //                         wave owns matching gate and up columns, so both MFMA
@@ -29,19 +29,27 @@ constexpr int kMoeMaxK = 8;   // top-k bound
 constexpr int kMoeW4Rows = 256;  // auto variant 4 from this many rows per expert
 constexpr int kMoeW4SplitTiles = 256;  // variant 4: down split over K below this many tiles
 
-// ---------------------------------------------------------------- align
-__global__ __launch_bounds__(1024) void moe_align_kernel(
-    const bf16_t* __restrict__ logits, int T, int E, int k,
-    int* __restrict__ sorted_tok, float* __restrict__ sorted_w,
-    int* __restrict__ inv_pos, float* __restrict__ topk_w,
-    int* __restrict__ tile_expert, int* __restrict__ tile_row0, int* __restrict__ tile_rows,
-    int* __restrict__ n_tiles, int* __restrict__ local_range, int max_tiles, int e_off,
-    int e_local, int bm, int lts, int les, int* __restrict__ grp_off) {
-  __shared__ int cnt[256], off[257], fill[256], toff[257];
+// ---------------------------------------------------------------- routing
+// Three passes over workgroups of 256 tokens (one workgroup for all T was 89 us at T = 8192,
+// profiles/r6j - 2 % of a Mixtral prefill MoE layer):
+//   moe_route_kernel    top-k of each token's logits (+ softmax over the selected k), and the
+//                       workgroup's per-expert pair counts;
+//   moe_offsets_kernel  one workgroup: expert offsets, the per-expert tile table, the expert
+//                       row groups (variant 4), and each (workgroup, expert)'s first position;
+//   moe_scatter_kernel  every pair to its position in expert order: within an expert, pairs of
+//                       lower workgroups first, then (slot j, token) order - a STABLE order, the
+//                       same for the same logits whatever the scheduling.
+constexpr int kMoeRouteWG = 256;
+
+__global__ __launch_bounds__(kMoeRouteWG) void moe_route_kernel(
+    const bf16_t* __restrict__ logits, int T, int E, int k, int lts, int les,
+    int* __restrict__ topi, float* __restrict__ topk_w, int* __restrict__ wg_cnt) {
+  __shared__ int hist[256];
   const int tid = threadIdx.x;
-  for (int e = tid; e < 256; e += 1024) { cnt[e] = 0; fill[e] = 0; }
+  for (int e = tid; e < E; e += kMoeRouteWG) hist[e] = 0;
   __syncthreads();
-  for (int t = tid; t < T; t += 1024) {
+  const int t = blockIdx.x * kMoeRouteWG + tid;
+  if (t < T) {
     // logit (t, e) at t * lts + e * les: [T, E] rows, or the router GEMM's [E, T] output read
     // in place (lts = 1: consecutive threads read consecutive tokens of one expert row)
     const bf16_t* lr = logits + (int64_t)t * lts;
@@ -70,10 +78,26 @@ __global__ __launch_bounds__(1024) void moe_align_kernel(
     for (int j = 0; j < kMoeMaxK; ++j) {
       if (j < k) {
         topk_w[t * k + j] = __expf(v[j] - v[0]) / s;
-        inv_pos[t * k + j] = id[j];  // expert id for now; position after the scatter
-        atomicAdd(&cnt[id[j]], 1);
+        topi[t * k + j] = id[j];
+        atomicAdd(&hist[id[j]], 1);  // a count: its order does not matter
       }
     }
+  }
+  __syncthreads();
+  for (int e = tid; e < E; e += kMoeRouteWG) wg_cnt[blockIdx.x * E + e] = hist[e];
+}
+
+__global__ __launch_bounds__(1024) void moe_offsets_kernel(
+    const int* __restrict__ wg_cnt, int G, int E, int* __restrict__ wg_base,
+    int* __restrict__ tile_expert, int* __restrict__ tile_row0, int* __restrict__ tile_rows,
+    int* __restrict__ n_tiles, int* __restrict__ local_range, int max_tiles, int e_off,
+    int e_local, int bm, int* __restrict__ grp_off) {
+  __shared__ int cnt[256], off[257], toff[257];
+  const int tid = threadIdx.x;
+  for (int e = tid; e < E; e += 1024) {
+    int c = 0;
+    for (int g = 0; g < G; ++g) c += wg_cnt[g * E + e];
+    cnt[e] = c;
   }
   __syncthreads();
   if (tid == 0) {
@@ -104,15 +128,50 @@ __global__ __launch_bounds__(1024) void moe_align_kernel(
         tile_rows[ti] = min(bm, cnt[e] - i * bm);
       }
     }
+    int b = off[e];
+    for (int g = 0; g < G; ++g) {
+      wg_base[g * E + e] = b;
+      b += wg_cnt[g * E + e];
+    }
   }
-  for (int t = tid; t < T; t += 1024) {
-    for (int j = 0; j < k; ++j) {
-      const int e = inv_pos[t * k + j];
-      const int p = off[e] + atomicAdd(&fill[e], 1);
+}
+
+__global__ __launch_bounds__(kMoeRouteWG) void moe_scatter_kernel(
+    const float* __restrict__ topk_w, const int* __restrict__ wg_base, int T, int E, int k,
+    int* __restrict__ sorted_tok, float* __restrict__ sorted_w, int* __restrict__ inv_pos) {
+  // inv_pos holds each pair's expert id (moe_route_kernel) and gets its position here
+  __shared__ int run[256];
+  __shared__ int wcnt[kMoeRouteWG / 64][256];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int t = blockIdx.x * kMoeRouteWG + tid;
+  const uint64_t below = (1ull << lane) - 1;
+  for (int e = tid; e < E; e += kMoeRouteWG) run[e] = 0;
+  __syncthreads();
+  for (int j = 0; j < k; ++j) {
+    const int e = t < T ? inv_pos[t * k + j] : -1;
+    int rank = 0;
+    for (int x = 0; x < E; ++x) {  // this wave's pairs of expert x, in lane order
+      const uint64_t m = __ballot(e == x);
+      if (e == x) rank = __popcll(m & below);
+      if (lane == 0) wcnt[w][x] = __popcll(m);
+    }
+    __syncthreads();
+    if (e >= 0) {
+      int r = run[e] + rank;
+      for (int w2 = 0; w2 < w; ++w2) r += wcnt[w2][e];
+      const int p = wg_base[blockIdx.x * E + e] + r;
       sorted_tok[p] = t;
       sorted_w[p] = topk_w[t * k + j];
       inv_pos[t * k + j] = p;
     }
+    __syncthreads();
+    for (int x = tid; x < E; x += kMoeRouteWG) {
+      int c = 0;
+#pragma unroll
+      for (int w2 = 0; w2 < kMoeRouteWG / 64; ++w2) c += wcnt[w2][x];
+      run[x] += c;
+    }
+    __syncthreads();
   }
 }
 
@@ -557,16 +616,23 @@ int launch_moe(void* out, const void* x, const void* router_logits, const void* 
   bf16_t* zbuf = (bf16_t*)(p + o); o = align(o + 2ll * P * H);
   int* grp_off = (int*)(p + o); o = align(o + 4ll * (e_local + 1));
   bf16_t* zbuf2 = (bf16_t*)(p + o); o = align(o + 2ll * P * H);  // (variant 4, split down)
+  const int G = (T + kMoeRouteWG - 1) / kMoeRouteWG;
+  int* wg_cnt = (int*)(p + o); o = align(o + 4ll * G * E);
+  int* wg_base = (int*)(p + o); o = align(o + 4ll * G * E);
   if (o > ws_bytes) return -2;
   // variant 4: down split over K in two when its 256 x 256 tiles (rows spread evenly over the
   // experts) would not fill the CUs once - one tile row per expert at Mixtral decode sizes
   const int64_t dn_tiles = (int64_t)e_local * ((rows_e + 255) / 256) * (H / 256);
   const bool dn_split = variant == 4 && dn_form == 0 && dn_tiles < kMoeW4SplitTiles &&
                         (I / 64) % 2 == 0 && I / 128 >= 2;
-  hipLaunchKernelGGL(moe_align_kernel, dim3(1), dim3(1024), 0, st, (const bf16_t*)router_logits, T,
-                     E, k, sorted_tok, sorted_w, inv_pos, topk_w, t_e, t_r0, t_n, n_tiles, local_range,
-                     max_tiles, e_off, e_local, bm, logit_ts, logit_es,
+  hipLaunchKernelGGL(moe_route_kernel, dim3(G), dim3(kMoeRouteWG), 0, st,
+                     (const bf16_t*)router_logits, T, E, k, logit_ts, logit_es, inv_pos, topk_w,
+                     wg_cnt);
+  hipLaunchKernelGGL(moe_offsets_kernel, dim3(1), dim3(1024), 0, st, (const int*)wg_cnt, G, E,
+                     wg_base, t_e, t_r0, t_n, n_tiles, local_range, max_tiles, e_off, e_local, bm,
                      variant == 4 ? grp_off : (int*)nullptr);
+  hipLaunchKernelGGL(moe_scatter_kernel, dim3(G), dim3(kMoeRouteWG), 0, st, (const float*)topk_w,
+                     (const int*)wg_base, T, E, k, sorted_tok, sorted_w, inv_pos);
   const dim3 g_gu((I / 64) * max_tiles), g_dn((H / 128) * max_tiles);
   if (variant == 4) {
     // xs (expert-ordered token rows) lives in zbuf: gate_up consumes it before down writes Z
@@ -650,8 +716,10 @@ int64_t moe_workspace_bytes(int T, int H, int I, int e_local, int k) {
   const int64_t P = (int64_t)T * k;
   const int64_t mt = (P + kMoeBM - 1) / kMoeBM + e_local;
   // (tile tables sized for the 128-row tiles: the largest count of any variant)
+  // (routing: per-workgroup counts and bases for up to 256 experts)
+  const int64_t G = (T + kMoeRouteWG - 1) / kMoeRouteWG;
   return 4 * align(4 * P) + 3 * align(4 * mt) + align(4) + align(8) + align(2 * P * I) +
-         2 * align(2 * P * H) + align(4 * (e_local + 1));
+         2 * align(2 * P * H) + align(4 * (e_local + 1)) + 2 * align(4 * G * 256);
 }
 
 }  // namespace drtc

@@ -551,7 +551,8 @@ def _moe_inputs(T, H, I, E, seed=0):
 
 @pytest.mark.parametrize("T,H,I,E,k", [(1, 256, 128, 4, 2), (37, 256, 192, 4, 2),
                                         (300, 4096, 1792, 8, 2), (1000, 512, 256, 16, 4),
-                                        (129, 256, 64, 8, 8)])
+                                        (129, 256, 64, 8, 8),
+                                        (700, 256, 128, 160, 2)])  # 3 routing workgroups, E > 64
 @pytest.mark.parametrize("act", ["silu", "gelu_tanh"])
 @pytest.mark.parametrize("variant", [0, 1, 2, -1])
 def test_fused_moe(hipk, T, H, I, E, k, act, variant):
