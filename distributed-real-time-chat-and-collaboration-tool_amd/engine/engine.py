@@ -78,8 +78,11 @@ class LLMEngine:
         self.max_prefill_tokens = max_prefill_tokens
         # prefill launch granularity: GEMMs stay at full efficiency from ~16k
         # rows; measured on the headline batch (one MI355X), 16k / 32k / 64k
-        # chunks: equal tok/s, p50 TTFT 0.85 / 1.02 / 1.37 s
-        self.prefill_chunk_tokens = int(os.environ.get("DRTC_PREFILL_CHUNK", "16384"))
+        # chunks: equal tok/s, p50 TTFT 0.85 / 1.02 / 1.37 s.  Per model
+        # (ModelConfig.prefill_chunk): Mixtral 32k (the MoE layers' rows per expert),
+        # Llama-3-70B 36k (one step per ask wave), profiles/r6t
+        self.prefill_chunk_tokens = int(os.environ.get(
+            "DRTC_PREFILL_CHUNK", str(getattr(cfg, "prefill_chunk", 16384))))
         self.max_blocks = math.ceil(self.max_model_len / BS)
         # hbm_budget: the fraction of the GPU's HBM this engine may hold (engine groups that
         # share a GPU, llm.server --serve ...:mem=F); every TP / EP rank gets the same

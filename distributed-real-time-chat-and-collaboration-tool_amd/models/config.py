@@ -37,6 +37,7 @@ class ModelConfig:
     eos_token_id: int = 2
     init_std: float = 0.02
     query_pre_attn_scalar: float | None = None
+    prefill_chunk: int = 16384       # engine prefill step, tokens (LLMEngine.prefill_chunk_tokens)
 
     @property
     def q_size(self) -> int:
@@ -77,7 +78,8 @@ LLAMA3_8B = ModelConfig(
 LLAMA3_70B = ModelConfig(
     name="llama-3-70b", vocab_size=128256, hidden_size=8192, intermediate_size=28672,
     num_layers=80, num_heads=64, num_kv_heads=8, head_dim=128, rope_theta=500000.0,
-    rms_eps=1e-5, max_position=8192, bos_token_id=128000, eos_token_id=128001)
+    rms_eps=1e-5, max_position=8192, bos_token_id=128000, eos_token_id=128001,
+    prefill_chunk=36864)  # a whole ask wave (256 x ~136 tokens) in one step, profiles/r6t
 
 GEMMA_2B = ModelConfig(
     name="gemma-2b", vocab_size=256000, hidden_size=2048, intermediate_size=16384,
@@ -89,7 +91,8 @@ MIXTRAL_8X7B = ModelConfig(
     name="mixtral-8x7b", vocab_size=32000, hidden_size=4096, intermediate_size=14336,
     num_layers=32, num_heads=32, num_kv_heads=8, head_dim=128, rope_theta=1e6,
     rms_eps=1e-5, max_position=32768, num_experts=8, experts_per_token=2,
-    bos_token_id=1, eos_token_id=2)
+    bos_token_id=1, eos_token_id=2,
+    prefill_chunk=32768)  # 8k rows per expert in the prefill MoE GEMMs, profiles/r6t
 
 # Tiny shapes with the same structural features, for CPU tests and smoke runs.
 TINY_LLAMA = ModelConfig(

@@ -22,10 +22,11 @@ from ._ext import check, hipk, on_gpu, stream_ptr
 from .activation import ACTS, act_glu_ref
 
 # Largest token chunk per kernel call: bounds the workspace (P = chunk * k rows of [I] and [H]
-# intermediates: 1.2 GB for Mixtral).  One Mixtral prefill step (~15k tokens) in one call:
-# 4k rows per expert on variant 4 (profiles/r6j: the 16k-token layer 8.94 ms in one chunk vs
-# 9.56 ms in two of 8192).
-MOE_CHUNK = int(os.environ.get("DRTC_MOE_CHUNK", "16384"))
+# intermediates: ~3 GB for Mixtral).  One Mixtral prefill step (ModelConfig.prefill_chunk,
+# 32k tokens) in one call: 8k rows per expert on variant 4 (profiles/r6j: the 16k-token layer
+# 8.94 ms in one call vs 9.56 ms in two of 8192; profiles/r6t: the batch-1024 wave +1.6 % with
+# 32k-token prefill steps and MoE calls).
+MOE_CHUNK = int(os.environ.get("DRTC_MOE_CHUNK", "32768"))
 
 # Grouped-GEMM structure (csrc/kernels/moe.hip): 0 = 128-row two-barrier,
 # 1 = 128-row 3-stage pipeline, 2 = 256-row 3-stage pipeline, 3 = gemm_xd's grouped mode
