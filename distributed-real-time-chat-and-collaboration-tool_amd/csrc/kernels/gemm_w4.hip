@@ -553,12 +553,25 @@ DRTC_DEVICE void w4_tile_of(const W4Params& p, int tt, int& tm, int& tn) {
   w4_tile_mn(p.tiles_m, p.tiles_n, p.group_m, tt, tm, tn);
 }
 
+// Rows [r0, r1) of group e, clamped to [0, M] and to the previous group's end (prev, carried
+// by the caller's walk over the groups): offsets written by another kernel can never make the
+// launch touch rows outside the operands it was sized for, nor two groups write one row.
+DRTC_DEVICE void w4_grp_rows(const W4Params& p, int e, int& prev, int& r0, int& r1) {
+  r0 = max(min(max(p.grp[e], 0), p.M), prev);
+  r1 = max(min(p.grp[e + 1], p.M), r0);
+  prev = r1;
+}
+
 // Tiles of the launch: tiles_m x tiles_n, or (grouped) the sum over the row groups.
 template <int V>
 DRTC_DEVICE int w4_ntiles(const W4Params& p) {
   if constexpr ((V & 64) != 0) {
-    int n = 0;
-    for (int e = 0; e < p.n_grp; ++e) n += (p.grp[e + 1] - p.grp[e] + 255) >> 8;
+    int n = 0, prev = 0;
+    for (int e = 0; e < p.n_grp; ++e) {
+      int r0, r1;
+      w4_grp_rows(p, e, prev, r0, r1);
+      n += (r1 - r0 + 255) >> 8;
+    }
     return n * p.tiles_n * p.ksplit;
   } else {
     return p.tiles_m * p.tiles_n;
@@ -571,9 +584,10 @@ template <int V>
 DRTC_DEVICE W4Pos w4_pos_of(const W4Params& p, int tt) {
   W4Pos q;
   if constexpr ((V & 64) != 0) {
-    int base = 0;
+    int base = 0, prev = 0;
     for (int e = 0; e < p.n_grp; ++e) {
-      const int r0 = p.grp[e], r1 = p.grp[e + 1];
+      int r0, r1;
+      w4_grp_rows(p, e, prev, r0, r1);
       const int tme = (r1 - r0 + 255) >> 8, ns = tme * p.tiles_n, nt = ns * p.ksplit;
       if (tt < base + nt) {
         const int s = (tt - base) / ns;  // K slice

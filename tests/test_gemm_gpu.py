@@ -609,6 +609,21 @@ def test_w4_grouped_split_k_partials_sum_to_fp32(hipk, ksplit):
         G.mfma_gemm_grouped(x, w2, grp, "silu", ksplit=2)
 
 
+def test_w4_grouped_clamps_offsets_to_the_operands(hipk):
+    """Device offsets past the rows the launch was sized for (or decreasing) are clamped: the
+    kernel never reads or writes outside its operands."""
+    g = torch.Generator(device="cuda").manual_seed(5)
+    R, N, K = 600, 256, 256
+    x = torch.randn(R, K, device="cuda", dtype=torch.bfloat16, generator=g)
+    w = torch.randn(3, N, K, device="cuda", dtype=torch.bfloat16, generator=g) * 0.05
+    grp = torch.tensor([-5, 400, 300, 10 ** 6], dtype=torch.int32, device="cuda")
+    out = torch.full((R, N), 7.0, device="cuda", dtype=torch.bfloat16)
+    G.mfma_gemm_grouped(x, w, grp, "store", out=out)
+    torch.cuda.synchronize()
+    _check(out[:400], _ref(x[:400], w[0], "store", None))     # group 0: rows [0, 400)
+    _check(out[400:], _ref(x[400:], w[2], "store", None))     # group 1 empty, group 2 [400, 600)
+
+
 def test_w4_grouped_graph_replay_follows_device_offsets(hipk):
     """The group offsets are read on the device at run time: a captured launch replays with
     new offsets written into the same tensor (no host sync, no re-capture)."""
