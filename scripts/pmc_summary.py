@@ -1,8 +1,11 @@
 import csv, sys, collections, re
 def short(n):
     if 'gemm_xd' in n:
-        m=re.search(r'XdCfg<(\d), (\d), (\d), (\d)>', n); return 'xd%s%s%s'%(m.group(1),m.group(2),m.group(4))
-    if 'gemm_w4' in n: return 'w4'
+        m=re.search(r'XdCfg<([^>]*)>\s*,\s*(\d+)', n)
+        return 'xd<%s> epi %s' % (m.group(1), m.group(2)) if m else 'xd'
+    if 'gemm_w4' in n:
+        m=re.search(r'gemm_w4_kernel<(\d+), (\d+)>', n)
+        return 'w4 epi %s v%s' % m.groups() if m else 'w4'
     if 'gemm_ring' in n: return 'ring'
     if 'ingest_kernel' in n:
         m=re.search(r'ingest_kernel<(\d+), (\d+), (\d+), (\d+)>', n)
