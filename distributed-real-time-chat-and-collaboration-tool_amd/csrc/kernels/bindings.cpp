@@ -127,6 +127,7 @@ PYBIND11_MODULE(_hipk, m) {
   m.def("set_splitk_spin_limit", &drtc::set_splitk_spin_limit);
   m.def("gemm_workspace_bytes", &drtc::gemm_w4_workspace_bytes);
   m.def("moe_workspace_bytes", &drtc::moe_workspace_bytes);
+  m.def("moe_set_w4_group_m", [](int gu, int dn) { drtc::moe_set_w4_group_m(gu, dn); });
   m.def("ep_plan", [](u64 topi, int npairs, int e_local, int world, int cap, u64 dst_row,
                       u64 send_pair, u64 send_e, u64 overflow, u64 st) {
     return drtc::launch_ep_plan(P<const int>(topi), npairs, e_local, world, cap, P<int>(dst_row),

@@ -62,6 +62,7 @@ int launch_moe(void* out, const void* x, const void* router_logits, const void* 
                void* slab, int64_t slab_bytes, int* counters, int n_counters, int logit_ts,
                int logit_es, hipStream_t st);
 int64_t moe_workspace_bytes(int T, int H, int I, int e_local, int k);
+void moe_set_w4_group_m(int gu, int dn);  // variant 4 tile-order row groups (A/B knob)
 // Expert-parallel dispatch / combine with a static per-destination capacity (moe_ep.hip).
 int launch_ep_plan(const int* topi, int P, int e_local, int world, int cap, int* dst_row,
                    int* send_pair, int* send_e, int* overflow, hipStream_t st);

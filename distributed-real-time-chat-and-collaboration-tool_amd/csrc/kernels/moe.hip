@@ -28,6 +28,12 @@ constexpr int kMoeBM = 128;   // rows per tile
 constexpr int kMoeMaxK = 8;   // top-k bound
 constexpr int kMoeW4Rows = 256;  // auto variant 4 from this many rows per expert
 constexpr int kMoeW4SplitTiles = 256;  // variant 4: down split over K below this many tiles
+// variant 4 row-tile groups of the grouped gemm_w4 tile order (gate_up, down): A/B knob
+static int g_moe_gm_gu = 4, g_moe_gm_dn = 8;
+void moe_set_w4_group_m(int gu, int dn) {
+  g_moe_gm_gu = gu > 0 ? gu : 4;
+  g_moe_gm_dn = dn > 0 ? dn : 8;
+}
 
 // ---------------------------------------------------------------- routing
 // Three passes over workgroups of 256 tokens (one workgroup for all T was 89 us at T = 8192,
@@ -640,7 +646,7 @@ int launch_moe(void* out, const void* x, const void* router_logits, const void* 
     hipLaunchKernelGGL(moe_gather_kernel, dim3(min(P, 8192)), dim3(256), 0, st, xs,
                        (const bf16_t*)x, sorted_tok, local_range, P, H);
     int e = launch_gemm_w4_grouped(hbuf, xs, w_gu, grp_off, e_local, P, I, H, H, H, I,
-                                   2ll * I * H, 2 + act, I, 4, 1, 0, st);
+                                   2ll * I * H, 2 + act, I, g_moe_gm_gu, 1, 0, st);
     if (e) return e;
     if (dn_form) {
       // down on gemm_xd's grouped split-K forms over the 256-row tile table (few rows per
@@ -652,7 +658,7 @@ int launch_moe(void* out, const void* x, const void* router_logits, const void* 
                                  slab_bytes, counters, n_counters, st);
     } else {
       e = launch_gemm_w4_grouped(zbuf, hbuf, w_dn, grp_off, e_local, P, H, I, I, I, H,
-                                 (int64_t)H * I, 0, 0, 8, dn_split ? 2 : 1,
+                                 (int64_t)H * I, 0, 0, g_moe_gm_dn, dn_split ? 2 : 1,
                                  dn_split ? (int64_t)(zbuf2 - zbuf) : 0, st);
     }
     if (e) return e;

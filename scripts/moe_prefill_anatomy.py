@@ -67,7 +67,17 @@ def main():
         ops.fused_moe(x, lg, wgu, wdn, k, workspace=ws, out=out, variant=4)
         lib.w4_set_grouped_rot(0)
 
+    def fused_gm(gu, dn):  # variant 4 with other row groups in the grouped tile order
+        def f():
+            lib.moe_set_w4_group_m(gu, dn)
+            ops.fused_moe(x, lg, wgu, wdn, k, workspace=ws, out=out, variant=4)
+            lib.moe_set_w4_group_m(0, 0)
+        return f
+
+    gms = [tuple(int(v) for v in a.split("/")) for a in
+           __import__("os").environ.get("MOE_GM_ARMS", "").split(",") if a]
     arms = {"fused_moe_v3": fused(3), "fused_moe_v4": fused(4), "fused_moe_v4_rot": fused_rot,
+            **{f"fused_moe_v4_gm{gu}/{dn}": fused_gm(gu, dn) for gu, dn in gms},
             "dense_w4_x8": dense,
             "dense_w4_gu_lib_down_x8": dense_lib_down}
     for f in arms.values():
