@@ -565,8 +565,10 @@ int launch_moe(void* out, const void* x, const void* router_logits, const void* 
     variant = 3;
   }
   // variant 4 with dn_form: down on a 256-row gemm_xd grouped form (the tile table's rows)
-  if (variant == 4 && dn_form && ((dn_form % 1000) / 100 != 2 || !moe_xd_ok(dn_form, H, I, false)))
-    return -1;
+  if (variant == 4 && dn_form && ((dn_form % 1000) / 100 != 2 || !moe_xd_ok(dn_form, H, I, false))) {
+    if (!auto_v) return -1;
+    variant = 3;  // a down form requested for variant 3 (DRTC_MOE_DN_FORM) keeps its variant
+  }
   if (variant == 3) {
     // 256-row tiles from ~1.5 tiles of rows per expert, else 128-row; 256 gated columns
     // (128 outputs) for gate_up where I allows; down with split-K 2 while the grid is below

@@ -10,6 +10,7 @@ def short(n):
     if 'ingest_kernel' in n:
         m=re.search(r'ingest_kernel<(\d+), (\d+), (\d+), (\d+)>', n)
         return 'ingest S%s W%s %sx%s' % m.groups() if m else n[:40]
+    if 'paged_decode_persist' in n: return 'decode_attn_persist'
     if 'Cijk' in n: return 'lib:'+n[:40]
     return n[:30]
 agg=collections.defaultdict(lambda: collections.defaultdict(float)); cnt=collections.Counter()
