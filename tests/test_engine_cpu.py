@@ -567,3 +567,29 @@ def test_mixed_admission_gathers_arrivals():
     assert st["mixed_steps"] == 1, dict(st)  # the whole burst admitted together
     _, st0 = run(0)
     assert st0["mixed_steps"] > 1
+
+
+def test_prefill_step_comes_from_the_model_config(monkeypatch):
+    """LLMEngine's prefill step is the model's ``prefill_chunk`` (Mixtral 32k, Llama-3-70B 36k,
+    others 16k; profiles/r6t) unless DRTC_PREFILL_CHUNK overrides it; a small step splits a
+    batch into several prefill launches with the same greedy outputs."""
+    import dataclasses
+
+    assert (LLAMA3_8B.prefill_chunk, MIXTRAL_8X7B.prefill_chunk, LLAMA3_70B.prefill_chunk) == \
+        (16384, 32768, 36864)
+    monkeypatch.delenv("DRTC_PREFILL_CHUNK", raising=False)
+    prompts = [list(range(1, 30 + 7 * i)) for i in range(4)]
+    outs = {}
+    for chunk in (16384, 40):
+        cfg = dataclasses.replace(TINY_LLAMA, prefill_chunk=chunk)
+        m = TransformerLM(cfg, "cpu", seed=3)
+        eng = LLMEngine(m, max_batch=4, max_model_len=256, num_blocks=64, use_graphs=False)
+        assert eng.prefill_chunk_tokens == chunk
+        reqs = eng.generate(prompts, SamplingParams.greedy(6, ignore_eos=True))
+        outs[chunk] = [r.output_ids for r in reqs]
+        assert eng.stats["prefill_steps"] == (1 if chunk > 1000 else 4)
+    assert outs[16384] == outs[40]
+    monkeypatch.setenv("DRTC_PREFILL_CHUNK", "96")
+    eng = LLMEngine(TransformerLM(TINY_LLAMA, "cpu", seed=3), max_batch=4, max_model_len=256,
+                    num_blocks=64, use_graphs=False)
+    assert eng.prefill_chunk_tokens == 96
