@@ -103,6 +103,12 @@ def _activate() -> dict:
                     if _prefill_enabled:
                         pre.setdefault((N, K, ldx), []).append(
                             (M, int(e["algo"]), bool(e.get("beta0")), bool(e.get("beta1"))))
+                    if not e.get("xd"):
+                        continue
+                    # a prefill-table shape that is also a decode batch above the buckets
+                    # (Gemma-2B's 2048 rows) with a measured gemm_xd winner: the gemm_xd form
+                    # only (its library algo stays with the prefill table)
+                    tab[(M, N, K, ldx)] = (-1, 0, 0, int(e["xd"]), 0)
                     continue
                 nt_tuned = bool(e.get("nt_tuned"))
                 tab[(M, N, K, ldx)] = (int(e.get("algo", -1)), int(e.get("skinny", 0)),
@@ -199,6 +205,10 @@ def _prefill_algo(M: int, N: int, K: int, ldx: int, beta: int) -> int:
 def _resolve(M: int, N: int, K: int, ldx: int) -> tuple[str, int]:
     tab = _activate()
     ent = tab.get((M, N, K, ldx))
+    if M > DECODE_MAX_M and ent is not None and _xd_big_m and ent[3] and xd_supported(M, N, K, ent[3]):
+        # a decode batch above the 1024 buckets with a measured gemm_xd winner (Gemma-2B's
+        # 2048: qkv / o / down, profiles/r6ak)
+        return ("xd", ent[3])
     if M > DECODE_MAX_M and ent is not None and ent[0] >= 0:
         # a decode batch above the 1024 buckets that was tuned as such (Gemma-2B's 2048)
         with _lock:
@@ -228,6 +238,10 @@ def _resolve(M: int, N: int, K: int, ldx: int) -> tuple[str, int]:
                 return ("lt", algo)
     v = skinny_variant(M, N, K, ldx)
     return ("skinny", v) if v else ("torch", 0)
+
+
+# DRTC_XD_BIG_M=0: decode batches above DECODE_MAX_M ignore tuned gemm_xd entries (A/B knob)
+_xd_big_m = os.environ.get("DRTC_XD_BIG_M", "1") != "0"
 
 
 def route(M: int, N: int, K: int, ldx: int) -> tuple[str, int]:

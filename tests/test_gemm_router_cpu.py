@@ -74,3 +74,19 @@ def test_every_tuned_xd_form_fits_its_shape():
                 assert N % 2 == 0
                 assert G.xd_supported(M, N // 2, K, e["xd_glu"], glu=True), (key, e["xd_glu"])
     assert n > 100
+
+
+def test_gemma_2048_decode_shapes_carry_a_gemm_xd_form():
+    """Gemma-2B's 2,048-row decode batch (above the 1,024 decode buckets): the tuned table
+    gives its qkv / o / down shapes a gemm_xd form next to their prefill library entries
+    (profiles/r6ak), and every such form fits its shape."""
+    tab = json.load(open(G.table_path()))
+    for ver, ents in tab.items():
+        for k, want in (("2048,2560,2048,2048", 241), ("2048,2048,2048,2048", 141),
+                        ("2048,2048,16384,16384", 242)):
+            e = ents.get(k)
+            if e is None:
+                continue
+            assert e.get("prefill") and e["xd"] == want
+            M, N, K, _ = (int(v) for v in k.split(","))
+            assert G.xd_supported(M, N, K, want)
